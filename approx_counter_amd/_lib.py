@@ -1,0 +1,87 @@
+"""ctypes binding of include/approx_counter_amd.h.
+
+The shared library is built in-tree (``make`` at the repo root) into
+``approx_counter_amd/lib/libapprox_counter_amd.so``.  There is deliberately no
+fallback: if the library is missing, importing the binding raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libapprox_counter_amd.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "approx_counter_amd.h")
+
+AC_OK, AC_ERR_INVALID, AC_ERR_DEVICE, AC_ERR_NOMEM, AC_ERR_INTERNAL = 0, 1, 2, 3, 4
+AC_MAX_SEGS = 4
+
+p32 = ctypes.POINTER(ctypes.c_uint32)
+p64 = ctypes.POINTER(ctypes.c_uint64)
+p8 = ctypes.POINTER(ctypes.c_uint8)
+
+
+class ACWindows(ctypes.Structure):
+    _fields_ = [("codes", p32), ("nmask", p32), ("start", p64), ("length", p32),
+                ("n_windows", ctypes.c_uint32), ("n_bases", ctypes.c_uint64)]
+
+
+class ACSegment(ctypes.Structure):
+    _fields_ = [("kmers", p64), ("n_kmers", ctypes.c_uint32), ("sample", ACWindows),
+                ("counts", p32)]
+
+
+class ApproxCounterError(RuntimeError):
+    def __init__(self, status: int, message: str):
+        super().__init__(f"[ac_status {status}] {message}")
+        self.status = status
+
+
+_lib = None
+
+
+def load():
+    """Load the in-tree library (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} not found: build it with `make` (hipcc, gfx950)")
+    L = ctypes.CDLL(LIB_PATH)
+    vp = ctypes.c_void_p
+    L.ac_abi_version.restype = ctypes.c_int
+    L.ac_last_error.argtypes = [vp]
+    L.ac_last_error.restype = ctypes.c_char_p
+    L.ac_create.argtypes = [ctypes.POINTER(vp), ctypes.c_int]
+    L.ac_create.restype = ctypes.c_int
+    L.ac_destroy.argtypes = [vp]
+    L.ac_destroy.restype = None
+    L.ac_error_count.argtypes = [vp, ctypes.c_uint32, p64, ctypes.c_uint32,
+                                 ctypes.POINTER(ACWindows), p64]
+    L.ac_error_count.restype = ctypes.c_int
+    for fn in (L.ac_error_count_device, L.ac_error_count_device_accumulate):
+        fn.argtypes = [vp, ctypes.c_uint32, ctypes.POINTER(ACSegment), ctypes.c_uint32, vp]
+        fn.restype = ctypes.c_int
+    L.ac_image_bases.argtypes = [p32, ctypes.c_uint32]
+    L.ac_image_bases.restype = ctypes.c_uint64
+    L.ac_pack_windows.argtypes = [p8, p64, p32, ctypes.c_uint32, p32, p32, p64, p32,
+                                  ctypes.c_uint64]
+    L.ac_pack_windows.restype = ctypes.c_int
+    L.ac_last_launch.argtypes = [vp, p64, p32, p32]
+    L.ac_last_launch.restype = ctypes.c_int
+    _lib = L
+    return L
+
+
+def header_functions():
+    """Names of the functions declared in include/approx_counter_amd.h."""
+    text = open(HEADER_PATH).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(ac_[a-z_]+)\s*\(", text)))
+
+
+def check(status: int, ctx=None) -> None:
+    if status != AC_OK:
+        msg = load().ac_last_error(ctx)
+        raise ApproxCounterError(status, msg.decode() if msg else "unknown error")

@@ -1,0 +1,195 @@
+"""Host-side mirror of the reference's approximate-count interface.
+
+``error_count(sequences, exact_count, nb_thread, k, v)`` has the argument
+meaning of ``errorCount`` (approx_counter.cpp:531): ``sequences`` is the
+sampled window set, ``exact_count`` the (k-mer, exact count) pairs kept by
+get_most_frequent / get_solid_kmers (887-899), and the result maps every
+candidate k-mer to its approximate count (``results[kmer] = total``, 596).
+``nb_thread`` and ``v`` are accepted for signature parity; the work runs on the
+GPU through the C ABI of include/approx_counter_amd.h.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import ACSegment, ACWindows, check
+
+_DNA5 = np.full(256, 4, dtype=np.uint8)
+for _c, _v in ((b"A", 0), (b"C", 1), (b"G", 2), (b"T", 3), (b"U", 3)):
+    _DNA5[_c[0]] = _v
+    _DNA5[_c.lower()[0]] = _v
+
+
+def to_dna5(seq) -> np.ndarray:
+    """Dna5 ordinal bytes (A0 C1 G2 T3, anything else 4), as SeqAn's Dna5String."""
+    if isinstance(seq, np.ndarray):
+        return np.ascontiguousarray(seq, dtype=np.uint8)
+    if isinstance(seq, str):
+        seq = seq.encode()
+    return _DNA5[np.frombuffer(bytes(seq), dtype=np.uint8)]
+
+
+def _ptr(a, t):
+    return a.ctypes.data_as(ctypes.POINTER(t))
+
+
+class PackedSample:
+    """Host window image (see ac_windows in include/approx_counter_amd.h)."""
+
+    def __init__(self, codes, nmask, start, length, n_bases):
+        self.codes, self.nmask, self.start, self.length = codes, nmask, start, length
+        self.n_bases = int(n_bases)
+
+    @property
+    def n_windows(self) -> int:
+        return int(self.length.size)
+
+    @property
+    def total_bases(self) -> int:
+        return int(self.length.sum(dtype=np.uint64))
+
+    def as_struct(self) -> ACWindows:
+        return ACWindows(_ptr(self.codes, ctypes.c_uint32), _ptr(self.nmask, ctypes.c_uint32),
+                         _ptr(self.start, ctypes.c_uint64), _ptr(self.length, ctypes.c_uint32),
+                         self.n_windows, self.n_bases)
+
+
+def pack_windows(windows) -> PackedSample:
+    """Pack Dna5 windows into the 2-bit + N-mask image with ac_pack_windows."""
+    L = _lib.load()
+    arrs = [to_dna5(w) for w in windows]
+    lengths = np.array([a.size for a in arrs], dtype=np.uint32)
+    starts = np.zeros(len(arrs), dtype=np.uint64)
+    if len(arrs) > 1:
+        starts[1:] = np.cumsum(lengths[:-1], dtype=np.uint64)
+    flat = np.concatenate(arrs) if arrs and lengths.sum() else np.zeros(1, np.uint8)
+    flat = np.ascontiguousarray(flat, dtype=np.uint8)
+    lens_c = lengths if lengths.size else np.zeros(1, np.uint32)
+    n_bases = int(L.ac_image_bases(_ptr(lens_c, ctypes.c_uint32), len(arrs)))
+    codes = np.zeros(n_bases // 16, dtype=np.uint32)
+    nmask = np.zeros(n_bases // 32, dtype=np.uint32)
+    out_start = np.zeros(max(len(arrs), 1), dtype=np.uint64)
+    out_len = np.zeros(max(len(arrs), 1), dtype=np.uint32)
+    st = L.ac_pack_windows(_ptr(flat, ctypes.c_uint8),
+                           _ptr(starts if starts.size else np.zeros(1, np.uint64), ctypes.c_uint64),
+                           _ptr(lens_c, ctypes.c_uint32), len(arrs),
+                           _ptr(codes, ctypes.c_uint32), _ptr(nmask, ctypes.c_uint32),
+                           _ptr(out_start, ctypes.c_uint64), _ptr(out_len, ctypes.c_uint32), n_bases)
+    check(st)
+    return PackedSample(codes, nmask, out_start[: len(arrs)], out_len[: len(arrs)], n_bases)
+
+
+class ApproxCounter:
+    """One device context (ac_create / ac_destroy)."""
+
+    def __init__(self, device: int = -1):
+        L = _lib.load()
+        self._L = L
+        h = ctypes.c_void_p()
+        check(L.ac_create(ctypes.byref(h), device))
+        self._h = h
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._L.ac_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    @property
+    def handle(self):
+        return self._h
+
+    def count(self, k: int, kmers, sample: PackedSample) -> np.ndarray:
+        """ac_error_count: host arrays in, uint64 counts out (input order)."""
+        kmers = np.ascontiguousarray(np.asarray(kmers, dtype=np.uint64))
+        counts = np.zeros(max(kmers.size, 1), dtype=np.uint64)
+        ws = sample.as_struct()
+        st = self._L.ac_error_count(self._h, int(k),
+                                    _ptr(kmers if kmers.size else np.zeros(1, np.uint64), ctypes.c_uint64),
+                                    int(kmers.size), ctypes.byref(ws), _ptr(counts, ctypes.c_uint64))
+        check(st, self._h)
+        return counts[: kmers.size]
+
+    def count_device(self, k: int, segments, stream=None, accumulate: bool = False) -> None:
+        """ac_error_count_device over DeviceSegment objects (asynchronous)."""
+        arr = (ACSegment * len(segments))(*[s.as_struct() for s in segments])
+        fn = self._L.ac_error_count_device_accumulate if accumulate else self._L.ac_error_count_device
+        st = fn(self._h, int(k), arr, len(segments), ctypes.c_void_p(stream or 0))
+        check(st, self._h)
+
+    def last_launch(self):
+        w, wpw, g = ctypes.c_uint64(), ctypes.c_uint32(), ctypes.c_uint32()
+        check(self._L.ac_last_launch(self._h, ctypes.byref(w), ctypes.byref(wpw), ctypes.byref(g)), self._h)
+        return {"waves": w.value, "windows_per_wave": wpw.value, "groups": g.value}
+
+
+class DeviceSegment:
+    """A segment whose arrays live in device memory (torch tensors on cuda)."""
+
+    def __init__(self, kmers, codes, nmask, start, length, counts, n_bases: int):
+        self.kmers, self.codes, self.nmask = kmers, codes, nmask
+        self.start, self.length, self.counts = start, length, counts
+        self.n_bases = int(n_bases)
+
+    @classmethod
+    def upload(cls, kmers, sample: PackedSample, device="cuda"):
+        import torch
+
+        def t(a):
+            # uint64 / uint32 views through int64 / int32 tensors (same bytes)
+            a = np.ascontiguousarray(a)
+            view = {np.dtype(np.uint64): np.int64, np.dtype(np.uint32): np.int32}[a.dtype]
+            return torch.from_numpy(a.view(view) if a.size else np.zeros(1, view)).to(device)
+
+        km = np.asarray(kmers, dtype=np.uint64)
+        counts = torch.zeros(max(km.size, 1), dtype=torch.int32, device=device)
+        seg = cls(t(km), t(sample.codes), t(sample.nmask), t(sample.start), t(sample.length),
+                  counts, sample.n_bases)
+        seg.n_kmers = int(km.size)
+        seg.n_windows = sample.n_windows
+        return seg
+
+    def as_struct(self) -> ACSegment:
+        def p(tensor, typ):
+            return ctypes.cast(ctypes.c_void_p(tensor.data_ptr()), ctypes.POINTER(typ))
+
+        ws = ACWindows(p(self.codes, ctypes.c_uint32), p(self.nmask, ctypes.c_uint32),
+                       p(self.start, ctypes.c_uint64), p(self.length, ctypes.c_uint32),
+                       self.n_windows, self.n_bases)
+        return ACSegment(p(self.kmers, ctypes.c_uint64), self.n_kmers, ws,
+                         p(self.counts, ctypes.c_uint32))
+
+    def counts_numpy(self) -> np.ndarray:
+        return self.counts[: self.n_kmers].cpu().numpy().view(np.uint32).astype(np.uint64)
+
+
+_default_counter = None
+
+
+def _counter() -> ApproxCounter:
+    global _default_counter
+    if _default_counter is None:
+        _default_counter = ApproxCounter()
+    return _default_counter
+
+
+def error_count(sequences, exact_count, nb_thread: int = 4, k: int = 16, v: int = 0) -> dict:
+    """errorCount (approx_counter.cpp:531-601): {kmer: approximate count}."""
+    del nb_thread, v  # OpenMP thread count / verbosity of the CPU reference
+    kmers = [int(km) for km, _ in exact_count]
+    if not kmers:
+        return {}
+    sample = pack_windows(sequences)
+    counts = _counter().count(k, kmers, sample)
+    return {km: int(c) for km, c in zip(kmers, counts)}

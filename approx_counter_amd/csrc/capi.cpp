@@ -1,0 +1,278 @@
+// capi.cpp -- C ABI of the MI355X approximate-count stage (include/approx_counter_amd.h).
+//
+// Replaces errorCount (approx_counter.cpp:531-601): where the reference builds
+// a bidirectional FM index over the sample (537-541) and runs SeqAn's
+// find<0,2> per candidate under OpenMP (547-599), this layer uploads the
+// packed sample once per call and launches one HIP kernel over the
+// candidate x window grid.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "approx_counter_amd.h"
+#include "wm_count.h"
+
+struct ac_ctx {
+    int device = 0;
+    int cu_count = 256;
+    hipStream_t stream = nullptr;
+    std::string err;
+    // grow-only device buffers for the host-buffer entry point
+    void* d_buf[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    size_t d_cap[6] = {0, 0, 0, 0, 0, 0};
+    std::vector<uint32_t> h_counts;
+    // last launch geometry
+    uint64_t last_waves = 0;
+    uint32_t last_wpw = 0, last_groups = 0;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+ac_status fail(ac_ctx* ctx, ac_status st, const std::string& msg) {
+    if (ctx) ctx->err = msg;
+    g_err = msg;
+    return st;
+}
+
+ac_status hip_fail(ac_ctx* ctx, hipError_t e, const char* what) {
+    return fail(ctx, e == hipErrorOutOfMemory ? AC_ERR_NOMEM : AC_ERR_DEVICE,
+                std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define AC_HIP(ctx, expr)                                  \
+    do {                                                   \
+        hipError_t e_ = (expr);                            \
+        if (e_ != hipSuccess) return hip_fail(ctx, e_, #expr); \
+    } while (0)
+
+uint32_t pack_factor(uint32_t k) { return std::min<uint32_t>(32u / k, AC_MAX_PACK); }
+
+ac_status check_k(ac_ctx* ctx, uint32_t k) {
+    // approx_counter.cpp:781-783: k must lie in [2, 32].
+    if (k < 2 || k > 32) return fail(ctx, AC_ERR_INVALID, "kmer size must be between 2 and 32 (included)");
+    return AC_OK;
+}
+
+ac_status ensure(ac_ctx* ctx, int slot, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    if (ctx->d_cap[slot] >= bytes) return AC_OK;
+    if (ctx->d_buf[slot]) (void)hipFree(ctx->d_buf[slot]);
+    ctx->d_buf[slot] = nullptr;
+    ctx->d_cap[slot] = 0;
+    AC_HIP(ctx, hipMalloc(&ctx->d_buf[slot], bytes));
+    ctx->d_cap[slot] = bytes;
+    return AC_OK;
+}
+
+ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hipStream_t stream,
+                 bool zero) {
+    if (ac_status st = check_k(ctx, k)) return st;
+    if (n > AC_MAX_SEGS) return fail(ctx, AC_ERR_INVALID, "too many segments in one launch (max 4)");
+    if (n && !segs) return fail(ctx, AC_ERR_INVALID, "segments is NULL");
+    const uint32_t P = pack_factor(k);
+    acamd::LaunchArgs a;
+    std::memset(&a, 0, sizeof a);
+    a.n_segs = n;
+    a.m = k;
+    a.P = P;
+    uint64_t items = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const ac_segment& s = segs[i];
+        if (s.n_kmers && (!s.kmers || !s.counts)) return fail(ctx, AC_ERR_INVALID, "segment kmers/counts is NULL");
+        if (s.n_kmers && s.sample.n_windows &&
+            (!s.sample.codes || !s.sample.nmask || !s.sample.start || !s.sample.length))
+            return fail(ctx, AC_ERR_INVALID, "segment sample has a NULL array");
+        if (s.sample.n_bases % 32) return fail(ctx, AC_ERR_INVALID, "sample n_bases must be a multiple of 32");
+        const uint32_t groups = (s.n_kmers + 64 * P - 1) / (64 * P);
+        items += (uint64_t)groups * s.sample.n_windows;
+    }
+    // Aim at 8 resident waves per SIMD (32 per CU) over the whole chip.
+    const uint64_t target = (uint64_t)ctx->cu_count * 32;
+    const uint32_t wpw = (uint32_t)std::max<uint64_t>(1, (items + target - 1) / target);
+    uint64_t wave = 0;
+    uint32_t groups_total = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const ac_segment& s = segs[i];
+        acamd::SegDev& d = a.seg[i];
+        d.kmers = s.kmers;
+        d.codes = s.sample.codes;
+        d.nmask = s.sample.nmask;
+        d.start = s.sample.start;
+        d.length = s.sample.length;
+        d.n_bases = s.sample.n_bases;
+        d.counts = s.counts;
+        d.n_kmers = s.n_kmers;
+        d.n_windows = s.sample.n_windows;
+        d.groups = std::max<uint32_t>(1, (s.n_kmers + 64 * P - 1) / (64 * P));
+        d.wpw = wpw;
+        d.wave_begin = wave;
+        if (s.n_kmers && s.sample.n_windows)
+            wave += (uint64_t)d.groups * ((s.sample.n_windows + wpw - 1) / wpw);
+        groups_total += s.n_kmers ? d.groups : 0;
+        if (zero && s.n_kmers) AC_HIP(ctx, hipMemsetAsync(s.counts, 0, sizeof(uint32_t) * s.n_kmers, stream));
+    }
+    // Segments with no waves are skipped by the lookup: give them an
+    // unreachable wave_begin so the kernel never selects them.
+    for (uint32_t i = 0; i < n; ++i)
+        if (!(segs[i].n_kmers && segs[i].sample.n_windows)) a.seg[i].wave_begin = ~0ull;
+    // The kernel picks the LAST segment whose wave_begin <= wave; keep the
+    // live segments' begins monotone.
+    a.total_waves = wave;
+    ctx->last_waves = wave;
+    ctx->last_wpw = wpw;
+    ctx->last_groups = groups_total;
+    AC_HIP(ctx, acamd::launch_wm2_count(a, stream));
+    return AC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ac_abi_version(void) { return AC_ABI_VERSION; }
+
+const char* ac_last_error(const ac_ctx* ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
+
+ac_status ac_create(ac_ctx** out, int device) {
+    if (!out) return fail(nullptr, AC_ERR_INVALID, "out is NULL");
+    *out = nullptr;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n == 0)
+        return fail(nullptr, AC_ERR_DEVICE, "no HIP device available (the approximate count runs on the GPU only)");
+    if (device < 0) {
+        if (hipGetDevice(&device) != hipSuccess) device = 0;
+    }
+    if (device >= n) return fail(nullptr, AC_ERR_INVALID, "device ordinal out of range");
+    ac_ctx* ctx = new (std::nothrow) ac_ctx();
+    if (!ctx) return fail(nullptr, AC_ERR_NOMEM, "cannot allocate context");
+    ctx->device = device;
+    hipDeviceProp_t prop;
+    if ((e = hipSetDevice(device)) != hipSuccess || (e = hipGetDeviceProperties(&prop, device)) != hipSuccess ||
+        (e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess) {
+        ac_status st = hip_fail(nullptr, e, "device setup");
+        delete ctx;
+        return st;
+    }
+    ctx->cu_count = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    *out = ctx;
+    return AC_OK;
+}
+
+void ac_destroy(ac_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    for (void* p : ctx->d_buf)
+        if (p) (void)hipFree(p);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+ac_status ac_error_count_device(ac_ctx* ctx, uint32_t k, const ac_segment* segments, uint32_t n_segments,
+                                void* hip_stream) {
+    if (!ctx) return fail(nullptr, AC_ERR_INVALID, "ctx is NULL");
+    AC_HIP(ctx, hipSetDevice(ctx->device));
+    return launch(ctx, k, segments, n_segments, (hipStream_t)hip_stream, true);
+}
+
+ac_status ac_error_count_device_accumulate(ac_ctx* ctx, uint32_t k, const ac_segment* segments,
+                                           uint32_t n_segments, void* hip_stream) {
+    if (!ctx) return fail(nullptr, AC_ERR_INVALID, "ctx is NULL");
+    AC_HIP(ctx, hipSetDevice(ctx->device));
+    return launch(ctx, k, segments, n_segments, (hipStream_t)hip_stream, false);
+}
+
+ac_status ac_error_count(ac_ctx* ctx, uint32_t k, const uint64_t* kmers, uint32_t n_kmers,
+                         const ac_windows* sample, uint64_t* counts) {
+    if (!ctx) return fail(nullptr, AC_ERR_INVALID, "ctx is NULL");
+    if (ac_status st = check_k(ctx, k)) return st;
+    if (n_kmers == 0) return AC_OK;
+    if (!kmers || !counts || !sample) return fail(ctx, AC_ERR_INVALID, "NULL argument");
+    const ac_windows& s = *sample;
+    if (s.n_bases % 32) return fail(ctx, AC_ERR_INVALID, "sample n_bases must be a multiple of 32");
+    if (s.n_windows && (!s.codes || !s.nmask || !s.start || !s.length))
+        return fail(ctx, AC_ERR_INVALID, "sample has a NULL array");
+    // Host-side layout check: every window inside the image and 32-aligned.
+    for (uint32_t i = 0; i < s.n_windows; ++i) {
+        if (s.start[i] % 32 || s.start[i] + s.length[i] > s.n_bases)
+            return fail(ctx, AC_ERR_INVALID, "window " + std::to_string(i) + " is misaligned or outside the image");
+    }
+    AC_HIP(ctx, hipSetDevice(ctx->device));
+    const size_t sz[6] = {sizeof(uint64_t) * n_kmers, sizeof(uint32_t) * (s.n_bases / 16),
+                          sizeof(uint32_t) * (s.n_bases / 32), sizeof(uint64_t) * s.n_windows,
+                          sizeof(uint32_t) * s.n_windows, sizeof(uint32_t) * n_kmers};
+    for (int i = 0; i < 6; ++i)
+        if (ac_status st = ensure(ctx, i, sz[i])) return st;
+    hipStream_t st = ctx->stream;
+    AC_HIP(ctx, hipMemcpyAsync(ctx->d_buf[0], kmers, sz[0], hipMemcpyHostToDevice, st));
+    if (s.n_windows) {
+        AC_HIP(ctx, hipMemcpyAsync(ctx->d_buf[1], s.codes, sz[1], hipMemcpyHostToDevice, st));
+        AC_HIP(ctx, hipMemcpyAsync(ctx->d_buf[2], s.nmask, sz[2], hipMemcpyHostToDevice, st));
+        AC_HIP(ctx, hipMemcpyAsync(ctx->d_buf[3], s.start, sz[3], hipMemcpyHostToDevice, st));
+        AC_HIP(ctx, hipMemcpyAsync(ctx->d_buf[4], s.length, sz[4], hipMemcpyHostToDevice, st));
+    }
+    ac_segment seg;
+    seg.kmers = (const uint64_t*)ctx->d_buf[0];
+    seg.n_kmers = n_kmers;
+    seg.sample.codes = (const uint32_t*)ctx->d_buf[1];
+    seg.sample.nmask = (const uint32_t*)ctx->d_buf[2];
+    seg.sample.start = (const uint64_t*)ctx->d_buf[3];
+    seg.sample.length = (const uint32_t*)ctx->d_buf[4];
+    seg.sample.n_windows = s.n_windows;
+    seg.sample.n_bases = s.n_bases;
+    seg.counts = (uint32_t*)ctx->d_buf[5];
+    if (ac_status rc = launch(ctx, k, &seg, 1, st, true)) return rc;
+    ctx->h_counts.resize(n_kmers);
+    AC_HIP(ctx, hipMemcpyAsync(ctx->h_counts.data(), ctx->d_buf[5], sz[5], hipMemcpyDeviceToHost, st));
+    AC_HIP(ctx, hipStreamSynchronize(st));
+    for (uint32_t i = 0; i < n_kmers; ++i) counts[i] = ctx->h_counts[i];
+    return AC_OK;
+}
+
+ac_status ac_last_launch(const ac_ctx* ctx, uint64_t* waves, uint32_t* windows_per_wave, uint32_t* groups) {
+    if (!ctx) return fail(nullptr, AC_ERR_INVALID, "ctx is NULL");
+    if (waves) *waves = ctx->last_waves;
+    if (windows_per_wave) *windows_per_wave = ctx->last_wpw;
+    if (groups) *groups = ctx->last_groups;
+    return AC_OK;
+}
+
+uint64_t ac_image_bases(const uint32_t* seq_len, uint32_t n) {
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < n; ++i) total += ((uint64_t)seq_len[i] + 31) / 32 * 32;
+    return total ? total : 32;
+}
+
+ac_status ac_pack_windows(const uint8_t* dna5, const uint64_t* seq_start, const uint32_t* seq_len, uint32_t n,
+                          uint32_t* codes, uint32_t* nmask, uint64_t* start, uint32_t* length, uint64_t n_bases) {
+    if (n && (!dna5 || !seq_start || !seq_len || !start || !length))
+        return fail(nullptr, AC_ERR_INVALID, "NULL argument");
+    if (!codes || !nmask) return fail(nullptr, AC_ERR_INVALID, "NULL image");
+    if (n_bases % 32 || n_bases < ac_image_bases(seq_len, n))
+        return fail(nullptr, AC_ERR_INVALID, "image too small (use ac_image_bases)");
+    std::memset(codes, 0, sizeof(uint32_t) * (n_bases / 16));
+    std::memset(nmask, 0, sizeof(uint32_t) * (n_bases / 32));
+    uint64_t pos = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint8_t* src = dna5 + seq_start[i];
+        const uint32_t len = seq_len[i];
+        start[i] = pos;
+        length[i] = len;
+        for (uint32_t j = 0; j < len; ++j) {
+            const uint64_t b = pos + j;
+            const uint8_t v = src[j];
+            if (v < 4) codes[b >> 4] |= (uint32_t)v << (2 * (b & 15));
+            else nmask[b >> 5] |= 1u << (b & 31);
+        }
+        pos += ((uint64_t)len + 31) / 32 * 32;
+    }
+    return AC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,136 @@
+/*
+ * approx_counter_amd.h -- C ABI of the MI355X approximate-count stage.
+ *
+ * Drop-in boundary for qbonenfant/approx_counter's hot path.  The reference
+ * has no plugin/FFI API; its one internal seam on the hot
+ * path is
+ *
+ *     counter errorCount(sequence_set_type& sequences, pair_vector& exact_count,
+ *                        uint8_t nb_thread, uint8_t k, uint8_t v);
+ *                                              -- approx_counter.cpp:531
+ *
+ * called once per (run, end) from main (approx_counter.cpp:922).  Every entry
+ * point below names the reference code it replaces.  Plain C types only; no
+ * exceptions and no exit() cross this boundary: every call returns an
+ * ac_status (0 = OK) and the text of the last failure is available from
+ * ac_last_error().  The library has no CPU fallback: without a HIP device
+ * ac_create() fails with AC_ERR_DEVICE.
+ *
+ * Counting contract (model M1): for every candidate k-mer,
+ *     count = sum over windows w of max(0, 3 - d(kmer, w))
+ * where d is the semi-global Levenshtein distance between the whole k-mer and
+ * the best substring of w, a non-ACGT base matching nothing.  This equals the
+ * reference's  sum_e popcount(tcount[e])  (approx_counter.cpp:553-593) under
+ * SeqAn 2.4's find<0,2>(..., EditDistance()) semantics.
+ */
+#ifndef APPROX_COUNTER_AMD_H
+#define APPROX_COUNTER_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AC_ABI_VERSION 1
+
+typedef int32_t ac_status;
+#define AC_OK 0
+#define AC_ERR_INVALID 1  /* bad argument (k outside [2,32], NULL pointer, layout) */
+#define AC_ERR_DEVICE 2   /* no HIP device, or a HIP runtime failure               */
+#define AC_ERR_NOMEM 3    /* device or host allocation failed                     */
+#define AC_ERR_INTERNAL 4
+
+typedef struct ac_ctx ac_ctx;
+
+/*
+ * Packed sample ("window image").  Replaces the StringSet<Dna5String> sample
+ * (approx_counter.cpp:38, built by sampleSequences 415-476).
+ *   codes : 2 bits per base (A0 C1 G2 T3; any value for N), base b at bits
+ *           2*(b%16)..2*(b%16)+1 of codes[b/16]          (n_bases/16 words)
+ *   nmask : bit (b%32) of nmask[b/32] set iff base b is not A/C/G/T
+ *           (Dna5 ordValue 4, "N")                       (n_bases/32 words)
+ *   start : window i occupies bases [start[i], start[i]+length[i]);
+ *           start[i] % 32 == 0 (each window begins on a 32-base boundary)
+ *   length: window length in bases (sl for a start window, sl+1 for an end
+ *           window, approx_counter.cpp:463/466); 0 is allowed
+ *   n_bases: size of the image in bases, a multiple of 32
+ * All pointers are host pointers for ac_error_count() and device pointers for
+ * the *_device entry points.
+ */
+typedef struct ac_windows {
+    const uint32_t* codes;
+    const uint32_t* nmask;
+    const uint64_t* start;
+    const uint32_t* length;
+    uint32_t n_windows;
+    uint64_t n_bases;
+} ac_windows;
+
+/* One approximate-count job = one errorCount call (approx_counter.cpp:922). */
+typedef struct ac_segment {
+    const uint64_t* kmers; /* dna2int layout (approx_counter.cpp:55-62)     */
+    uint32_t n_kmers;
+    ac_windows sample;
+    uint32_t* counts;      /* n_kmers counters, input order                 */
+} ac_segment;
+
+/* Opens a context on HIP device `device` (-1: the current device).  Replaces
+ * the index construction + omp_set_num_threads of errorCount (537-547). */
+ac_status ac_create(ac_ctx** out, int device);
+void ac_destroy(ac_ctx* ctx);
+/* Last failure text for ctx (or for the calling thread when ctx is NULL). */
+const char* ac_last_error(const ac_ctx* ctx);
+int ac_abi_version(void);
+
+/*
+ * errorCount (approx_counter.cpp:531-601), host buffers in and out:
+ * counts[i] = M1 count of kmers[i] over `sample`.  Copies the inputs to the
+ * device, runs the HIP kernel, copies the counts back; synchronous.
+ * Replaces: index build (537-541), the omp parallel search loop (550-599),
+ * the per-level bitfields and their sum (553, 580-593) and results[kmer]=total
+ * (595-596).  Duplicate k-mers are allowed and counted independently.
+ */
+ac_status ac_error_count(ac_ctx* ctx, uint32_t k, const uint64_t* kmers, uint32_t n_kmers,
+                         const ac_windows* sample, uint64_t* counts);
+
+/*
+ * Device-resident form (same semantics), asynchronous on `hip_stream`
+ * (a hipStream_t; NULL = the default stream).  All segments share k and run
+ * in ONE kernel launch (both read ends of one run, 858-953).  Each segment's
+ * counts are zeroed on the stream and then accumulated: uint32 counters.
+ */
+ac_status ac_error_count_device(ac_ctx* ctx, uint32_t k, const ac_segment* segments,
+                                uint32_t n_segments, void* hip_stream);
+
+/* Same as ac_error_count_device but accumulates into `counts` without
+ * zeroing them first (used to combine window shards on one device). */
+ac_status ac_error_count_device_accumulate(ac_ctx* ctx, uint32_t k, const ac_segment* segments,
+                                           uint32_t n_segments, void* hip_stream);
+
+/*
+ * Host packing of Dna5 windows into a window image (no reference counterpart:
+ * SeqAn keeps 1 byte per base; this is the boundary's wire format).
+ *   dna5     : window bytes, ordValues 0..3 for ACGT, >= 4 for N
+ *   seq_start/seq_len: window i = dna5[seq_start[i] .. +seq_len[i])
+ * ac_image_bases() returns the image size (bases) needed for these lengths.
+ * The caller allocates codes (n_bases/16 words), nmask (n_bases/32 words),
+ * start (n windows) and length (n windows).
+ */
+uint64_t ac_image_bases(const uint32_t* seq_len, uint32_t n);
+ac_status ac_pack_windows(const uint8_t* dna5, const uint64_t* seq_start, const uint32_t* seq_len,
+                          uint32_t n, uint32_t* codes, uint32_t* nmask, uint64_t* start,
+                          uint32_t* length, uint64_t n_bases);
+
+/*
+ * Launch geometry actually used for the last device launch of ctx (for
+ * measurement): waves launched, windows per wave, candidate groups.
+ */
+ac_status ac_last_launch(const ac_ctx* ctx, uint64_t* waves, uint32_t* windows_per_wave,
+                         uint32_t* groups);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* APPROX_COUNTER_AMD_H */

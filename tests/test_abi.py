@@ -1,0 +1,87 @@
+"""CPU tests of the C ABI library: it loads, exports every declared symbol, and the
+host-only entry points (packing, argument checks) behave; no kernel calls here."""
+import ctypes
+import subprocess
+
+import numpy as np
+import pytest
+
+import approx_counter_amd as ac
+from approx_counter_amd import _lib
+
+
+def test_library_exports_every_header_symbol():
+    L = _lib.load()
+    names = _lib.header_functions()
+    assert "ac_error_count" in names and "ac_error_count_device" in names
+    for n in names:
+        assert hasattr(L, n), n
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if ln.strip()}
+    assert set(names) <= exported
+
+
+def test_library_targets_gfx950():
+    out = subprocess.run(["strings", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    assert "gfx950" in out
+
+
+def test_abi_version():
+    assert _lib.load().ac_abi_version() == 1
+
+
+def test_pack_layout():
+    wins = ["ACGTN", "A" * 40, "", "acgtRYgt", "T" * 32]
+    s = ac.pack_windows(wins)
+    assert s.n_bases % 32 == 0
+    assert list(s.length) == [5, 40, 0, 8, 32]
+    assert all(int(x) % 32 == 0 for x in s.start)
+    for w, st, ln in zip(wins, s.start, s.length):
+        d5 = ac.to_dna5(w)
+        for j in range(int(ln)):
+            b = int(st) + j
+            code = (int(s.codes[b // 16]) >> (2 * (b % 16))) & 3
+            isn = (int(s.nmask[b // 32]) >> (b % 32)) & 1
+            assert isn == int(d5[j] >= 4)
+            if not isn:
+                assert code == d5[j]
+    assert s.start[-1] + s.length[-1] <= s.n_bases
+
+
+def test_dna5_mapping():
+    assert list(ac.to_dna5("ACGTUacgtuNRYX-")) == [0, 1, 2, 3, 3, 0, 1, 2, 3, 3, 4, 4, 4, 4, 4]
+
+
+def test_null_ctx_is_rejected():
+    L = _lib.load()
+    st = L.ac_error_count(None, 16, None, 0, None, None)
+    assert st == _lib.AC_ERR_INVALID
+    assert b"ctx" in L.ac_last_error(None)
+
+
+def _has_gpu():
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:
+        return False
+
+
+@pytest.mark.skipif(_has_gpu(), reason="only meaningful without a GPU")
+def test_no_device_fails_loudly():
+    with pytest.raises(ac.ApproxCounterError) as ei:
+        ac.ApproxCounter()
+    assert ei.value.status == _lib.AC_ERR_DEVICE
+
+
+def test_image_too_small_rejected():
+    L = _lib.load()
+    lens = np.array([40], np.uint32)
+    codes = np.zeros(2, np.uint32)
+    nmask = np.zeros(1, np.uint32)
+    dna = np.zeros(40, np.uint8)
+    st = L.ac_pack_windows(dna.ctypes.data_as(_lib.p8), np.zeros(1, np.uint64).ctypes.data_as(_lib.p64),
+                           lens.ctypes.data_as(_lib.p32), 1, codes.ctypes.data_as(_lib.p32),
+                           nmask.ctypes.data_as(_lib.p32), np.zeros(1, np.uint64).ctypes.data_as(_lib.p64),
+                           np.zeros(1, np.uint32).ctypes.data_as(_lib.p32), ctypes.c_uint64(32))
+    assert st == _lib.AC_ERR_INVALID
