@@ -8,31 +8,35 @@
 // candidate's counter (the vectorSum of 590-593).
 //
 // Algorithm: bit-parallel Wu-Manber NFA for edit distance <= 2 (Wu & Manber
-// 1992, "Fast text searching allowing errors"), free start in the text.
-// Bit i of row R_d = "pattern prefix of length i+1 ends at the current text
-// position with <= d edits":
-//   R0' = ((R0 << 1) | 1) & Eq
-//   Rd' = ((Rd << 1) & Eq) | Rd-1 | (Rd-1 << 1) | (Rd-1' << 1) | low_d
-// (low_d = bits 0..d-1, always set).  The top bit (i = k-1) ORed over the
-// window is [d_min <= d]; the count adds the three levels.
+// 1992) in its complemented "shift-or" form (Baeza-Yates & Gonnet 1992), free
+// start in the text.  With R_d bit i = "pattern prefix of length i+1 ends at
+// the current text position with <= d edits" and D_d = ~R_d:
+//   D0' = (D0 >> P) | ~Eq
+//   Dd' = ((Dd >> P) | ~Eq) & Dd-1 & (Dd-1 >> P) & (Dd-1' >> P)      d = 1, 2
+// The shift brings in zeros, i.e. "R bit set": that is the free start of row
+// 0 and the always-set prefix bits of rows 1 and 2, with no mask operation.
+// A window hits level d iff the AND of D_d over its positions has the
+// pattern's last bit clear; the count adds the three levels.
 //
 // MI355X mapping:
-//  * lane = candidate(s), window text wave-uniform.  The 2-bit text and the
-//    N mask are read with scalar loads; each base becomes sign-extended SGPR
-//    masks H, L so Eq = ~(ph ^ H) & ~(pl ^ L) is two VALU ops with no per-lane
-//    table lookup.
-//  * P = floor(32/k) (<= 4) candidates are packed side by side in one 32-bit
-//    register.  Bits shifted out of pattern p land in pattern p+1's always-set
-//    low bits (row 0: the "| 1"; rows 1, 2: low_d), so they are absorbed.
-//  * Issue cost drives the instruction choice.  On gfx950 v_add_u32, v_and,
-//    v_or, v_xor and v_bitop3_b32 issue in 2 cycles per wave64 while shifts,
-//    v_lshl_or, v_or3 and v_and_or take 4 (tools/ubench_valu.hip,
-//    profiles/r01_ubench_valu.txt).  So every shift is x + x and every 3-input
-//    boolean is one v_bitop3_b32; each row's shifted value (t_d = R_d' << 1) is
-//    computed once and reused as (R_d << 1) at the next base.  A base costs
-//    9 ops of NFA + 2 of Eq + 1.5 of hit accumulation (v_bitop3 OR3 over two
-//    bases) = 12.5 full-rate ops for P candidates.
-//  * Integer-only VALU work: no MFMA, no LDS.  Counts are uint32 atomics
+//  * lane = P candidates, window text wave-uniform.  P = floor(32/k) (<= 4)
+//    patterns are INTERLEAVED in one 32-bit register: character i of pattern p
+//    sits at bit 31 - (i*P + p), so one logical right shift by P advances every
+//    pattern at once and the zero fill reaches every pattern's first character.
+//  * Issue cost drives the instruction choice (tools/ubench_valu.hip,
+//    profiles/r01_ubench_valu.txt): on gfx950 v_and/v_or/v_xor/v_add/
+//    v_lshrrev_b32 and v_bitop3_b32 issue in 2 cycles per wave64 with VGPR
+//    operands; shifts left, v_or3, v_and_or, v_lshl_or and ANY instruction
+//    reading an SGPR take 4.  So every 3-input boolean is one v_bitop3_b32 and
+//    the text masks reach the VALU as VGPRs: each wave expands its window into
+//    per-base masks H = -(bit 1), L = -(bit 0) in LDS (one lane per base pair,
+//    ~0.1 VALU op per base) and reads them back as wave-uniform broadcast
+//    ds_read_b128 (two bases per read).  A base then costs 2 ops of ~Eq
+//    ( (ph ^ H) | (pl ^ L) ) + 8 ops of NFA + 1.5 of hit accumulation (v_bitop3
+//    AND3 over two bases) = 11.5 full-rate VALU ops for P candidates.
+//  * N (any non-ACGT base) never matches: chunks of 16 bases holding an N take
+//    a branch that ORs the N mask into ~Eq (one extra, SGPR-reading op).
+//  * Integer-only VALU work: no MFMA.  Counts are uint32 atomics
 //    (order-independent, bit-exact).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -42,47 +46,45 @@
 namespace acamd {
 namespace {
 
-// One text base of the NFA as ONE asm statement (no hipcc boundary pads inside;
-// plain VALU -> VALU dependencies need no software wait states on gfx950):
-//   xh  = ph ^ H ; eq = ~xh & ~(pl ^ L) [& ~N]            Eq of this base
-//   x0  = s0 | one ; r0' = x0 & eq ; t0 = r0' + r0'        row 0, t0 = r0' << 1
-//   h   = x0 | r0 | t0 ; r1' = (s1 & eq) | h ; t1 = r1' + r1'
-//   h   = s1 | r1 | t1 ; r2' = (s2 & eq) | h ; t2 = r2' + r2'
-// v_bitop3 tables over (s0, s1, s2) = (0xf0, 0xcc, 0xaa): 0x09 = ~a & ~(b ^ c),
-// 0xfe = a | b | c, 0xea = (a & b) | c.  With ACC, the hit accumulators take
-// the OR of this base's rows and the previous base's (q0..q2): 0xfe again.
-#define AC_STEP_EQ "v_xor_b32 %[xh], %[H], %[ph]\n\tv_bitop3_b32 %[eq], %[xh], %[pl], %[L] bitop3:0x09\n\t"
-#define AC_STEP_N "v_and_b32 %[eq], %[nN], %[eq]\n\t"
-#define AC_STEP_NFA                                                         \
-    "v_or_b32 %[x0], %[one], %[s0]\n\t"                                     \
-    "v_and_b32 %[r0n], %[x0], %[eq]\n\t"                                    \
-    "v_add_u32 %[t0], %[r0n], %[r0n]\n\t"                                   \
-    "v_bitop3_b32 %[h], %[x0], %[r0], %[t0] bitop3:0xfe\n\t"                \
-    "v_bitop3_b32 %[r1n], %[s1], %[eq], %[h] bitop3:0xea\n\t"               \
-    "v_add_u32 %[t1], %[r1n], %[r1n]\n\t"                                   \
-    "v_bitop3_b32 %[h], %[s1], %[r1], %[t1] bitop3:0xfe\n\t"                \
-    "v_bitop3_b32 %[r2n], %[s2], %[eq], %[h] bitop3:0xea\n\t"               \
-    "v_add_u32 %[t2], %[r2n], %[r2n]\n\t"
-#define AC_STEP_ACC                                                         \
-    "v_bitop3_b32 %[a0], %[a0], %[r0], %[r0n] bitop3:0xfe\n\t"              \
-    "v_bitop3_b32 %[a1], %[a1], %[r1], %[r1n] bitop3:0xfe\n\t"              \
-    "v_bitop3_b32 %[a2], %[a2], %[r2], %[r2n] bitop3:0xfe\n\t"
-#define AC_STEP_OUT                                                                              \
-    [r0n] "=&v"(r0n), [r1n] "=&v"(r1n), [r2n] "=&v"(r2n), [t0] "=&v"(t0), [t1] "=&v"(t1),         \
-        [t2] "=&v"(t2), [xh] "=&v"(xh), [eq] "=&v"(eq), [x0] "=&v"(x0), [h] "=&v"(h)
-#define AC_STEP_IN                                                                               \
-    [r0] "v"(s.r0), [r1] "v"(s.r1), [r2] "v"(s.r2), [s0] "v"(s.s0), [s1] "v"(s.s1), [s2] "v"(s.s2), \
-        [ph] "v"(c.ph), [pl] "v"(c.pl), [H] "s"(H), [L] "s"(L), [one] "s"(c.one)
+constexpr int WAVES_PER_BLOCK = 4;
+constexpr uint32_t SEG_BASES = 128;  // window bases staged in LDS per pass (one pair per lane)
+
+// v_bitop3 truth tables over (s0, s1, s2) = (0xf0, 0xcc, 0xaa).
+//   0xf6 = a | (b ^ c)      ~Eq from (ph ^ H, pl, L)
+//   0xbe = (a ^ b) | c      ph ^ H with the N mask folded in
+//   0x80 = a & b & c
+//   0xa8 = (a | b) & c
+// One text base as ONE asm statement: hipcc pads nothing inside it, and plain
+// VALU -> VALU dependencies need no software wait states on gfx950.
+#define AC_NEQ "v_xor_b32 %[xh], %[H], %[ph]\n\tv_bitop3_b32 %[ne], %[xh], %[pl], %[L] bitop3:0xf6\n\t"
+#define AC_NEQ_N                                                                    \
+    "v_bitop3_b32 %[xh], %[ph], %[H], %[N] bitop3:0xbe\n\t"                          \
+    "v_bitop3_b32 %[ne], %[xh], %[pl], %[L] bitop3:0xf6\n\t"
+#define AC_NFA                                                                  \
+    "v_or_b32 %[d0n], %[s0], %[ne]\n\t"                                              \
+    "v_lshrrev_b32 %[t0], %[sh], %[d0n]\n\t"                                        \
+    "v_bitop3_b32 %[g], %[s0], %[d0], %[t0] bitop3:0x80\n\t"                         \
+    "v_bitop3_b32 %[d1n], %[s1], %[ne], %[g] bitop3:0xa8\n\t"                        \
+    "v_lshrrev_b32 %[t1], %[sh], %[d1n]\n\t"                                        \
+    "v_bitop3_b32 %[g], %[s1], %[d1], %[t1] bitop3:0x80\n\t"                         \
+    "v_bitop3_b32 %[d2n], %[s2], %[ne], %[g] bitop3:0xa8\n\t"                        \
+    "v_lshrrev_b32 %[t2], %[sh], %[d2n]\n\t"
+#define AC_ACC                                                                      \
+    "v_bitop3_b32 %[a0], %[a0], %[d0], %[d0n] bitop3:0x80\n\t"                       \
+    "v_bitop3_b32 %[a1], %[a1], %[d1], %[d1n] bitop3:0x80\n\t"                       \
+    "v_bitop3_b32 %[a2], %[a2], %[d2], %[d2n] bitop3:0x80\n\t"
+#define AC_OUT                                                                                  \
+    [d0n] "=&v"(d0n), [d1n] "=&v"(d1n), [d2n] "=&v"(d2n), [t0] "=&v"(t0), [t1] "=&v"(t1),        \
+        [t2] "=&v"(t2), [xh] "=&v"(xh), [ne] "=&v"(ne), [g] "=&v"(g)
+#define AC_IN                                                                                   \
+    [d0] "v"(s.d0), [d1] "v"(s.d1), [d2] "v"(s.d2), [s0] "v"(s.s0), [s1] "v"(s.s1),              \
+        [s2] "v"(s.s2), [ph] "v"(ph), [pl] "v"(pl), [H] "v"(H), [L] "v"(L), [sh] "i"(P)
+#define AC_ACC_OUT [a0] "+v"(s.a0), [a1] "+v"(s.a1), [a2] "+v"(s.a2)
 
 struct Nfa {
-    uint32_t r0, r1, r2;  // rows
-    uint32_t s0, s1, s2;  // rows << 1
-    uint32_t a0, a1, a2;  // OR of the rows over the window
-};
-
-struct Lane {
-    uint32_t ph, pl;  // high / low bit of every pattern base (lane constants)
-    uint32_t one;     // bit 0 of every pattern (wave-uniform)
+    uint32_t d0, d1, d2;  // complemented rows
+    uint32_t s0, s1, s2;  // rows >> P
+    uint32_t a0, a1, a2;  // AND of the rows over the window
 };
 
 // Sign-extended single bit: 0 or 0xffffffff (one s_bfe_i32 on a uniform word).
@@ -90,63 +92,64 @@ __device__ __forceinline__ uint32_t sbit(uint32_t w, int bit) {
     return (uint32_t)(((int32_t)(w << (31 - bit))) >> 31);
 }
 
-// One base j of a code word.  ACC: also OR this base's rows and the previous
-// base's (still in s.r*) into the hit accumulators (called on odd bases).
-template <bool HAS_N, bool ACC>
-__device__ __forceinline__ void nfa_base(Nfa& s, const Lane& c, uint32_t code, uint32_t nm, int j) {
-    const uint32_t H = sbit(code, 2 * j + 1), L = sbit(code, 2 * j);
-    uint32_t r0n, r1n, r2n, t0, t1, t2, xh, eq, x0, h;
+// One text base with masks (H, L).  ACC (odd bases): also AND this base's rows
+// and the previous base's (still in s.d*) into the hit accumulators.  HAS_N:
+// `nm` bit j marks an N.
+template <int P, bool HAS_N, bool ACC>
+__device__ __forceinline__ void nfa_base(Nfa& s, uint32_t ph, uint32_t pl, uint32_t H, uint32_t L,
+                                         uint32_t nm, int j) {
+    uint32_t d0n, d1n, d2n, t0, t1, t2, xh, ne, g;
     if constexpr (!HAS_N && !ACC) {
-        asm(AC_STEP_EQ AC_STEP_NFA : AC_STEP_OUT : AC_STEP_IN);
+        asm(AC_NEQ AC_NFA : AC_OUT : AC_IN);
     } else if constexpr (!HAS_N && ACC) {
-        asm(AC_STEP_EQ AC_STEP_NFA AC_STEP_ACC
-            : AC_STEP_OUT, [a0] "+v"(s.a0), [a1] "+v"(s.a1), [a2] "+v"(s.a2) : AC_STEP_IN);
+        asm(AC_NEQ AC_NFA AC_ACC : AC_OUT, AC_ACC_OUT : AC_IN);
     } else if constexpr (HAS_N && !ACC) {
-        const uint32_t nN = ~sbit(nm, j);
-        asm(AC_STEP_EQ AC_STEP_N AC_STEP_NFA : AC_STEP_OUT : AC_STEP_IN, [nN] "s"(nN));
+        const uint32_t N = sbit(nm, j);
+        asm(AC_NEQ_N AC_NFA : AC_OUT : AC_IN, [N] "s"(N));
     } else {
-        const uint32_t nN = ~sbit(nm, j);
-        asm(AC_STEP_EQ AC_STEP_N AC_STEP_NFA AC_STEP_ACC
-            : AC_STEP_OUT, [a0] "+v"(s.a0), [a1] "+v"(s.a1), [a2] "+v"(s.a2) : AC_STEP_IN, [nN] "s"(nN));
+        const uint32_t N = sbit(nm, j);
+        asm(AC_NEQ_N AC_NFA AC_ACC : AC_OUT, AC_ACC_OUT : AC_IN, [N] "s"(N));
     }
-    s.r0 = r0n;
-    s.r1 = r1n;
-    s.r2 = r2n;
+    s.d0 = d0n;
+    s.d1 = d1n;
+    s.d2 = d2n;
     s.s0 = t0;
     s.s1 = t1;
     s.s2 = t2;
 }
 
-// NB bases (even) from the low bits of one code word: 12.5 VALU per base.
-template <int NB, bool HAS_N>
-__device__ __forceinline__ void chunk(Nfa& s, const Lane& c, uint32_t code, uint32_t nm) {
+// NB (even) bases starting at pair index q of the staged masks; `nm` bit j is
+// the N flag of base j of this group.
+template <int P, int NB, bool HAS_N>
+__device__ __forceinline__ void run(Nfa& s, uint32_t ph, uint32_t pl, const uint4* __restrict__ hl,
+                                    uint32_t q, uint32_t nm) {
 #pragma unroll
     for (int j = 0; j < NB; j += 2) {
-        nfa_base<HAS_N, false>(s, c, code, nm, j);
-        nfa_base<HAS_N, true>(s, c, code, nm, j + 1);
+        const uint4 m = hl[q + j / 2];
+        nfa_base<P, HAS_N, false>(s, ph, pl, m.x, m.y, nm, j);
+        nfa_base<P, HAS_N, true>(s, ph, pl, m.z, m.w, nm, j + 1);
     }
 }
 
-template <int NB>
-__device__ __forceinline__ void chunk_any(Nfa& s, const Lane& c, uint32_t code, uint32_t nm) {
-    if (nm == 0u) chunk<NB, false>(s, c, code, nm);
-    else chunk<NB, true>(s, c, code, nm);
+template <int P, int NB>
+__device__ __forceinline__ void run_any(Nfa& s, uint32_t ph, uint32_t pl, const uint4* __restrict__ hl,
+                                        uint32_t q, uint32_t nm) {
+    if (nm == 0u) run<P, NB, false>(s, ph, pl, hl, q, nm);
+    else run<P, NB, true>(s, ph, pl, hl, q, nm);
 }
 
-__device__ __forceinline__ void one_base(Nfa& s, const Lane& c, uint32_t code, uint32_t nm) {
-    nfa_base<true, false>(s, c, code, nm, 0);
-    s.a0 |= s.r0;
-    s.a1 |= s.r1;
-    s.a2 |= s.r2;
+// N flags of bases [b, b + 16) of a window (b a multiple of 16) from the mask image.
+__device__ __forceinline__ uint32_t nflags16(const uint32_t* __restrict__ nmask, uint32_t b) {
+    return (nmask[b >> 5] >> (b & 16u)) & 0xffffu;
 }
 
-}  // namespace
-
-__global__ __launch_bounds__(256) void wm2_count_kernel(LaunchArgs a) {
+template <int P>
+__device__ __forceinline__ void count_kernel_body(const LaunchArgs& a, uint4* __restrict__ stage) {
     const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t wave =
-        (uint64_t)blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t wave = (uint64_t)blockIdx.x * WAVES_PER_BLOCK + wib;
     if (wave >= a.total_waves) return;
+    uint4* __restrict__ hl = stage + wib * (SEG_BASES / 2);
 
     // Segment lookup (wave-uniform, <= AC_MAX_SEGS entries).
     int si = 0;
@@ -157,36 +160,31 @@ __global__ __launch_bounds__(256) void wm2_count_kernel(LaunchArgs a) {
     const uint64_t local = wave - sg.wave_begin;
     const uint32_t g = (uint32_t)(local % sg.groups);
     const uint32_t wb = (uint32_t)(local / sg.groups);
+    const uint32_t m = a.m;
 
-    const uint32_t m = a.m, P = a.P;
-
-    // Lane constants: P patterns of m bits side by side, pattern base i at bit p*m+i.
-    Lane c;
-    c.ph = 0;
-    c.pl = 0;
-    uint32_t one = 0;
-    uint32_t cand[AC_MAX_PACK];
+    // Lane constants: character i of pattern p at bit 31 - (i*P + p).
+    uint32_t ph = 0, pl = 0, first = 0, last_bit[P];
+    uint32_t cand[P];
 #pragma unroll
-    for (int p = 0; p < AC_MAX_PACK; ++p) {
+    for (int p = 0; p < P; ++p) {
         cand[p] = g * 64u * P + (uint32_t)p * 64u + lane;
-        if ((uint32_t)p < P) {
-            one |= 1u << (p * m);
-            if (cand[p] < sg.n_kmers) {
-                const uint64_t km = sg.kmers[cand[p]];
-                for (uint32_t i = 0; i < m; ++i) {
-                    const uint32_t b = (uint32_t)(km >> (2u * (m - 1u - i))) & 3u;
-                    c.ph |= (b >> 1) << (p * m + i);
-                    c.pl |= (b & 1u) << (p * m + i);
-                }
+        last_bit[p] = 31u - ((m - 1u) * P + (uint32_t)p);
+        first |= 1u << (31 - p);
+        if (cand[p] < sg.n_kmers) {
+            const uint64_t km = sg.kmers[cand[p]];
+            for (uint32_t i = 0; i < m; ++i) {
+                const uint32_t b = (uint32_t)(km >> (2u * (m - 1u - i))) & 3u;
+                ph |= (b >> 1) << (31u - (i * P + p));
+                pl |= (b & 1u) << (31u - (i * P + p));
             }
         }
     }
-    c.one = __builtin_amdgcn_readfirstlane(one);
-    const uint32_t low2 = c.one | (c.one << 1);
-    const uint32_t tops = c.one << (m - 1);
-    const uint32_t sh = m - 1;
+    // Initial rows (empty text): R1 has character 0 set, R2 characters 0 and 1.
+    const uint32_t d1_init = ~first, d2_init = ~(first | (first >> P));
 
-    uint32_t cnt[AC_MAX_PACK] = {0, 0, 0, 0};
+    uint32_t cnt[P];
+#pragma unroll
+    for (int p = 0; p < P; ++p) cnt[p] = 0;
 
     const uint32_t w_begin = wb * sg.wpw;
     const uint32_t w_end = min(sg.n_windows, w_begin + sg.wpw);
@@ -196,61 +194,91 @@ __global__ __launch_bounds__(256) void wm2_count_kernel(LaunchArgs a) {
         if ((base & 31u) || base + len > sg.n_bases) continue;  // malformed window: never read outside the image
         const uint32_t* __restrict__ codes = sg.codes + (base >> 4);
         const uint32_t* __restrict__ nmask = sg.nmask + (base >> 5);
-        // Initial rows: prefixes of length <= d match the empty text with d deletions.
         Nfa s;
-        s.r0 = 0u;
-        s.r1 = c.one;
-        s.r2 = low2;
-        s.s0 = 0u;
-        s.s1 = c.one << 1;
-        s.s2 = low2 << 1;
-        s.a0 = 0u;
-        s.a1 = c.one;
-        s.a2 = low2;  // for m <= 2 the empty alignment already reaches the top bit
-        const uint32_t nfull = len >> 4;
-        for (uint32_t ch = 0; ch < nfull; ++ch) {
-            const uint32_t code = codes[ch];
-            const uint32_t nm = (nmask[ch >> 1] >> ((ch & 1u) << 4)) & 0xffffu;
-            chunk_any<16>(s, c, code, nm);
+        s.d0 = ~0u;
+        s.d1 = d1_init;
+        s.d2 = d2_init;
+        s.s0 = ~0u >> P;
+        s.s1 = d1_init >> P;
+        s.s2 = d2_init >> P;
+        s.a0 = ~0u;
+        s.a1 = d1_init;
+        s.a2 = d2_init;  // for k <= 2 the empty alignment already reaches the last character
+        for (uint32_t sb = 0; sb < len; sb += SEG_BASES) {
+            // Stage bases [sb, sb + 128) as (H, L) mask pairs: lane l expands bases sb+2l, sb+2l+1.
+            {
+                const uint32_t b = sb + 2u * lane;
+                const uint32_t code = b < len ? codes[b >> 4] : 0u;
+                const int sh = (int)(2u * (b & 15u));
+                uint4 v;
+                v.x = sbit(code, sh + 1);
+                v.y = sbit(code, sh);
+                v.z = sbit(code, sh + 3);
+                v.w = sbit(code, sh + 2);
+                hl[lane] = v;
+            }
+            const uint32_t nb = min(SEG_BASES, len - sb);
+            const uint32_t nfull = nb >> 4;
+            for (uint32_t ch = 0; ch < nfull; ++ch)
+                run_any<P, 16>(s, ph, pl, hl, ch * 8u, nflags16(nmask, sb + ch * 16u));
+            const uint32_t rem = nb & 15u;
+            if (rem) {
+                uint32_t q = nfull * 8u;
+                uint32_t nm = nflags16(nmask, sb + nfull * 16u);
+                if (rem & 8u) {
+                    run_any<P, 8>(s, ph, pl, hl, q, nm);
+                    q += 4u;
+                    nm >>= 8;
+                }
+                if (rem & 4u) {
+                    run_any<P, 4>(s, ph, pl, hl, q, nm);
+                    q += 2u;
+                    nm >>= 4;
+                }
+                if (rem & 2u) {
+                    run_any<P, 2>(s, ph, pl, hl, q, nm);
+                    q += 1u;
+                    nm >>= 2;
+                }
+                if (rem & 1u) {
+                    const uint4 mm = hl[q];
+                    nfa_base<P, true, false>(s, ph, pl, mm.x, mm.y, nm, 0);
+                    s.a0 &= s.d0;
+                    s.a1 &= s.d1;
+                    s.a2 &= s.d2;
+                }
+            }
         }
-        const uint32_t rem = len & 15u;
-        if (rem) {
-            uint32_t code = codes[nfull];
-            uint32_t nm = (nmask[nfull >> 1] >> ((nfull & 1u) << 4)) & 0xffffu;
-            if (rem & 8u) {
-                chunk_any<8>(s, c, code, nm);
-                code >>= 16;
-                nm >>= 8;
-            }
-            if (rem & 4u) {
-                chunk_any<4>(s, c, code, nm);
-                code >>= 8;
-                nm >>= 4;
-            }
-            if (rem & 2u) {
-                chunk_any<2>(s, c, code, nm);
-                code >>= 4;
-                nm >>= 2;
-            }
-            if (rem & 1u) one_base(s, c, code, nm);
-        }
-        const uint32_t t = ((s.a0 & tops) >> sh) + ((s.a1 & tops) >> sh) + ((s.a2 & tops) >> sh);
 #pragma unroll
-        for (int p = 0; p < AC_MAX_PACK; ++p)
-            if ((uint32_t)p < P) cnt[p] += (t >> (p * m)) & 3u;
+        for (int p = 0; p < P; ++p)
+            cnt[p] += 3u - ((s.a0 >> last_bit[p]) & 1u) - ((s.a1 >> last_bit[p]) & 1u) -
+                      ((s.a2 >> last_bit[p]) & 1u);
     }
 
 #pragma unroll
-    for (int p = 0; p < AC_MAX_PACK; ++p)
-        if ((uint32_t)p < P && cand[p] < sg.n_kmers && cnt[p]) atomicAdd(&sg.counts[cand[p]], cnt[p]);
+    for (int p = 0; p < P; ++p)
+        if (cand[p] < sg.n_kmers && cnt[p]) atomicAdd(&sg.counts[cand[p]], cnt[p]);
+}
+
+}  // namespace
+
+template <int P>
+__global__ __launch_bounds__(64 * WAVES_PER_BLOCK) void wm2_count_kernel(LaunchArgs a) {
+    __shared__ uint4 stage[WAVES_PER_BLOCK * (SEG_BASES / 2)];
+    count_kernel_body<P>(a, stage);
 }
 
 hipError_t launch_wm2_count(const LaunchArgs& args, hipStream_t stream) {
     if (args.total_waves == 0) return hipSuccess;
-    const uint32_t waves_per_block = 4;
-    const uint64_t blocks = (args.total_waves + waves_per_block - 1) / waves_per_block;
-    hipLaunchKernelGGL(wm2_count_kernel, dim3((uint32_t)blocks), dim3(64 * waves_per_block), 0,
-                       stream, args);
+    const uint64_t blocks = (args.total_waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
+    const dim3 grid((uint32_t)blocks), block(64 * WAVES_PER_BLOCK);
+    switch (args.P) {
+        case 1: hipLaunchKernelGGL(wm2_count_kernel<1>, grid, block, 0, stream, args); break;
+        case 2: hipLaunchKernelGGL(wm2_count_kernel<2>, grid, block, 0, stream, args); break;
+        case 3: hipLaunchKernelGGL(wm2_count_kernel<3>, grid, block, 0, stream, args); break;
+        case 4: hipLaunchKernelGGL(wm2_count_kernel<4>, grid, block, 0, stream, args); break;
+        default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 
