@@ -12,6 +12,8 @@ import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libapprox_counter_amd.so")
+# Kernel-tuning experiments (tools/variants.sh) point this at another build of the same sources.
+LIB_PATH = os.environ.get("APPROX_COUNTER_AMD_LIB", LIB_PATH)
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "approx_counter_amd.h")
 
 AC_OK, AC_ERR_INVALID, AC_ERR_DEVICE, AC_ERR_NOMEM, AC_ERR_INTERNAL = 0, 1, 2, 3, 4

@@ -25,6 +25,8 @@ struct ac_ctx {
     void* d_buf[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     size_t d_cap[6] = {0, 0, 0, 0, 0, 0};
     std::vector<uint32_t> h_counts;
+    // resident waves of the count kernel per pattern pack P (0 = not queried yet)
+    uint32_t resident[AC_MAX_PACK + 1] = {0, 0, 0, 0, 0};
     // last launch geometry
     uint64_t last_waves = 0;
     uint32_t last_wpw = 0, last_groups = 0;
@@ -51,8 +53,6 @@ ac_status hip_fail(ac_ctx* ctx, hipError_t e, const char* what) {
         if (e_ != hipSuccess) return hip_fail(ctx, e_, #expr); \
     } while (0)
 
-uint32_t pack_factor(uint32_t k) { return std::min<uint32_t>(32u / k, AC_MAX_PACK); }
-
 ac_status check_k(ac_ctx* ctx, uint32_t k) {
     // approx_counter.cpp:781-783: k must lie in [2, 32].
     if (k < 2 || k > 32) return fail(ctx, AC_ERR_INVALID, "kmer size must be between 2 and 32 (included)");
@@ -75,7 +75,8 @@ ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hi
     if (ac_status st = check_k(ctx, k)) return st;
     if (n > AC_MAX_SEGS) return fail(ctx, AC_ERR_INVALID, "too many segments in one launch (max 4)");
     if (n && !segs) return fail(ctx, AC_ERR_INVALID, "segments is NULL");
-    const uint32_t P = pack_factor(k);
+    const uint32_t P = acamd::pack_factor(k);
+    const uint32_t cpw = acamd::cands_per_wave(P);
     acamd::LaunchArgs a;
     std::memset(&a, 0, sizeof a);
     a.n_segs = n;
@@ -89,11 +90,14 @@ ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hi
             (!s.sample.codes || !s.sample.nmask || !s.sample.start || !s.sample.length))
             return fail(ctx, AC_ERR_INVALID, "segment sample has a NULL array");
         if (s.sample.n_bases % 32) return fail(ctx, AC_ERR_INVALID, "sample n_bases must be a multiple of 32");
-        const uint32_t groups = (s.n_kmers + 64 * P - 1) / (64 * P);
+        const uint32_t groups = (s.n_kmers + cpw - 1) / cpw;
         items += (uint64_t)groups * s.sample.n_windows;
     }
-    // Aim at 8 resident waves per SIMD (32 per CU) over the whole chip.
-    const uint64_t target = (uint64_t)ctx->cu_count * 32;
+    // One round of resident waves: every wave gets the same number of windows
+    // (windows of one job have near-equal lengths), and all of them are on the
+    // chip together, so the launch has no second, partly filled round.
+    if (!ctx->resident[P]) AC_HIP(ctx, acamd::resident_waves(P, ctx->cu_count, &ctx->resident[P]));
+    const uint64_t target = ctx->resident[P];
     const uint32_t wpw = (uint32_t)std::max<uint64_t>(1, (items + target - 1) / target);
     uint64_t wave = 0;
     uint32_t groups_total = 0;
@@ -109,7 +113,7 @@ ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hi
         d.counts = s.counts;
         d.n_kmers = s.n_kmers;
         d.n_windows = s.sample.n_windows;
-        d.groups = std::max<uint32_t>(1, (s.n_kmers + 64 * P - 1) / (64 * P));
+        d.groups = std::max<uint32_t>(1, (s.n_kmers + cpw - 1) / cpw);
         d.wpw = wpw;
         d.wave_begin = wave;
         if (s.n_kmers && s.sample.n_windows)
@@ -274,5 +278,10 @@ ac_status ac_pack_windows(const uint8_t* dna5, const uint64_t* seq_start, const 
     }
     return AC_OK;
 }
+
+#ifdef AC_STAMPS
+// Diagnostic builds only: per-wave timestamps of the last launch (not declared in the public header).
+int ac_debug_stamps(void* host, size_t bytes) { return (int)acamd::debug_stamps(host, bytes); }
+#endif
 
 }  // extern "C"

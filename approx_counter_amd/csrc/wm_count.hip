@@ -19,23 +19,28 @@
 // pattern's last bit clear; the count adds the three levels.
 //
 // MI355X mapping:
-//  * lane = P candidates, window text wave-uniform.  P = floor(32/k) (<= 4)
+//  * lane = 2 words x P candidates, window text wave-uniform.  P = floor(32/k) (<= 4)
 //    patterns are INTERLEAVED in one 32-bit register: character i of pattern p
 //    sits at bit 31 - (i*P + p), so one logical right shift by P advances every
 //    pattern at once and the zero fill reaches every pattern's first character.
+//    Each lane runs AC_WAVE_WORDS = 2 independent words (two candidate groups)
+//    over the same text: two independent dependency chains per wave and one
+//    staging / LDS read per base for 2P candidates.
 //  * Issue cost drives the instruction choice (tools/ubench_valu.hip,
 //    profiles/r01_ubench_valu.txt): on gfx950 v_and/v_or/v_xor/v_add/
 //    v_lshrrev_b32 and v_bitop3_b32 issue in 2 cycles per wave64 with VGPR
 //    operands; shifts left, v_or3, v_and_or, v_lshl_or and ANY instruction
 //    reading an SGPR take 4.  So every 3-input boolean is one v_bitop3_b32 and
 //    the text masks reach the VALU as VGPRs: each wave expands its window into
-//    per-base masks H = -(bit 1), L = -(bit 0) in LDS (one lane per base pair,
-//    ~0.1 VALU op per base) and reads them back as wave-uniform broadcast
-//    ds_read_b128 (two bases per read).  A base then costs 2 ops of ~Eq
+//    per-base masks H = -(bit 1), L = -(bit 0), N in LDS (one lane per 4
+//    bases, ~0.1 VALU op per base) and reads them back as wave-uniform
+//    broadcast ds_read_b128 (two bases per read).  The next window's code and
+//    N-mask words are loaded while the current window is computed.  A base then costs 2 ops of ~Eq
 //    ( (ph ^ H) | (pl ^ L) ) + 8 ops of NFA + 1.5 of hit accumulation (v_bitop3
 //    AND3 over two bases) = 11.5 full-rate VALU ops for P candidates.
-//  * N (any non-ACGT base) never matches: chunks of 16 bases holding an N take
-//    a branch that ORs the N mask into ~Eq (one extra, SGPR-reading op).
+//  * N (any non-ACGT base) never matches: a ballot at staging flags the
+//    16-base chunks holding an N; those take a path that ORs the base's N
+//    mask (also staged in LDS) into ~Eq at no extra VALU cost.
 //  * Integer-only VALU work: no MFMA.  Counts are uint32 atomics
 //    (order-independent, bit-exact).
 #include <hip/hip_runtime.h>
@@ -47,109 +52,183 @@ namespace acamd {
 namespace {
 
 constexpr int WAVES_PER_BLOCK = 4;
-constexpr uint32_t SEG_BASES = 128;  // window bases staged in LDS per pass (one pair per lane)
+#ifdef AC_STAMPS
+// Diagnostic build only (tools/variants.sh ... -DAC_STAMPS): per-wave
+// s_memrealtime stamps (100 MHz) at entry, after the prologue, after the last
+// window and at exit; read back with ac_debug_stamps().  No output value is
+// computed from them.
+}  // namespace
+__device__ uint64_t g_stamps[1 << 20];
+namespace {
+__device__ __forceinline__ void stamp(uint64_t wave, int i) {
+    if ((threadIdx.x & 63u) == 0 && wave < (1u << 18)) g_stamps[wave * 4 + i] = __builtin_amdgcn_s_memrealtime();
+}
+#else
+__device__ __forceinline__ void stamp(uint64_t, int) {}
+#endif
+constexpr int W = AC_WAVE_WORDS;
+constexpr uint32_t SEG = 256;  // window bases staged in LDS per pass (4 per lane)
 
-// v_bitop3 truth tables over (s0, s1, s2) = (0xf0, 0xcc, 0xaa).
-//   0xf6 = a | (b ^ c)      ~Eq from (ph ^ H, pl, L)
-//   0xbe = (a ^ b) | c      ph ^ H with the N mask folded in
-//   0x80 = a & b & c
-//   0xa8 = (a | b) & c
-// One text base as ONE asm statement: hipcc pads nothing inside it, and plain
-// VALU -> VALU dependencies need no software wait states on gfx950.
-#define AC_NEQ "v_xor_b32 %[xh], %[H], %[ph]\n\tv_bitop3_b32 %[ne], %[xh], %[pl], %[L] bitop3:0xf6\n\t"
-#define AC_NEQ_N                                                                    \
-    "v_bitop3_b32 %[xh], %[ph], %[H], %[N] bitop3:0xbe\n\t"                          \
-    "v_bitop3_b32 %[ne], %[xh], %[pl], %[L] bitop3:0xf6\n\t"
-#define AC_NFA                                                                  \
-    "v_or_b32 %[d0n], %[s0], %[ne]\n\t"                                              \
-    "v_lshrrev_b32 %[t0], %[sh], %[d0n]\n\t"                                        \
-    "v_bitop3_b32 %[g], %[s0], %[d0], %[t0] bitop3:0x80\n\t"                         \
-    "v_bitop3_b32 %[d1n], %[s1], %[ne], %[g] bitop3:0xa8\n\t"                        \
-    "v_lshrrev_b32 %[t1], %[sh], %[d1n]\n\t"                                        \
-    "v_bitop3_b32 %[g], %[s1], %[d1], %[t1] bitop3:0x80\n\t"                         \
-    "v_bitop3_b32 %[d2n], %[s2], %[ne], %[g] bitop3:0xa8\n\t"                        \
-    "v_lshrrev_b32 %[t2], %[sh], %[d2n]\n\t"
-#define AC_ACC                                                                      \
-    "v_bitop3_b32 %[a0], %[a0], %[d0], %[d0n] bitop3:0x80\n\t"                       \
-    "v_bitop3_b32 %[a1], %[a1], %[d1], %[d1n] bitop3:0x80\n\t"                       \
-    "v_bitop3_b32 %[a2], %[a2], %[d2], %[d2n] bitop3:0x80\n\t"
-#define AC_OUT                                                                                  \
-    [d0n] "=&v"(d0n), [d1n] "=&v"(d1n), [d2n] "=&v"(d2n), [t0] "=&v"(t0), [t1] "=&v"(t1),        \
-        [t2] "=&v"(t2), [xh] "=&v"(xh), [ne] "=&v"(ne), [g] "=&v"(g)
-#define AC_IN                                                                                   \
-    [d0] "v"(s.d0), [d1] "v"(s.d1), [d2] "v"(s.d2), [s0] "v"(s.s0), [s1] "v"(s.s1),              \
-        [s2] "v"(s.s2), [ph] "v"(ph), [pl] "v"(pl), [H] "v"(H), [L] "v"(L), [sh] "i"(P)
-#define AC_ACC_OUT [a0] "+v"(s.a0), [a1] "+v"(s.a1), [a2] "+v"(s.a2)
-
-struct Nfa {
-    uint32_t d0, d1, d2;  // complemented rows
-    uint32_t s0, s1, s2;  // rows >> P
-    uint32_t a0, a1, a2;  // AND of the rows over the window
+// Per-wave LDS staging of one window segment (3 KB).
+struct Stage {
+    uint4 hl[SEG / 2];  // (H, L) of bases 2q and 2q+1
+    uint32_t n[SEG];    // N mask of each base (0 or ~0)
 };
 
-// Sign-extended single bit: 0 or 0xffffffff (one s_bfe_i32 on a uniform word).
-__device__ __forceinline__ uint32_t sbit(uint32_t w, int bit) {
-    return (uint32_t)(((int32_t)(w << (31 - bit))) >> 31);
+// v_bitop3_b32 truth tables over (s0, s1, s2) = (0xf0, 0xcc, 0xaa).
+constexpr int NEQ = 0xf6;     // a | (b ^ c)      ~Eq from (ph ^ H, pl, L)
+constexpr int XOR_OR = 0xbe;  // (a ^ b) | c      ph ^ H with the N mask folded in
+constexpr int AND3 = 0x80;    // a & b & c
+constexpr int OR_AND = 0xa8;  // (a | b) & c
+template <int TT>
+__device__ __forceinline__ uint32_t bop3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, TT);
 }
 
-// One text base with masks (H, L).  ACC (odd bases): also AND this base's rows
-// and the previous base's (still in s.d*) into the hit accumulators.  HAS_N:
-// `nm` bit j marks an N.
+struct Nfa {
+    uint32_t d0[W], d1[W], d2[W];  // complemented rows
+    uint32_t s0[W], s1[W], s2[W];  // rows >> P
+    uint32_t a0[W], a1[W], a2[W];  // AND of the rows over the window
+};
+
+// One text base (masks H, L, N) for both words: 11 full-rate VALU ops per
+// word, 8 of them NFA.  ACC (odd bases): also AND this base's rows and the
+// previous base's (still in s.d*) into the hit accumulators (3 more ops per
+// word per two bases).
 template <int P, bool HAS_N, bool ACC>
-__device__ __forceinline__ void nfa_base(Nfa& s, uint32_t ph, uint32_t pl, uint32_t H, uint32_t L,
-                                         uint32_t nm, int j) {
-    uint32_t d0n, d1n, d2n, t0, t1, t2, xh, ne, g;
-    if constexpr (!HAS_N && !ACC) {
-        asm(AC_NEQ AC_NFA : AC_OUT : AC_IN);
-    } else if constexpr (!HAS_N && ACC) {
-        asm(AC_NEQ AC_NFA AC_ACC : AC_OUT, AC_ACC_OUT : AC_IN);
-    } else if constexpr (HAS_N && !ACC) {
-        const uint32_t N = sbit(nm, j);
-        asm(AC_NEQ_N AC_NFA : AC_OUT : AC_IN, [N] "s"(N));
-    } else {
-        const uint32_t N = sbit(nm, j);
-        asm(AC_NEQ_N AC_NFA AC_ACC : AC_OUT, AC_ACC_OUT : AC_IN, [N] "s"(N));
+__device__ __forceinline__ void step(Nfa& s, const uint32_t (&ph)[W], const uint32_t (&pl)[W], uint32_t H,
+                                     uint32_t L, uint32_t N) {
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+        const uint32_t xh = HAS_N ? bop3<XOR_OR>(ph[w], H, N) : (ph[w] ^ H);
+        const uint32_t ne = bop3<NEQ>(xh, pl[w], L);
+        const uint32_t d0n = s.s0[w] | ne;
+        const uint32_t t0 = d0n >> P;
+        const uint32_t d1n = bop3<OR_AND>(s.s1[w], ne, bop3<AND3>(s.s0[w], s.d0[w], t0));
+        const uint32_t t1 = d1n >> P;
+        const uint32_t d2n = bop3<OR_AND>(s.s2[w], ne, bop3<AND3>(s.s1[w], s.d1[w], t1));
+        const uint32_t t2 = d2n >> P;
+        if (ACC) {
+            s.a0[w] = bop3<AND3>(s.a0[w], s.d0[w], d0n);
+            s.a1[w] = bop3<AND3>(s.a1[w], s.d1[w], d1n);
+            s.a2[w] = bop3<AND3>(s.a2[w], s.d2[w], d2n);
+        }
+        s.d0[w] = d0n;
+        s.d1[w] = d1n;
+        s.d2[w] = d2n;
+        s.s0[w] = t0;
+        s.s1[w] = t1;
+        s.s2[w] = t2;
     }
-    s.d0 = d0n;
-    s.d1 = d1n;
-    s.d2 = d2n;
-    s.s0 = t0;
-    s.s1 = t1;
-    s.s2 = t2;
 }
 
-// NB (even) bases starting at pair index q of the staged masks; `nm` bit j is
-// the N flag of base j of this group.
+// NB (even) staged bases from pair index q; the next pair is read one pair ahead.
 template <int P, int NB, bool HAS_N>
-__device__ __forceinline__ void run(Nfa& s, uint32_t ph, uint32_t pl, const uint4* __restrict__ hl,
-                                    uint32_t q, uint32_t nm) {
+__device__ __forceinline__ void run(Nfa& s, const uint32_t (&ph)[W], const uint32_t (&pl)[W],
+                                    const Stage& st, uint32_t q) {
+    uint4 cur = st.hl[q];
 #pragma unroll
     for (int j = 0; j < NB; j += 2) {
-        const uint4 m = hl[q + j / 2];
-        nfa_base<P, HAS_N, false>(s, ph, pl, m.x, m.y, nm, j);
-        nfa_base<P, HAS_N, true>(s, ph, pl, m.z, m.w, nm, j + 1);
+        const uint4 nxt = st.hl[min(q + j / 2 + 1, SEG / 2 - 1)];
+        uint32_t n0 = 0, n1 = 0;
+        if constexpr (HAS_N) {
+            n0 = st.n[2 * (q + j / 2)];
+            n1 = st.n[2 * (q + j / 2) + 1];
+        }
+        step<P, HAS_N, false>(s, ph, pl, cur.x, cur.y, n0);
+        step<P, HAS_N, true>(s, ph, pl, cur.z, cur.w, n1);
+        cur = nxt;
+        // Keep the one-pair-ahead read in this pair's block: without the fence
+        // hipcc hoists the whole chunk's reads (32 VGPRs) and occupancy drops.
+        __builtin_amdgcn_sched_barrier(0);
     }
 }
 
 template <int P, int NB>
-__device__ __forceinline__ void run_any(Nfa& s, uint32_t ph, uint32_t pl, const uint4* __restrict__ hl,
-                                        uint32_t q, uint32_t nm) {
-    if (nm == 0u) run<P, NB, false>(s, ph, pl, hl, q, nm);
-    else run<P, NB, true>(s, ph, pl, hl, q, nm);
+__device__ __forceinline__ void run_any(Nfa& s, const uint32_t (&ph)[W], const uint32_t (&pl)[W],
+                                        const Stage& st, uint32_t q, bool has_n) {
+    if (!has_n) run<P, NB, false>(s, ph, pl, st, q);
+    else run<P, NB, true>(s, ph, pl, st, q);
 }
 
-// N flags of bases [b, b + 16) of a window (b a multiple of 16) from the mask image.
-__device__ __forceinline__ uint32_t nflags16(const uint32_t* __restrict__ nmask, uint32_t b) {
-    return (nmask[b >> 5] >> (b & 16u)) & 0xffffu;
+// Lane `lane`'s share of staging window bases [sb, sb + SEG): bases sb + 4*lane .. +3.
+struct Fetch {
+    uint32_t code;  // the code word holding the lane's 4 bases (0 past the window)
+    uint32_t nmw;   // the N-mask word holding them
+};
+
+__device__ __forceinline__ Fetch fetch(const uint32_t* __restrict__ codes, const uint32_t* __restrict__ nmask,
+                                       uint32_t len, uint32_t sb, uint32_t lane) {
+    const uint32_t b = sb + 4u * lane;
+    Fetch f = {0u, 0u};
+    if (b < len) {
+        f.code = codes[b >> 4];
+        f.nmw = nmask[b >> 5];
+    }
+    return f;
+}
+
+// Writes the lane's 4 bases into the stage; returns the wave's ballot of
+// "my 4 bases hold an N" (bit l = bases 4l..4l+3 of the segment).
+__device__ __forceinline__ uint64_t stage_write(Stage& st, const Fetch& f, uint32_t lane) {
+    const uint32_t sh = 8u * (lane & 3u);  // 2 bits per base, 4 bases per lane, 16 per code word
+    const uint32_t c = f.code >> sh;
+    auto sx = [](uint32_t v, int bit) { return (uint32_t)(-(int32_t)((v >> bit) & 1u)); };
+    st.hl[2 * lane] = make_uint4(sx(c, 1), sx(c, 0), sx(c, 3), sx(c, 2));
+    st.hl[2 * lane + 1] = make_uint4(sx(c, 5), sx(c, 4), sx(c, 7), sx(c, 6));
+    const uint32_t nb = (f.nmw >> (4u * (lane & 7u))) & 0xfu;
+    *reinterpret_cast<uint4*>(&st.n[4 * lane]) = make_uint4(sx(nb, 0), sx(nb, 1), sx(nb, 2), sx(nb, 3));
+    return __ballot(nb != 0u);
+}
+
+// 32-bit outer unshuffle (Hacker's Delight 7-2): odd bits to the upper half,
+// even bits to the lower half, order kept.
+__device__ __forceinline__ uint32_t unshuffle32(uint32_t x) {
+    uint32_t t;
+    t = (x ^ (x >> 1)) & 0x22222222u; x ^= t ^ (t << 1);
+    t = (x ^ (x >> 2)) & 0x0c0c0c0cu; x ^= t ^ (t << 2);
+    t = (x ^ (x >> 4)) & 0x00f000f0u; x ^= t ^ (t << 4);
+    t = (x ^ (x >> 8)) & 0x0000ff00u; x ^= t ^ (t << 8);
+    return x;
+}
+
+// Lane masks of P k-mers (dna2int layout, approx_counter.cpp:55-62):
+// character i of pattern p at bit 31 - (i*P + p); ph holds the high bit of
+// each character's 2-bit code, pl the low bit.  No per-character loop for the
+// two packs the baseline configurations use (P = 2: k = 11..16, P = 1: k > 16).
+template <int P>
+__device__ __forceinline__ void build_masks(const uint64_t (&km)[P], uint32_t m, uint32_t& ph, uint32_t& pl) {
+    if constexpr (P == 2) {
+        // Left-aligned 2-bit codes already interleave a pattern's high and low
+        // bits; the second pattern slots in one bit lower.
+        const uint32_t a = (uint32_t)km[0] << (32u - 2u * m), b = (uint32_t)km[1] << (32u - 2u * m);
+        ph = (a & 0xaaaaaaaau) | ((b & 0xaaaaaaaau) >> 1);
+        pl = ((a << 1) & 0xaaaaaaaau) | (b & 0x55555555u);
+    } else if constexpr (P == 1) {
+        const uint64_t x = km[0] << (64u - 2u * m);
+        const uint32_t H = unshuffle32((uint32_t)(x >> 32)), L = unshuffle32((uint32_t)x);
+        ph = (H & 0xffff0000u) | (L >> 16);
+        pl = (H << 16) | (L & 0xffffu);
+    } else {
+        ph = 0;
+        pl = 0;
+#pragma unroll
+        for (int p = 0; p < P; ++p)
+            for (uint32_t i = 0; i < m; ++i) {
+                const uint32_t b = (uint32_t)(km[p] >> (2u * (m - 1u - i))) & 3u;
+                ph |= (b >> 1) << (31u - (i * P + p));
+                pl |= (b & 1u) << (31u - (i * P + p));
+            }
+    }
 }
 
 template <int P>
-__device__ __forceinline__ void count_kernel_body(const LaunchArgs& a, uint4* __restrict__ stage) {
+__device__ __forceinline__ void count_body(const LaunchArgs& a, Stage& st) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t wave = (uint64_t)blockIdx.x * WAVES_PER_BLOCK + wib;
     if (wave >= a.total_waves) return;
-    uint4* __restrict__ hl = stage + wib * (SEG_BASES / 2);
+    stamp(wave, 0);
 
     // Segment lookup (wave-uniform, <= AC_MAX_SEGS entries).
     int si = 0;
@@ -162,110 +241,165 @@ __device__ __forceinline__ void count_kernel_body(const LaunchArgs& a, uint4* __
     const uint32_t wb = (uint32_t)(local / sg.groups);
     const uint32_t m = a.m;
 
-    // Lane constants: character i of pattern p at bit 31 - (i*P + p).
-    uint32_t ph = 0, pl = 0, first = 0, last_bit[P];
-    uint32_t cand[P];
+    // Lane constants: character i of pattern p of word w at bit 31 - (i*P + p).
+    uint32_t ph[W], pl[W], cand[W][P];
+    uint32_t first = 0;
 #pragma unroll
-    for (int p = 0; p < P; ++p) {
-        cand[p] = g * 64u * P + (uint32_t)p * 64u + lane;
-        last_bit[p] = 31u - ((m - 1u) * P + (uint32_t)p);
-        first |= 1u << (31 - p);
-        if (cand[p] < sg.n_kmers) {
-            const uint64_t km = sg.kmers[cand[p]];
-            for (uint32_t i = 0; i < m; ++i) {
-                const uint32_t b = (uint32_t)(km >> (2u * (m - 1u - i))) & 3u;
-                ph |= (b >> 1) << (31u - (i * P + p));
-                pl |= (b & 1u) << (31u - (i * P + p));
-            }
+    for (int p = 0; p < P; ++p) first |= 1u << (31 - p);
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+        uint64_t km[P];
+#pragma unroll
+        for (int p = 0; p < P; ++p) {
+            cand[w][p] = g * (64u * P * W) + (uint32_t)(w * P + p) * 64u + lane;
+            km[p] = cand[w][p] < sg.n_kmers ? sg.kmers[cand[w][p]] : 0ull;
         }
+        build_masks<P>(km, m, ph[w], pl[w]);
     }
     // Initial rows (empty text): R1 has character 0 set, R2 characters 0 and 1.
     const uint32_t d1_init = ~first, d2_init = ~(first | (first >> P));
 
-    uint32_t cnt[P];
+    uint32_t cnt[W][P];
 #pragma unroll
-    for (int p = 0; p < P; ++p) cnt[p] = 0;
+    for (int w = 0; w < W; ++w)
+#pragma unroll
+        for (int p = 0; p < P; ++p) cnt[w][p] = 0;
 
+    stamp(wave, 1);
     const uint32_t w_begin = wb * sg.wpw;
     const uint32_t w_end = min(sg.n_windows, w_begin + sg.wpw);
+
+    // Window pipeline: window w+1's first segment is fetched while w is counted.
+    auto valid = [&](uint64_t base, uint32_t len) { return !(base & 31u) && base + len <= sg.n_bases; };
+    uint64_t nbase = 0;
+    uint32_t nlen = 0;
+    Fetch nf = {0u, 0u};
+    if (w_begin < w_end) {
+        nbase = sg.start[w_begin];
+        nlen = sg.length[w_begin];
+        if (valid(nbase, nlen)) nf = fetch(sg.codes + (nbase >> 4), sg.nmask + (nbase >> 5), nlen, 0, lane);
+    }
     for (uint32_t w = w_begin; w < w_end; ++w) {
-        const uint64_t base = sg.start[w];
-        const uint32_t len = sg.length[w];
-        if ((base & 31u) || base + len > sg.n_bases) continue;  // malformed window: never read outside the image
+        const uint64_t base = nbase;
+        const uint32_t len = nlen;
+        const Fetch f0 = nf;
+        if (w + 1 < w_end) {
+            nbase = sg.start[w + 1];
+            nlen = sg.length[w + 1];
+            if (valid(nbase, nlen)) nf = fetch(sg.codes + (nbase >> 4), sg.nmask + (nbase >> 5), nlen, 0, lane);
+        }
+        if (!valid(base, len)) continue;  // malformed window: never read outside the image
         const uint32_t* __restrict__ codes = sg.codes + (base >> 4);
         const uint32_t* __restrict__ nmask = sg.nmask + (base >> 5);
         Nfa s;
-        s.d0 = ~0u;
-        s.d1 = d1_init;
-        s.d2 = d2_init;
-        s.s0 = ~0u >> P;
-        s.s1 = d1_init >> P;
-        s.s2 = d2_init >> P;
-        s.a0 = ~0u;
-        s.a1 = d1_init;
-        s.a2 = d2_init;  // for k <= 2 the empty alignment already reaches the last character
-        for (uint32_t sb = 0; sb < len; sb += SEG_BASES) {
-            // Stage bases [sb, sb + 128) as (H, L) mask pairs: lane l expands bases sb+2l, sb+2l+1.
-            {
-                const uint32_t b = sb + 2u * lane;
-                const uint32_t code = b < len ? codes[b >> 4] : 0u;
-                const int sh = (int)(2u * (b & 15u));
-                uint4 v;
-                v.x = sbit(code, sh + 1);
-                v.y = sbit(code, sh);
-                v.z = sbit(code, sh + 3);
-                v.w = sbit(code, sh + 2);
-                hl[lane] = v;
-            }
-            const uint32_t nb = min(SEG_BASES, len - sb);
+#pragma unroll
+        for (int x = 0; x < W; ++x) {
+            s.d0[x] = ~0u;
+            s.d1[x] = d1_init;
+            s.d2[x] = d2_init;
+            s.s0[x] = ~0u >> P;
+            s.s1[x] = d1_init >> P;
+            s.s2[x] = d2_init >> P;
+            s.a0[x] = ~0u;
+            s.a1[x] = d1_init;
+            s.a2[x] = d2_init;  // for k <= 2 the empty alignment already reaches the last character
+        }
+        for (uint32_t sb = 0; sb < len; sb += SEG) {
+            const Fetch f = sb == 0 ? f0 : fetch(codes, nmask, len, sb, lane);
+            const uint64_t any_n = stage_write(st, f, lane);
+            const uint32_t nb = min(SEG, len - sb);
             const uint32_t nfull = nb >> 4;
             for (uint32_t ch = 0; ch < nfull; ++ch)
-                run_any<P, 16>(s, ph, pl, hl, ch * 8u, nflags16(nmask, sb + ch * 16u));
+                run_any<P, 16>(s, ph, pl, st, ch * 8u, ((any_n >> (4u * ch)) & 0xfu) != 0u);
             const uint32_t rem = nb & 15u;
             if (rem) {
-                uint32_t q = nfull * 8u;
-                uint32_t nm = nflags16(nmask, sb + nfull * 16u);
+                uint32_t o = nfull * 16u;  // base offset in the segment
+                const uint32_t fl = (uint32_t)(any_n >> (o >> 2)) & 0xfu;  // 4-base groups o/4 .. o/4+3
+                uint32_t gi = 0;                                        // group index within fl
                 if (rem & 8u) {
-                    run_any<P, 8>(s, ph, pl, hl, q, nm);
-                    q += 4u;
-                    nm >>= 8;
+                    run_any<P, 8>(s, ph, pl, st, o / 2, (fl & 3u) != 0u);
+                    o += 8u;
+                    gi += 2u;
                 }
                 if (rem & 4u) {
-                    run_any<P, 4>(s, ph, pl, hl, q, nm);
-                    q += 2u;
-                    nm >>= 4;
+                    run_any<P, 4>(s, ph, pl, st, o / 2, ((fl >> gi) & 1u) != 0u);
+                    o += 4u;
+                    gi += 1u;
                 }
                 if (rem & 2u) {
-                    run_any<P, 2>(s, ph, pl, hl, q, nm);
-                    q += 1u;
-                    nm >>= 2;
+                    run_any<P, 2>(s, ph, pl, st, o / 2, ((fl >> gi) & 1u) != 0u);
+                    o += 2u;
                 }
                 if (rem & 1u) {
-                    const uint4 mm = hl[q];
-                    nfa_base<P, true, false>(s, ph, pl, mm.x, mm.y, nm, 0);
-                    s.a0 &= s.d0;
-                    s.a1 &= s.d1;
-                    s.a2 &= s.d2;
+                    const uint4 mm = st.hl[o / 2];
+                    step<P, true, false>(s, ph, pl, mm.x, mm.y, st.n[o]);
+#pragma unroll
+                    for (int x = 0; x < W; ++x) {
+                        s.a0[x] &= s.d0[x];
+                        s.a1[x] &= s.d1[x];
+                        s.a2[x] &= s.d2[x];
+                    }
                 }
             }
         }
 #pragma unroll
-        for (int p = 0; p < P; ++p)
-            cnt[p] += 3u - ((s.a0 >> last_bit[p]) & 1u) - ((s.a1 >> last_bit[p]) & 1u) -
-                      ((s.a2 >> last_bit[p]) & 1u);
+        for (int x = 0; x < W; ++x) {
+#pragma unroll
+            for (int p = 0; p < P; ++p) {
+                const uint32_t lb = 31u - ((m - 1u) * P + (uint32_t)p);
+                cnt[x][p] += 3u - ((s.a0[x] >> lb) & 1u) - ((s.a1[x] >> lb) & 1u) - ((s.a2[x] >> lb) & 1u);
+            }
+        }
     }
 
+    stamp(wave, 2);
 #pragma unroll
-    for (int p = 0; p < P; ++p)
-        if (cand[p] < sg.n_kmers && cnt[p]) atomicAdd(&sg.counts[cand[p]], cnt[p]);
+    for (int x = 0; x < W; ++x)
+#pragma unroll
+        for (int p = 0; p < P; ++p)
+#ifdef AC_TIMING_NO_ATOMICS  // timing-only build: results discarded (kept live by an impossible store)
+            if (cand[x][p] < sg.n_kmers && cnt[x][p] == 0xdeadbeefu) sg.counts[cand[x][p]] = 1u;
+#else
+            if (cand[x][p] < sg.n_kmers && cnt[x][p]) atomicAdd(&sg.counts[cand[x][p]], cnt[x][p]);
+#endif
+    stamp(wave, 3);
 }
 
 }  // namespace
 
 template <int P>
-__global__ __launch_bounds__(64 * WAVES_PER_BLOCK) void wm2_count_kernel(LaunchArgs a) {
-    __shared__ uint4 stage[WAVES_PER_BLOCK * (SEG_BASES / 2)];
-    count_kernel_body<P>(a, stage);
+__global__ __launch_bounds__(64 * WAVES_PER_BLOCK, AC_MIN_WAVES_PER_SIMD) void wm2_count_kernel(LaunchArgs a) {
+    __shared__ Stage stage[WAVES_PER_BLOCK];
+    count_body<P>(a, stage[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)]);
+}
+
+namespace {
+template <int P>
+hipError_t occupancy(int cu_count, uint32_t* waves) {
+    int blocks = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, wm2_count_kernel<P>, 64 * WAVES_PER_BLOCK, 0);
+    if (e != hipSuccess) return e;
+    if (blocks < 1) blocks = 1;
+    *waves = (uint32_t)blocks * WAVES_PER_BLOCK * (uint32_t)cu_count;
+    return hipSuccess;
+}
+}  // namespace
+
+#ifdef AC_STAMPS
+hipError_t debug_stamps(void* host, size_t bytes) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), bytes < sizeof(g_stamps) ? bytes : sizeof(g_stamps), 0,
+                               hipMemcpyDeviceToHost);
+}
+#endif
+
+hipError_t resident_waves(uint32_t P, int cu_count, uint32_t* waves) {
+    switch (P) {
+        case 1: return occupancy<1>(cu_count, waves);
+        case 2: return occupancy<2>(cu_count, waves);
+        case 3: return occupancy<3>(cu_count, waves);
+        case 4: return occupancy<4>(cu_count, waves);
+        default: return hipErrorInvalidValue;
+    }
 }
 
 hipError_t launch_wm2_count(const LaunchArgs& args, hipStream_t stream) {
