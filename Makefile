@@ -1,5 +1,7 @@
 # Build of the MI355X approximate counter (gfx950).  `make` builds:
-#   approx_counter_amd/lib/libapprox_counter_amd.so   C-ABI + HIP kernel
+#   approx_counter_amd/lib/libapprox_counter_amd.so   C-ABI + HIP kernel (the hot path)
+#   approx_counter_amd/lib/libac_host.so              host stages' C ABI (tests of the CLI's CPU stages)
+#   approx_counter_amd/bin/adaptFinder                the drop-in CLI (host C++ + the C-ABI library)
 #   oracle/_build/libac_oracle.so                     CPU oracle (tests only)
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
@@ -13,7 +15,16 @@ OBJDIR := build/obj
 DEV_SRC := $(CSRC)/wm_count.hip $(CSRC)/capi.cpp
 HDRS := include/approx_counter_amd.h $(CSRC)/wm_count.h
 
-all: $(LIB) oracle
+CXX ?= g++
+HOST_CXXFLAGS ?= -O3 -std=c++17 -fPIC -Wall -Wextra
+HOSTDIR := $(CSRC)/host
+HOST_SRC := $(HOSTDIR)/host_stages.cpp
+HOST_HDRS := $(HOSTDIR)/host_stages.h include/approx_counter_host.h include/approx_counter_amd.h
+HOSTLIB := $(LIBDIR)/libac_host.so
+BINDIR := $(PKG)/bin
+CLI := $(BINDIR)/adaptFinder
+
+all: $(LIB) $(HOSTLIB) $(CLI) oracle
 
 $(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
@@ -27,6 +38,15 @@ $(LIB): $(OBJDIR)/wm_count.o $(OBJDIR)/capi.o
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
 
+$(HOSTLIB): $(HOST_SRC) $(HOSTDIR)/host_capi.cpp $(HOST_HDRS)
+	@mkdir -p $(LIBDIR)
+	$(CXX) $(HOST_CXXFLAGS) -Iinclude -I$(HOSTDIR) -shared -o $@ $(HOST_SRC) $(HOSTDIR)/host_capi.cpp
+
+$(CLI): $(HOSTDIR)/adaptfinder.cpp $(HOST_SRC) $(HOST_HDRS) $(LIB)
+	@mkdir -p $(BINDIR)
+	$(CXX) $(HOST_CXXFLAGS) -Iinclude -I$(HOSTDIR) -o $@ $(HOSTDIR)/adaptfinder.cpp $(HOST_SRC) \
+		-L$(LIBDIR) -lapprox_counter_amd -Wl,-rpath,'$$ORIGIN/../lib' -pthread
+
 oracle:
 	$(MAKE) -s -C oracle
 
@@ -35,6 +55,6 @@ asm: $(CSRC)/wm_count.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -Iinclude -I$(CSRC) --cuda-device-only -S $< -o build/asm/wm_count.s
 
 clean:
-	rm -rf build $(LIBDIR) oracle/_build
+	rm -rf build $(LIBDIR) $(BINDIR) oracle/_build
 
 .PHONY: all oracle asm clean

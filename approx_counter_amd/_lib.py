@@ -53,6 +53,7 @@ def load():
     L = ctypes.CDLL(LIB_PATH)
     vp = ctypes.c_void_p
     L.ac_abi_version.restype = ctypes.c_int
+    L.ac_device_count.restype = ctypes.c_int
     L.ac_last_error.argtypes = [vp]
     L.ac_last_error.restype = ctypes.c_char_p
     L.ac_create.argtypes = [ctypes.POINTER(vp), ctypes.c_int]

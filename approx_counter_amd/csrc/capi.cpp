@@ -141,6 +141,12 @@ extern "C" {
 
 int ac_abi_version(void) { return AC_ABI_VERSION; }
 
+int ac_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
 const char* ac_last_error(const ac_ctx* ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
 
 ac_status ac_create(ac_ctx** out, int device) {

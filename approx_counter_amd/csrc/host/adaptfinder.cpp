@@ -1,0 +1,448 @@
+// adaptfinder.cpp -- the drop-in command line (binary `adaptFinder`).
+//
+// Same flags, config file, precedence, defaults, messages and output files as
+// qbonenfant/approx_counter's main (approx_counter.cpp:604-958), so that
+// Porechop_ABI can run it unchanged.  The approximate count (errorCount,
+// approx_counter.cpp:531-601) goes through the C ABI of
+// include/approx_counter_amd.h to the HIP kernel; there is no CPU fallback.
+//
+// Extensions (not in the reference, documented in DESIGN.md):
+//   -g, --gpus N    shard the sampled windows over N GPUs of this node (default 1)
+//   --seed N        seed the read sampling (the reference always uses std::random_device)
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <iostream>
+#include <map>
+#include <random>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "approx_counter_amd.h"
+#include "host_stages.h"
+
+using namespace achost;
+
+namespace {
+
+const auto boot_time = std::chrono::steady_clock::now();
+
+// print (approx_counter.cpp:85-94)
+template <typename T>
+void print(const T& text, int tab = 0) {
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - boot_time).count();
+    std::cout << "[" << ms << " ms]\t";
+    for (int i = 0; i < tab; ++i) std::cout << "\t";
+    std::cout << text << std::endl;
+}
+
+// ---------------------------------------------------------------------------
+// Argument parsing with the SeqAn ArgumentParser spellings (get_args, 604-669)
+// ---------------------------------------------------------------------------
+enum class Kind { Int, Double, String, Flag };
+struct Opt {
+    const char* s;
+    const char* l;
+    Kind kind;
+    const char* help;
+};
+const Opt OPTS[] = {
+    {"lc", "low_complexity", Kind::Double, "low complexity filter threshold (for k=16), default 1.5"},
+    {"sn", "sample_n", Kind::Int, "sample n sequences from dataset, default 10k sequences"},
+    {"sl", "sample_length", Kind::Int, "size of the sampled portion, default 100 bases"},
+    {"nt", "nb_thread", Kind::Int, "Number of thread to work with, default is 4"},
+    {"k", "kmer_size", Kind::Int, "Size of the kmers, default is 16"},
+    {"lim", "limit", Kind::Int, "limit the number of kmer used after initial counting, default is 500"},
+    {"mr", "multi_run", Kind::Int, "Number of time the count must be performed. Each count is exported separately."},
+    {"v", "verbosity", Kind::Int, "Level of details printed out"},
+    {"e", "exact_file", Kind::String, "path to export the exact k-mer count, if needed. Default: no export"},
+    {"conf", "config", Kind::String, "path to the config file"},
+    {"fk", "forbidden_kmer", Kind::String,
+     "take a file containing 'forbidden' kmers, excluding them from the search pool. One kmer per line."},
+    {"sk", "solid_km", Kind::Int,
+     "Use solid kmer instead of most frequents. This option will override sample number (-sn / --sample_n)."},
+    {"se", "skip_end", Kind::Flag,
+     "Skip end adapter ressearch (only search start). /!\\ If this option is set, and adaptFinder is run trough "
+     "PorechopABI, the --guess_only / -go MUST be set."},
+    {"o", "out_file", Kind::String, "path to the output file, default is ./out.txt"},
+    {"g", "gpus", Kind::Int, "[MI355X build] number of GPUs of this node to shard the count over, default 1"},
+    {"", "seed", Kind::Int, "[MI355X build] seed of the read sampling, default: std::random_device"},
+};
+
+struct Args {
+    std::map<std::string, std::string> val;  // by long name
+    std::string input;
+};
+
+void usage(std::ostream& os) {
+    os << "adaptFinder\n===========\n\nSYNOPSIS\n    adaptFinder [OPTIONS] \"input filename\"\n\n"
+          "REQUIRED ARGUMENTS\n    input filename STRING\n\nOPTIONS\n    -h, --help\n          Display the help message.\n";
+    for (const Opt& o : OPTS) {
+        os << "    ";
+        if (*o.s) os << "-" << o.s << ", ";
+        os << "--" << o.l;
+        switch (o.kind) {
+            case Kind::Int: os << " INTEGER"; break;
+            case Kind::Double: os << " DOUBLE"; break;
+            case Kind::String: os << " STRING"; break;
+            case Kind::Flag: break;
+        }
+        os << "\n          " << o.help << "\n";
+    }
+}
+
+bool valid_value(Kind kind, const std::string& v) {
+    if (v.empty()) return false;
+    char* end = nullptr;
+    if (kind == Kind::Int) {
+        std::strtoll(v.c_str(), &end, 10);
+        return *end == '\0';
+    }
+    if (kind == Kind::Double) {
+        std::strtod(v.c_str(), &end);
+        return *end == '\0';
+    }
+    return true;
+}
+
+// Returns 0 = OK, 1 = parse error, 2 = help printed.
+int parse_args(int argc, char const** argv, Args& a) {
+    std::vector<std::string> positional;
+    for (int i = 1; i < argc; ++i) {
+        std::string t = argv[i];
+        if (t == "-h" || t == "--help") {
+            usage(std::cout);
+            return 2;
+        }
+        if (t.size() > 1 && t[0] == '-' && !(t.size() > 1 && (std::isdigit((unsigned char)t[1]) || t[1] == '.'))) {
+            std::string name = t.substr(t[1] == '-' ? 2 : 1), value;
+            bool has_inline = false;
+            const size_t eq = name.find('=');
+            if (eq != std::string::npos) {
+                value = name.substr(eq + 1);
+                name = name.substr(0, eq);
+                has_inline = true;
+            }
+            const Opt* opt = nullptr;
+            for (const Opt& o : OPTS)
+                if ((t[1] == '-' && name == o.l) || (t[1] != '-' && *o.s && name == o.s)) opt = &o;
+            if (!opt) {
+                std::cerr << "adaptFinder: illegal option -- " << name << "\n";
+                return 1;
+            }
+            if (opt->kind == Kind::Flag) {
+                a.val[opt->l] = "1";
+                continue;
+            }
+            if (!has_inline) {
+                if (i + 1 >= argc) {
+                    std::cerr << "adaptFinder: option requires an argument -- " << name << "\n";
+                    return 1;
+                }
+                value = argv[++i];
+            }
+            if (!valid_value(opt->kind, value)) {
+                std::cerr << "adaptFinder: the given value '" << value << "' cannot be casted to "
+                          << (opt->kind == Kind::Int ? "integer" : "double") << "\n";
+                return 1;
+            }
+            a.val[opt->l] = value;
+        } else {
+            positional.push_back(t);
+        }
+    }
+    if (positional.size() != 1) {
+        std::cerr << "adaptFinder: " << (positional.empty() ? "Not enough" : "Too many") << " arguments given.\n";
+        return 1;
+    }
+    a.input = positional[0];
+    return 0;
+}
+
+template <typename T>
+void get_option(const Args& a, const char* long_name, T& out);
+template <>
+void get_option(const Args& a, const char* n, uint64_t& out) {
+    auto it = a.val.find(n);
+    if (it != a.val.end()) out = (uint64_t)std::strtoll(it->second.c_str(), nullptr, 10);
+}
+template <>
+void get_option(const Args& a, const char* n, float& out) {
+    auto it = a.val.find(n);
+    if (it != a.val.end()) out = (float)std::strtod(it->second.c_str(), nullptr);
+}
+template <>
+void get_option(const Args& a, const char* n, std::string& out) {
+    auto it = a.val.find(n);
+    if (it != a.val.end()) out = it->second;
+}
+
+// ---------------------------------------------------------------------------
+// errorCount (approx_counter.cpp:531-601) through the C ABI, windows sharded
+// over n_gpus devices (contiguous ranges balanced by bases), counts summed.
+// ---------------------------------------------------------------------------
+struct Packed {
+    std::vector<uint32_t> codes, nmask, length;
+    std::vector<uint64_t> start;
+    uint64_t n_bases = 32;
+    ac_windows view() const {
+        return ac_windows{codes.data(), nmask.data(), start.data(), length.data(), (uint32_t)length.size(), n_bases};
+    }
+};
+
+Packed pack(const SeqSet& s, size_t lo, size_t hi) {
+    Packed p;
+    std::vector<uint64_t> src(hi - lo);
+    std::vector<uint32_t> len(hi - lo);
+    for (size_t i = lo; i < hi; ++i) {
+        src[i - lo] = s.offset[i];
+        len[i - lo] = s.length[i];
+    }
+    p.n_bases = ac_image_bases(len.data(), (uint32_t)len.size());
+    p.codes.assign(p.n_bases / 16, 0);
+    p.nmask.assign(p.n_bases / 32, 0);
+    p.start.assign(std::max<size_t>(hi - lo, 1), 0);
+    p.length.assign(std::max<size_t>(hi - lo, 1), 0);
+    if (ac_pack_windows(s.bases.data(), src.data(), len.data(), (uint32_t)len.size(), p.codes.data(), p.nmask.data(),
+                        p.start.data(), p.length.data(), p.n_bases) != AC_OK)
+        throw std::runtime_error(std::string("window packing failed: ") + ac_last_error(nullptr));
+    p.start.resize(hi - lo);
+    p.length.resize(hi - lo);
+    return p;
+}
+
+struct Devices {
+    std::vector<ac_ctx*> ctx;
+    ~Devices() {
+        for (ac_ctx* c : ctx) ac_destroy(c);
+    }
+};
+
+pair_vector error_count(Devices& dev, const SeqSet& sample, const pair_vector& first_n, uint32_t k) {
+    const size_t n = first_n.size();
+    pair_vector out(n);
+    if (n == 0) return out;
+    std::vector<uint64_t> kmers(n);
+    for (size_t i = 0; i < n; ++i) kmers[i] = first_n[i].first;
+    const size_t G = dev.ctx.size();
+    // shard boundaries balanced by Σ window length
+    uint64_t total = 0;
+    for (uint32_t l : sample.length) total += l;
+    std::vector<size_t> cut(G + 1, sample.size());
+    cut[0] = 0;
+    {
+        uint64_t acc = 0;
+        size_t g = 1;
+        for (size_t i = 0; i < sample.size() && g < G; ++i) {
+            acc += sample.length[i];
+            while (g < G && acc * G >= total * g) cut[g++] = i + 1;
+        }
+    }
+    std::vector<std::vector<uint64_t>> part(G, std::vector<uint64_t>(n, 0));
+    std::vector<std::string> err(G);
+    std::vector<std::thread> th;
+    for (size_t g = 0; g < G; ++g) {
+        th.emplace_back([&, g] {
+            try {
+                Packed p = pack(sample, cut[g], cut[g + 1]);
+                const ac_windows w = p.view();
+                if (ac_error_count(dev.ctx[g], k, kmers.data(), (uint32_t)n, &w, part[g].data()) != AC_OK)
+                    err[g] = ac_last_error(dev.ctx[g]);
+            } catch (const std::exception& e) {
+                err[g] = e.what();
+            }
+        });
+    }
+    for (auto& t : th) t.join();
+    for (size_t g = 0; g < G; ++g)
+        if (!err[g].empty()) throw std::runtime_error("approximate count failed on GPU " + std::to_string(g) + ": " + err[g]);
+    for (size_t i = 0; i < n; ++i) {
+        uint64_t s = 0;
+        for (size_t g = 0; g < G; ++g) s += part[g][i];
+        out[i] = {kmers[i], s};
+    }
+    return out;
+}
+
+}  // namespace
+
+int main(int argc, char const** argv) {
+    Args args;
+    const int pr = parse_args(argc, argv, args);
+    if (pr != 0) return pr == 1;
+
+    // Defaults (approx_counter.cpp:700-715)
+    std::string output = "out.txt", exact_out, config_file, forbid_kmer;
+    uint64_t solid_km = 0, nb_thread = 4, k = 16, sl = 100, sn = 40000, limit = 500, v = 1, nb_of_runs = 1;
+    float param_lc = 1.0f, lc = 1.0f;
+    bool skip_end = false;
+    uint64_t n_gpus = 1;
+    std::string seed_str;
+
+    // Config file (721-737): CLI > config > defaults
+    get_option(args, "config", config_file);
+    if (!config_file.empty()) {
+        bool opened = false;
+        arg_map p = parse_config(config_file, &opened);
+        if (!opened) std::cerr << "/!\\ WARNING: Could not open config file\n";
+        param_lc = p.count("lc") ? std::stof(p["lc"]) : lc;
+        k = p.count("k") ? std::stoi(p["k"]) : k;
+        v = p.count("v") ? std::stoi(p["v"]) : v;
+        sn = p.count("sn") ? std::stoi(p["sn"]) : sn;
+        sl = p.count("sl") ? std::stoi(p["sl"]) : sl;
+        limit = p.count("lim") ? std::stoi(p["lim"]) : limit;
+        nb_thread = p.count("nt") ? std::stoi(p["nt"]) : nb_thread;
+        solid_km = p.count("sk") ? std::stoi(p["sk"]) : solid_km;
+        skip_end = p.count("se") > 0;
+        forbid_kmer = p.count("fk") ? p["fk"] : forbid_kmer;
+        exact_out = p.count("e") ? p["e"] : exact_out;
+        nb_of_runs = p.count("mr") ? std::stoi(p["mr"]) : nb_of_runs;
+    }
+    get_option(args, "limit", limit);
+    get_option(args, "low_complexity", param_lc);
+    get_option(args, "kmer_size", k);
+    get_option(args, "verbosity", v);
+    get_option(args, "sample_length", sl);
+    get_option(args, "sample_n", sn);
+    get_option(args, "nb_thread", nb_thread);
+    get_option(args, "out_file", output);
+    get_option(args, "exact_file", exact_out);
+    get_option(args, "forbidden_kmer", forbid_kmer);
+    get_option(args, "solid_km", solid_km);
+    get_option(args, "multi_run", nb_of_runs);
+    get_option(args, "gpus", n_gpus);
+    get_option(args, "seed", seed_str);
+    skip_end = skip_end || args.val.count("skip_end");
+    const std::string input_file = args.input;
+
+    kmer_set forbidden;
+    if (!forbid_kmer.empty()) {
+        print("Parsing the fobidden kmer list");
+        if (!parse_kmer_list(forbid_kmer, forbidden)) {
+            std::cerr << "/!\\ ERROR: COULD NOT OPEN EXCLUDED KMER FILE, must quit\n";
+            std::exit(1);
+        }
+    }
+    const int mr_v = (nb_of_runs > 1 && v < 2) ? 0 : (int)v;
+    const std::string warning = "/!\\ WARNING: ", error_pref = "/!\\ ERROR: ";
+    if (k < 2 || k > 32) throw std::invalid_argument(error_pref + "kmer size must be between 2 and 32 (included)");
+    if (k > sl) throw std::invalid_argument(error_pref + "kmer size must be smaller than the sampling length (k <= sl)");
+    lc = adjust_threshold(param_lc, 16, (uint32_t)k);
+
+    if (v > 0) {
+        std::cout << "Kmer size:             " << k << std::endl;
+        std::cout << "Sampled sequences:     " << sn << std::endl;
+        std::cout << "Sampling length        " << sl << std::endl;
+        std::cout << "LC filter threshold:   " << param_lc << std::endl;
+        std::cout << "Adjusted LC threshold: " << lc << std::endl;
+        std::cout << "Nb thread:             " << nb_thread << std::endl;
+        if (solid_km != 0) std::cout << "Solid kmers:           " << solid_km << std::endl;
+        else std::cout << "Number of kept kmer:   " << limit << std::endl;
+        std::cout << "Number of runs:        " << nb_of_runs << std::endl;
+        std::cout << "Verbosity level:       " << v << std::endl;
+    }
+    int tab_level = 0;
+    if (v > 0 && nb_of_runs > 1) std::cout << "\nA total of " << nb_of_runs << " runs will be performed." << std::endl;
+
+    std::vector<std::string> ids;
+    SeqSet seqs;
+    if (v > 0) print("Parsing FASTA file", tab_level);
+    read_records(input_file, ids, seqs);  // throws (uncaught, like SeqAn's IOError) on an unreadable file
+    if (v > 0) print("Number of sequences found: " + std::to_string(seqs.size()) + ".", tab_level);
+
+    // The GPU contexts (the reference builds its index inside errorCount; the
+    // device set is opened once here).
+    Devices dev;
+    std::mt19937 rng(seed_str.empty() ? std::random_device{}() : (uint32_t)std::strtoull(seed_str.c_str(), nullptr, 10));
+
+    for (uint64_t run = 0; run < nb_of_runs; ++run) {
+        const std::string run_suffix = "_" + std::to_string(run);
+        if (nb_of_runs > 1 && v > 0) std::cout << "Starting run number " << run + 1 << std::endl;
+        if (sn > seqs.size()) {
+            std::cerr << warning << "Sequence set too small for the requested sample size\n";
+            std::cerr << warning << "The whole set will be used.\n";
+            sn = seqs.size();
+        }
+        bool bottom = false;
+        tab_level += 1;
+        for (const std::string which_end : {"start", "end"}) {
+            if (v > 0) print("Working on sequence " + which_end + ".", tab_level - 1);
+            if (mr_v > 0) print("Sampling", tab_level);
+            if (mr_v > 0) print(bottom ? "Sampling the ends of reads" : "Sampling the start of reads", 1);
+            SeqSet sample = sample_sequences(seqs, sn, sl, bottom, rng);
+            if (mr_v > 0) print("Sampled " + std::to_string(sample.size()) + " sequences", 1);
+            if (mr_v > 0) print("Exact k-mer count", tab_level);
+            uint64_t had_n = 0;
+            pair_vector count = count_kmers(sample, (uint32_t)k, lc, forbidden, &had_n);
+            if (had_n > 0) {
+                std::cerr << "/!\\ WARNING: This dataset contained sequences with 'N' symbols. ";
+                std::cerr << "/!\\ WARNING: Current implementation ignores k-mers containing 'N'.";
+                std::cerr << "/!\\ WARNING: A total of " << had_n << " k-mers were ignored." << std::endl;
+            }
+            if (mr_v > 0) print("Number of kmer found: " + std::to_string(count.size()), tab_level);
+            pair_vector first_n;
+            if (solid_km != 0) {
+                if (mr_v > 0) print("Keeping solid k-mer", tab_level);
+                first_n = get_solid_kmers(std::move(count), solid_km, (uint32_t)k);
+            } else {
+                if (mr_v > 0) print("Keeping most frequent k-mer", tab_level);
+                first_n = get_most_frequent(std::move(count), limit, (uint32_t)k);
+            }
+            if (mr_v > 0) print("Number of kmer kept:  " + std::to_string(first_n.size()), tab_level);
+            if (!exact_out.empty()) {
+                if (mr_v > 0) print("Exporting exact kmer count", tab_level);
+                if (!export_counter(first_n, (uint32_t)k, exact_out + run_suffix + "." + which_end)) {
+                    std::cerr << error_pref + "Failed to export exact k-mer count" << std::endl;
+                    std::cerr << "Path: " << exact_out + run_suffix + "." + which_end << std::endl;
+                    return 1;
+                }
+            }
+            if (mr_v > 0) print("Approximate k-mer count", tab_level);
+            pair_vector error_counter;
+            try {
+                if (dev.ctx.empty()) {
+                    // -g N: N window shards, shard g on device g mod (visible devices).
+                    if (n_gpus < 1) n_gpus = 1;
+                    const int n_dev = ac_device_count();
+                    if (n_dev < 1) throw std::runtime_error("no HIP device available (the approximate count runs on the GPU only)");
+                    if ((int)n_gpus > n_dev)
+                        std::cerr << warning << n_gpus << " shards requested on " << n_dev << " visible GPU(s)\n";
+                    for (uint64_t g = 0; g < n_gpus; ++g) {
+                        ac_ctx* c = nullptr;
+                        if (ac_create(&c, (int)(g % (uint64_t)n_dev)) != AC_OK)
+                            throw std::runtime_error(ac_last_error(nullptr));
+                        dev.ctx.push_back(c);
+                    }
+                }
+                error_counter = error_count(dev, sample, first_n, (uint32_t)k);
+            } catch (const std::exception& e) {
+                std::cerr << error_pref << "approximate count failed: " << e.what() << std::endl;
+                return 1;
+            }
+            pair_vector sorted_error_count = get_most_frequent(std::move(error_counter), limit, (uint32_t)k);
+            if (mr_v > 0) print("Exporting approximate count", tab_level);
+            if (!export_counter(sorted_error_count, (uint32_t)k, output + run_suffix + "." + which_end)) {
+                std::cerr << error_pref + "Failed to export approximate k-mer count" << std::endl;
+                std::cerr << "Path: " << output + run_suffix + "." + which_end << std::endl;
+                return 1;
+            }
+            if (mr_v > 0) print("Done", tab_level);
+            // approx_counter.cpp:943-951: the break only happens when verbose
+            // (without it the second pass samples read STARTS again and writes
+            // them to the .end file -- kept for drop-in fidelity).
+            if (skip_end) {
+                if (mr_v > 0) {
+                    print("Skipping end adapter ressearch");
+                    break;
+                }
+            } else {
+                bottom = true;
+            }
+        }
+        tab_level--;
+    }
+    return 0;
+}

@@ -1,0 +1,363 @@
+// host_stages.cpp -- see host_stages.h.  Product code for the CLI's CPU stages.
+#include "host_stages.h"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <numeric>
+#include <stdexcept>
+
+namespace achost {
+
+void SeqSet::add(const uint8_t* s, uint32_t n) {
+    offset.push_back(bases.size());
+    length.push_back(n);
+    bases.insert(bases.end(), s, s + n);
+}
+
+void SeqSet::clear() {
+    bases.clear();
+    offset.clear();
+    length.clear();
+}
+
+uint8_t dna5(char c) {
+    switch (c) {
+        case 'A': case 'a': return 0;
+        case 'C': case 'c': return 1;
+        case 'G': case 'g': return 2;
+        case 'T': case 't': case 'U': case 'u': return 3;
+        default: return 4;
+    }
+}
+
+namespace {
+
+// Streaming line reader that copes with '\r\n' and a missing final newline.
+struct LineReader {
+    std::FILE* f;
+    std::vector<char> buf = std::vector<char>(1 << 20);
+    size_t pos = 0, end = 0;
+    bool eof = false;
+    bool get(std::string& line) {
+        line.clear();
+        for (;;) {
+            if (pos == end) {
+                if (eof) return !line.empty();
+                end = std::fread(buf.data(), 1, buf.size(), f);
+                pos = 0;
+                if (end == 0) {
+                    eof = true;
+                    return !line.empty();
+                }
+            }
+            const char* s = buf.data() + pos;
+            const char* nl = static_cast<const char*>(std::memchr(s, '\n', end - pos));
+            if (nl) {
+                line.append(s, nl - s);
+                pos += (nl - s) + 1;
+                if (!line.empty() && line.back() == '\r') line.pop_back();
+                return true;
+            }
+            line.append(s, end - pos);
+            pos = end;
+        }
+    }
+};
+
+void append_bases(std::vector<uint8_t>& out, const std::string& line) {
+    for (char c : line) {
+        if (c == ' ' || c == '\t' || c == '\r') continue;  // SeqAn skips blanks inside sequence lines
+        out.push_back(dna5(c));
+    }
+}
+
+}  // namespace
+
+void read_records(const std::string& path, std::vector<std::string>& ids, SeqSet& seqs) {
+    std::FILE* f = std::fopen(path.c_str(), "rb");
+    if (!f) throw std::runtime_error("Could not open input file: " + path);
+    LineReader r{f};
+    std::string line;
+    std::vector<uint8_t> cur;
+    // Skip leading empty lines, find the format from the first record marker.
+    bool have = false;
+    while ((have = r.get(line)) && line.empty()) {
+    }
+    if (!have) {
+        std::fclose(f);
+        return;  // empty file: no records
+    }
+    if (line[0] == '>') {
+        std::string id = line.substr(1);
+        for (;;) {
+            const bool more = r.get(line);
+            if (!more || (!line.empty() && line[0] == '>')) {
+                ids.push_back(id);
+                seqs.add(cur.data(), (uint32_t)cur.size());
+                cur.clear();
+                if (!more) break;
+                id = line.substr(1);
+                continue;
+            }
+            append_bases(cur, line);
+        }
+    } else if (line[0] == '@') {
+        for (;;) {
+            if (line.empty()) {
+                if (!r.get(line)) break;
+                continue;
+            }
+            if (line[0] != '@') {
+                std::fclose(f);
+                throw std::runtime_error("Malformed FASTQ record in " + path);
+            }
+            const std::string id = line.substr(1);
+            cur.clear();
+            // sequence lines until the '+' separator
+            bool ok = false;
+            while (r.get(line)) {
+                if (!line.empty() && line[0] == '+') {
+                    ok = true;
+                    break;
+                }
+                append_bases(cur, line);
+            }
+            if (!ok) {
+                std::fclose(f);
+                throw std::runtime_error("Truncated FASTQ record in " + path);
+            }
+            // quality lines: as many characters as the sequence holds
+            size_t q = 0;
+            while (q < cur.size() && r.get(line)) q += line.size();
+            ids.push_back(id);
+            seqs.add(cur.data(), (uint32_t)cur.size());
+            if (!r.get(line)) break;
+        }
+    } else {
+        std::fclose(f);
+        throw std::runtime_error("Unknown sequence file format (expected FASTA or FASTQ): " + path);
+    }
+    std::fclose(f);
+}
+
+uint64_t dna2int(const uint8_t* s, uint32_t k) {
+    uint64_t v = 0;
+    for (uint32_t i = 0; i < k; ++i) v = (v << 2) | s[i];
+    return v;
+}
+
+std::string int2dna(uint64_t value, uint32_t k) {
+    static const char DNA[] = "ACGT";
+    std::string s(k, 'A');
+    for (uint32_t i = 0; i < k; ++i) {
+        s[k - 1 - i] = DNA[value & 3u];
+        value >>= 2;
+    }
+    return s;
+}
+
+float adjust_threshold(float c_old, uint32_t k_old, uint32_t k_new) {
+    // float(pow(k_new - 1, 2) / pow(k_old - 1, 2)) in double, then a float product.
+    const double ratio = ((double)k_new - 2 + 1) * ((double)k_new - 2 + 1) /
+                         (((double)k_old - 2 + 1) * ((double)k_old - 2 + 1));
+    return c_old * (float)ratio;
+}
+
+float get_complexity(uint64_t kmer, uint32_t k) {
+    uint64_t counts[16] = {0};
+    for (uint32_t i = 0; i + 1 < k; ++i) {
+        counts[kmer & 15u]++;
+        kmer >>= 2;
+    }
+    size_t sum = 0;
+    for (uint64_t v : counts) sum += v * (v - 1);
+    return (float)sum / float(2 * ((int)k - 2));
+}
+
+bool CompareCount::operator()(const kmer_count& a, const kmer_count& b) const {
+    if (a.second == b.second) {
+        const float ac = get_complexity(a.first, k), bc = get_complexity(b.first, k);
+        if (ac == bc) return a.first > b.first;
+        return ac < bc;
+    }
+    return a.second > b.second;
+}
+
+SeqSet sample_sequences(const SeqSet& seqs, uint64_t nb_sample, uint64_t cut, bool bot, std::mt19937& rng) {
+    SeqSet sample;
+    std::vector<int> vec(seqs.size());
+    std::iota(vec.begin(), vec.end(), 0);
+    std::shuffle(vec.begin(), vec.end(), rng);
+    uint64_t nb_seq = 0;
+    for (size_t i = 0; nb_seq < nb_sample && i < vec.size(); ++i) {
+        const size_t id = (size_t)vec[i];
+        const uint64_t len = seqs.length[id];
+        const uint64_t cur_cut = std::min<uint64_t>(len, cut);
+        if (len >= cut * 2) {
+            if (bot) {
+                const uint64_t from = len - 1 - cur_cut;  // suffix(seq, len - 1 - cut): cut + 1 bases
+                sample.add(seqs.seq(id) + from, (uint32_t)(len - from));
+            } else {
+                sample.add(seqs.seq(id), (uint32_t)cur_cut);
+            }
+            ++nb_seq;
+        }
+    }
+    return sample;
+}
+
+namespace {
+
+// LSD radix sort of 2k-bit keys, 11 bits per pass.
+void radix_sort(std::vector<uint64_t>& a, uint32_t bits) {
+    std::vector<uint64_t> tmp(a.size());
+    constexpr uint32_t R = 11, B = 1u << R;
+    std::vector<size_t> cnt(B);
+    for (uint32_t sh = 0; sh < bits; sh += R) {
+        std::fill(cnt.begin(), cnt.end(), 0);
+        for (uint64_t v : a) cnt[(v >> sh) & (B - 1)]++;
+        size_t s = 0;
+        for (auto& c : cnt) {
+            const size_t t = c;
+            c = s;
+            s += t;
+        }
+        for (uint64_t v : a) tmp[cnt[(v >> sh) & (B - 1)]++] = v;
+        a.swap(tmp);
+    }
+}
+
+}  // namespace
+
+pair_vector count_kmers(const SeqSet& sample, uint32_t k, float threshold, const kmer_set& forbidden,
+                        uint64_t* had_n) {
+    std::vector<uint64_t> vals;
+    size_t total = 0;
+    for (size_t i = 0; i < sample.size(); ++i)
+        if (sample.length[i] >= k) total += sample.length[i] - k + 1;
+    vals.reserve(total);
+    const uint64_t mask = k == 32 ? ~0ull : ((1ull << (2 * k)) - 1);
+    uint64_t n_skipped = 0;
+    for (size_t i = 0; i < sample.size(); ++i) {
+        const uint8_t* s = sample.seq(i);
+        const uint32_t len = sample.length[i];
+        if (len < k) continue;
+        uint64_t v = 0;
+        uint32_t run = 0;  // bases since the last N
+        for (uint32_t j = 0; j < len; ++j) {
+            if (s[j] >= 4) {
+                run = 0;
+                v = 0;
+            } else {
+                v = ((v << 2) | s[j]) & mask;
+                ++run;
+            }
+            if (j + 1 >= k) {
+                if (run >= k) vals.push_back(v);
+                else ++n_skipped;
+            }
+        }
+    }
+    if (had_n) *had_n = n_skipped;
+    radix_sort(vals, 2 * k);
+    pair_vector out;
+    for (size_t i = 0; i < vals.size();) {
+        size_t j = i + 1;
+        while (j < vals.size() && vals[j] == vals[i]) ++j;
+        const uint64_t km = vals[i];
+        if (!have_low_complexity(km, k, threshold) && forbidden.find(km) == forbidden.end())
+            out.emplace_back(km, (uint64_t)(j - i));
+        i = j;
+    }
+    return out;
+}
+
+pair_vector get_most_frequent(pair_vector counts, uint64_t limit, uint32_t k) {
+    // CompareCount is a strict total order (the k-mer value breaks every tie),
+    // so a partial sort gives exactly the first `limit` entries of the full sort.
+    struct Keyed {
+        uint64_t count, kmer;
+        float comp;
+    };
+    std::vector<Keyed> v(counts.size());
+    for (size_t i = 0; i < counts.size(); ++i)
+        v[i] = {counts[i].second, counts[i].first, get_complexity(counts[i].first, k)};
+    auto less = [](const Keyed& a, const Keyed& b) {
+        if (a.count != b.count) return a.count > b.count;
+        if (a.comp != b.comp) return a.comp < b.comp;
+        return a.kmer > b.kmer;
+    };
+    const size_t n = std::min<uint64_t>(limit, v.size());
+    std::partial_sort(v.begin(), v.begin() + n, v.end(), less);
+    pair_vector out(n);
+    for (size_t i = 0; i < n; ++i) out[i] = {v[i].kmer, v[i].count};
+    return out;
+}
+
+pair_vector get_solid_kmers(pair_vector counts, uint64_t solid, uint32_t k) {
+    pair_vector kept;
+    for (const auto& kv : counts)
+        if (kv.second >= solid) kept.push_back(kv);
+    return get_most_frequent(std::move(kept), ~0ull, k);
+}
+
+bool export_counter(const pair_vector& v, uint32_t k, const std::string& path) {
+    std::FILE* f = std::fopen(path.c_str(), "wb");
+    if (!f) {
+        std::fprintf(stderr, "/!\\ ERROR: COULD NOT OPEN FILE %s\n", path.c_str());
+        return false;
+    }
+    std::string line;
+    for (const auto& kv : v) {
+        line = int2dna(kv.first, k);
+        line += '\t';
+        line += std::to_string(kv.second);
+        line += '\n';
+        std::fwrite(line.data(), 1, line.size(), f);
+    }
+    std::fclose(f);
+    return true;
+}
+
+arg_map parse_config(const std::string& path, bool* opened) {
+    arg_map params;
+    std::ifstream in(path);
+    if (opened) *opened = in.is_open();
+    if (!in.is_open()) return params;
+    std::string line;
+    while (std::getline(in, line)) {
+        if (!line.empty() && line[0] == '#') continue;
+        std::string arg, val;
+        bool sep = false;
+        for (char c : line) {
+            if (c == '=') sep = true;
+            else if (c != ' ') (sep ? val : arg) += c;
+        }
+        params[arg] = val;
+    }
+    return params;
+}
+
+bool parse_kmer_list(const std::string& path, kmer_set& out) {
+    std::ifstream in(path);
+    if (!in.is_open()) return false;
+    std::string line;
+    while (std::getline(in, line)) {
+        uint64_t v = 0;
+        bool ok = true;
+        for (char c : line) {
+            const uint8_t b = dna5(c);
+            if (b >= 4) {
+                ok = false;
+                break;
+            }
+            v = (v << 2) | b;
+        }
+        if (ok) out.insert(v);
+    }
+    return true;
+}
+
+}  // namespace achost

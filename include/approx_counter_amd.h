@@ -80,6 +80,11 @@ typedef struct ac_segment {
  * the index construction + omp_set_num_threads of errorCount (537-547). */
 ac_status ac_create(ac_ctx** out, int device);
 void ac_destroy(ac_ctx* ctx);
+/* Number of HIP devices visible to this process (0 without a GPU).  The
+ * reference has no counterpart: its errorCount runs on the host's OpenMP
+ * threads (approx_counter.cpp:547); the CLI uses this to map -g shards onto
+ * devices. */
+int ac_device_count(void);
 /* Last failure text for ctx (or for the calling thread when ctx is NULL). */
 const char* ac_last_error(const ac_ctx* ctx);
 int ac_abi_version(void);
