@@ -1,20 +1,32 @@
 #!/usr/bin/env python3
 """Benchmark of the approximate-count stage (errorCount, approx_counter.cpp:531-601).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4|cfg5]
 
 A step is one pass of the hot path over one batch: both read ends of one run
 (start + end windows, approx_counter.cpp:858) counted against their own
-top-`lim` candidates in ONE fused kernel launch, inputs already resident in
-HBM.  Workload = BASELINE config 2 (k=16, sn=10,000, sl=100, lim=500) on
-seeded synthetic reads.  With N > 1 ranks (one process per
-GPU, torchrun) every rank counts its own 10,000 reads against the same
+top-`lim` candidates in ONE fused kernel launch (plus the zeroing of the count
+vector), inputs already resident in HBM.  Default workload = BASELINE.json
+configs[1] (k=16, sn=10,000, sl=100, lim=500), the configuration the metric is
+quoted on, on seeded synthetic reads.  With N > 1 ranks (one
+process per GPU, torchrun) every rank counts its own sn reads against the same
 candidates and the per-candidate count vector is summed with one RCCL
 all-reduce per step (weak scaling).  Rank 0 prints ONE JSON line.
+
+Roofline: the count kernel is bound by integer VALU
+issue, not HBM and not MFMA.  `roofline.achieved` = algorithmic VALU lane-ops
+per launch / mean kernel duration (HIP events around each launch, on the
+launch stream, inside the timed loop); algorithmic work = 11.5 full-rate lane
+ops per text base per lane word of P candidates (P = 2 at k=16, 1 at k=22);
+`peak` = 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (MI355X_MICROARCH.md: SIMD-32,
+2-cycle wave64 VALU issue).  `traffic` = HBM bytes per launch from the
+committed rocprofv3 PMC passes (profiles/*_pmc_traffic.json) for the same
+workload, FETCH_SIZE doubled per the gfx950 correction, or null.
 """
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import sys
@@ -26,11 +38,17 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "approx-count kmer×base pairs/sec (k=16, lim=500, 10k×100bp ends)"
-# int32 VALU peak: 256 CU x 4 SIMD x 32 lanes/clk x 2.4 GHz (MI355X_MICROARCH.md:28-34,54)
-VALU_PEAK_OPS = 256 * 4 * 32 * 2.4e9
-# VALU lane-ops per text base per lane word (kernel section): 2 (Eq) + 10
-# (three NFA rows) + 1.5 (hit accumulators, v_or3 over two bases).
-OPS_PER_BASE_WORD = 13.5
+VALU_PEAK_OPS = 256 * 4 * 32 * 2.4e9       # int32 lane-ops/s (2-cycle wave64 issue per SIMD-32)
+HBM_PEAK = 8.0e12                           # B/s (MI355X_MICROARCH.md, spec)
+OPS_PER_BASE_WORD = 11.5                    # 2 ~Eq + 8 NFA + 1.5 hit accumulation
+SAMPLE_BYTES_PER_BASE = 0.375               # 2-bit code + 1-bit N mask, read once
+
+CONFIGS = {  # BASELINE.json configs (sn per rank for the bench)
+    "cfg2": dict(k=16, sn=10_000, sl=100, lim=500),
+    "cfg3": dict(k=16, sn=100_000, sl=100, lim=2000),
+    "cfg4": dict(k=16, sn=1_000_000, sl=100, lim=500),
+    "cfg5": dict(k=22, sn=100_000, sl=150, lim=1000),
+}
 
 
 def parse():
@@ -38,40 +56,62 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--k", type=int, default=16)
-    ap.add_argument("--sn", type=int, default=10_000)
-    ap.add_argument("--sl", type=int, default=100)
-    ap.add_argument("--lim", type=int, default=500)
+    ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
+    ap.add_argument("--k", type=int)
+    ap.add_argument("--sn", type=int)
+    ap.add_argument("--sl", type=int)
+    ap.add_argument("--lim", type=int)
     ap.add_argument("--read-len", type=int, default=400)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="target duration of the bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify", action="store_true", help="check counts against the oracle (slow)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    for key, v in CONFIGS[a.config].items():
+        if getattr(a, key) is None:
+            setattr(a, key, v)
+    a.read_len = max(a.read_len, 2 * a.sl)
+    return a
 
 
 def cpu_baseline(wl, k, seconds):
-    """Oracle Myers (OpenMP C, the restated CPU path) on a bounded sample of the same
-    workload: all start candidates against the first W start windows."""
+    """The oracle's OpenMP Myers restatement (the 'port' CPU path) timed on this
+    host's cores over the same workload (both ends), repeated to fill ~`seconds`."""
     import oracle
 
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    kmers = wl["start"]["kmers"]
-    wins = wl["start"]["windows"]
-    probe = wins[:200]
+    units_rep = sum(wl[e]["kmers"].size * sum(int(w.size) for w in wl[e]["windows"]) for e in ("start", "end"))
+
+    def one():
+        for e in ("start", "end"):
+            oracle.count_myers(k, wl[e]["kmers"], wl[e]["windows"], threads)
+
     t = time.perf_counter()
-    oracle.count_myers(k, kmers, probe, threads)
-    dt = max(time.perf_counter() - t, 1e-6)
-    n_win = int(min(len(wins), max(200, 200 * seconds / dt)))
-    sample = wins[:n_win]
-    units = len(kmers) * sum(int(w.size) for w in sample)
+    one()
+    dt1 = max(time.perf_counter() - t, 1e-6)
+    reps = max(1, int(seconds / dt1))
     t = time.perf_counter()
-    oracle.count_myers(k, kmers, sample, threads)
+    for _ in range(reps):
+        one()
     dt = time.perf_counter() - t
-    return {"value": units / dt, "unit": "kmer*bp/s", "cores": threads, "kind": "port",
-            "sample": f"{len(kmers)} start candidates x {n_win} start windows ({units:.3g} kmer*bp), "
-                      f"oracle Myers 64-bit OpenMP, {dt:.2f} s"}
+    return {"value": units_rep * reps / dt, "unit": "kmer*bp/s", "cores": threads, "kind": "port",
+            "sample": f"the full workload (both ends, {units_rep:.4g} kmer*bp) x {reps} repetitions = {dt:.1f} s; "
+                      f"oracle/ac_oracle.c Myers bit-vector, OpenMP over candidates (the reference's SeqAn "
+                      f"FM-index path cannot be built here: SURVEY.md 8(c))"}
+
+
+def load_traffic(workload: str):
+    """HBM bytes per launch of the count kernel from committed PMC summaries."""
+    best = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json"))):
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if d.get("workload") == workload:
+            best = d
+    return best
 
 
 def main():
@@ -103,12 +143,19 @@ def main():
         seg.counts = counts[off:off + n]
         off += n
         segs.append(seg)
-    units = sum(n * sum(int(w.size) for w in wl[e]["windows"]) for e, n in zip(ends, n_c))
+    bases = [sum(int(w.size) for w in wl[e]["windows"]) for e in ends]
+    units = sum(n * b for n, b in zip(n_c, bases))
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
 
-    def step():
-        counter.count_device(args.k, segs, stream=sp)
+    def step(i=None):
+        counts.zero_()
+        if i is not None:
+            evs[i][0].record(stream)
+        counter.count_device(args.k, segs, stream=sp, accumulate=True)
+        if i is not None:
+            evs[i][1].record(stream)
         if world > 1:
             dist.all_reduce(counts)
 
@@ -118,8 +165,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    for i in range(args.steps):
+        step(i)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -128,16 +175,6 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-
-    # Kernel-only duration with HIP events on the launch stream (counts zeroed outside).
-    n_ev = max(10, min(args.steps, 200))
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_ev)]
-    for a, b in evs:
-        counts.zero_()
-        a.record(stream)
-        counter.count_device(args.k, segs, stream=sp, accumulate=True)
-        b.record(stream)
-    torch.cuda.synchronize(dev)
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
     geo = counter.last_launch()
 
@@ -153,11 +190,12 @@ def main():
 
     if rank == 0:
         P = min(32 // args.k, 4)
-        base_words = sum(((n + 64 * P - 1) // (64 * P)) * 64 * sum(int(w.size) for w in wl[e]["windows"])
-                         for e, n in zip(ends, n_c))
-        ops = OPS_PER_BASE_WORD * base_words  # lane-ops per launch (all lane words, incl. padding)
-        achieved = ops / (kern_ms * 1e-3) / 1e9
-        peak = VALU_PEAK_OPS / 1e9
+        workload_name = (f"{args.config}: k={args.k} sn={args.sn} sl={args.sl} lim={args.lim}, "
+                         f"start+end ends fused, {args.sn} reads/rank")
+        ops = OPS_PER_BASE_WORD / P * units  # algorithmic lane-ops per launch (one rank)
+        achieved = ops / (kern_ms * 1e-3)
+        sample_bytes = SAMPLE_BYTES_PER_BASE * sum(bases) + 12 * sum(n_c)  # sample + kmers in + counts out
+        tr = load_traffic(workload_name)
         out = {
             "metric": METRIC,
             "value": units * args.steps * world / elapsed,
@@ -171,18 +209,23 @@ def main():
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic (seeded reads, SURVEY.md 8(d)); inputs resident in HBM",
-            "config": {"workload": f"cfg2: k={args.k} sn={args.sn} sl={args.sl} lim={args.lim}, "
-                                   f"start+end ends fused, {args.sn} reads/rank",
-                       "k": args.k, "sn_per_rank": args.sn, "sl": args.sl, "lim": args.lim,
-                       "candidates": n_c, "kmer_bp_per_rank_step": units,
-                       "parallelism": f"window shards x{world}, all-reduce of counts"},
+            "config": {"workload": workload_name, "k": args.k, "sn_per_rank": args.sn, "sl": args.sl,
+                       "lim": args.lim, "candidates": n_c, "kmer_bp_per_rank_step": units,
+                       "parallelism": f"window shards x{world}, RCCL all-reduce of counts" if world > 1
+                       else "1 GPU"},
             "kernel_ms": kern_ms,
             "kernel_kmer_bp_per_s": units / (kern_ms * 1e-3),
             "launch": geo,
-            "roofline": {"bound": "valu", "achieved": achieved, "peak": peak, "unit": "Gop/s",
-                         "frac": achieved / peak, "traffic": None,
-                         "note": f"int32 VALU lane-ops: {OPS_PER_BASE_WORD} per base per lane word "
-                                 f"({P} candidates per lane word)"},
+            "roofline": {"bound": "valu", "achieved": achieved / 1e12, "peak": VALU_PEAK_OPS / 1e12,
+                         "unit": "Tops/s", "frac": achieved / VALU_PEAK_OPS,
+                         "traffic": tr["hbm_bytes_per_launch"] if tr else None,
+                         "note": f"int32 VALU lane-ops, {OPS_PER_BASE_WORD}/P per kmer*bp (P={P}); HIP events "
+                                 f"around every timed launch; traffic from "
+                                 f"{os.path.basename(tr['source']) if tr else 'n/a'}"},
+            "roofline_hbm": {"bound": "hbm (informational)", "achieved": sample_bytes / (kern_ms * 1e-3) / 1e9,
+                             "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                             "frac": sample_bytes / (kern_ms * 1e-3) / HBM_PEAK,
+                             "algorithmic_bytes_per_launch": sample_bytes},
         }
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(wl, args.k, args.cpu_seconds)
