@@ -58,14 +58,25 @@ class PackedSample:
 
 
 def pack_windows(windows) -> PackedSample:
-    """Pack Dna5 windows into the 2-bit + N-mask image with ac_pack_windows."""
+    """Pack Dna5 windows into the 2-bit + N-mask image with ac_pack_windows.
+    `windows` is a sequence of strings / byte strings / Dna5 ordinal arrays, or a
+    2-D uint8 array of equal-length windows (Dna5 ordinals, one per row)."""
     L = _lib.load()
-    arrs = [to_dna5(w) for w in windows]
-    lengths = np.array([a.size for a in arrs], dtype=np.uint32)
-    starts = np.zeros(len(arrs), dtype=np.uint64)
-    if len(arrs) > 1:
-        starts[1:] = np.cumsum(lengths[:-1], dtype=np.uint64)
-    flat = np.concatenate(arrs) if arrs and lengths.sum() else np.zeros(1, np.uint8)
+    if isinstance(windows, np.ndarray) and windows.ndim == 2:
+        n, wl = windows.shape
+        arrs = [None] * n
+        lengths = np.full(n, wl, dtype=np.uint32)
+        starts = np.arange(n, dtype=np.uint64) * np.uint64(wl)
+        flat = np.ascontiguousarray(windows, dtype=np.uint8).reshape(-1)
+        if flat.size == 0:
+            flat = np.zeros(1, np.uint8)
+    else:
+        arrs = [to_dna5(w) for w in windows]
+        lengths = np.array([a.size for a in arrs], dtype=np.uint32)
+        starts = np.zeros(len(arrs), dtype=np.uint64)
+        if len(arrs) > 1:
+            starts[1:] = np.cumsum(lengths[:-1], dtype=np.uint64)
+        flat = np.concatenate(arrs) if arrs and lengths.sum() else np.zeros(1, np.uint8)
     flat = np.ascontiguousarray(flat, dtype=np.uint8)
     lens_c = lengths if lengths.size else np.zeros(1, np.uint32)
     n_bases = int(L.ac_image_bases(_ptr(lens_c, ctypes.c_uint32), len(arrs)))

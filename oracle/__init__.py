@@ -80,6 +80,12 @@ def int2dna(value: int, k: int) -> str:
 
 
 def _flatten(windows):
+    if isinstance(windows, np.ndarray) and windows.ndim == 2:  # equal-length windows, Dna5 ordinals
+        n, L = windows.shape
+        bases = np.ascontiguousarray(windows, dtype=np.uint8).reshape(-1)
+        if bases.size == 0:
+            bases = np.zeros(1, dtype=np.uint8)
+        return bases, np.arange(n, dtype=np.uint64) * np.uint64(L), np.full(n, L, dtype=np.uint32)
     arrs = [encode_dna5(w) for w in windows]
     lengths = np.array([len(a) for a in arrs], dtype=np.uint32)
     offsets = np.zeros(len(arrs), dtype=np.uint64)

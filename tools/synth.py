@@ -79,3 +79,25 @@ def write_fasta(path: str, reads, width: int = 0) -> None:
                     fh.write(r[j:j + width] + b"\n")
             else:
                 fh.write(r + b"\n")
+
+
+def make_windows_fast(n: int, length: int, seed: int = 1, p_n: float = 0.001, adapter_len: int = 28,
+                      p_adapter: float = 0.6, max_subs: int = 2, at_end: bool = False):
+    """Vectorised equal-length windows for the 1M-window scale tests (Dna5 ordinals,
+    shape (n, length)).  Like make_reads' read ends but with substitution-only
+    adapter copies (0..max_subs per copy) so no per-read Python loop is needed."""
+    rng = np.random.default_rng(seed)
+    w = rng.integers(0, 4, size=(n, length), dtype=np.uint8)
+    adapter = rng.integers(0, 4, size=adapter_len, dtype=np.uint8)
+    rows = np.nonzero(rng.random(n) < p_adapter)[0]
+    off = rng.integers(0, 5, size=rows.size)
+    cols = (length - adapter_len - off)[:, None] + np.arange(adapter_len) if at_end else \
+        off[:, None] + np.arange(adapter_len)
+    cp = np.broadcast_to(adapter, (rows.size, adapter_len)).copy()
+    for _ in range(max_subs):
+        hit = rng.random(rows.size) < 0.4
+        pos = rng.integers(0, adapter_len, size=rows.size)
+        cp[hit, pos[hit]] = rng.integers(0, 4, size=int(hit.sum()), dtype=np.uint8)
+    w[rows[:, None], cols] = cp
+    w[rng.random(size=w.shape) < p_n] = 4
+    return w, adapter
