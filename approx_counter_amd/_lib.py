@@ -50,6 +50,14 @@ def load():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"{LIB_PATH} not found: build it with `make` (hipcc, gfx950)")
+    # torch ships its own libamdhip64.so.7.  Whichever runtime is loaded first
+    # serves the whole process (same soname); if ours (/opt/rocm) comes first,
+    # torch's later CUDA init fails with "No HIP GPUs are available".  So when
+    # torch is present, let it load its runtime first and share it.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     vp = ctypes.c_void_p
     L.ac_abi_version.restype = ctypes.c_int
