@@ -25,6 +25,10 @@ struct ac_ctx {
     void* d_buf[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     size_t d_cap[6] = {0, 0, 0, 0, 0, 0};
     std::vector<uint32_t> h_counts;
+    // work-queue counters: two banks of qcap u32; dirty[b] =
+    // counters of bank b used by the last launch on it (zeroed by the next launch)
+    uint32_t* queue = nullptr;
+    uint32_t qcap = 0, bank = 0, dirty[2] = {0, 0};
     // resident waves of the count kernel per pattern pack P (0 = not queried yet)
     uint32_t resident[AC_MAX_PACK + 1] = {0, 0, 0, 0, 0};
     // last launch geometry
@@ -93,14 +97,26 @@ ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hi
         const uint32_t groups = (s.n_kmers + cpw - 1) / cpw;
         items += (uint64_t)groups * s.sample.n_windows;
     }
-    // One round of resident waves: every wave gets the same number of windows
-    // (windows of one job have near-equal lengths), and all of them are on the
-    // chip together, so the launch has no second, partly filled round.
+    // Launch plan.  One round of resident waves; work is pulled
+    // from dynamic queues: items of `chunk` windows (1 when waves get few
+    // windows, so the launch tail is about one window; up to 8 when they get
+    // hundreds, for fewer atomics), each candidate group's items spread over
+    // sub-queues of about 64 waves.  A segment gets sub-queues in proportion
+    // to its windows, so every sub-queue holds about the same work, and wave
+    // i serves sub-queue i mod n_queues.
     if (!ctx->resident[P]) AC_HIP(ctx, acamd::resident_waves(P, ctx->cu_count, &ctx->resident[P]));
-    const uint64_t target = ctx->resident[P];
-    const uint32_t wpw = (uint32_t)std::max<uint64_t>(1, (items + target - 1) / target);
+    const uint64_t resident = ctx->resident[P];
+    const uint32_t wpw = (uint32_t)std::max<uint64_t>(1, (items + resident - 1) / resident);
+    const uint32_t chunk = std::max<uint32_t>(1, std::min<uint32_t>(8, wpw / 64));
+    uint32_t groups_live = 0, max_nw = 1;
+    for (uint32_t i = 0; i < n; ++i)
+        if (segs[i].n_kmers && segs[i].sample.n_windows) {
+            groups_live += (segs[i].n_kmers + cpw - 1) / cpw;
+            max_nw = std::max<uint32_t>(max_nw, segs[i].sample.n_windows);
+        }
+    const uint64_t s_base = std::max<uint64_t>(1, std::min<uint64_t>(32, resident / (64ull * std::max(1u, groups_live))));
     uint64_t wave = 0;
-    uint32_t groups_total = 0;
+    uint32_t groups_total = 0, qbegin = 0;
     for (uint32_t i = 0; i < n; ++i) {
         const ac_segment& s = segs[i];
         acamd::SegDev& d = a.seg[i];
@@ -114,24 +130,48 @@ ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hi
         d.n_kmers = s.n_kmers;
         d.n_windows = s.sample.n_windows;
         d.groups = std::max<uint32_t>(1, (s.n_kmers + cpw - 1) / cpw);
-        d.wpw = wpw;
-        d.wave_begin = wave;
-        if (s.n_kmers && s.sample.n_windows)
-            wave += (uint64_t)d.groups * ((s.sample.n_windows + wpw - 1) / wpw);
-        groups_total += s.n_kmers ? d.groups : 0;
+        d.chunk = chunk;
+        d.subq = (uint32_t)std::max<uint64_t>(1, (s_base * s.sample.n_windows + max_nw / 2) / max_nw);
+        d.queue_begin = qbegin;
+        if (s.n_kmers && s.sample.n_windows) {
+            qbegin += d.groups * d.subq;
+            groups_total += d.groups;
+        } else {
+            d.queue_begin = ~0u;  // never selected by the kernel's segment lookup
+        }
         if (zero && s.n_kmers) AC_HIP(ctx, hipMemsetAsync(s.counts, 0, sizeof(uint32_t) * s.n_kmers, stream));
     }
-    // Segments with no waves are skipped by the lookup: give them an
-    // unreachable wave_begin so the kernel never selects them.
-    for (uint32_t i = 0; i < n; ++i)
-        if (!(segs[i].n_kmers && segs[i].sample.n_windows)) a.seg[i].wave_begin = ~0ull;
-    // The kernel picks the LAST segment whose wave_begin <= wave; keep the
-    // live segments' begins monotone.
+    const uint32_t n_counters = qbegin;
+    if (n_counters) wave = std::max<uint64_t>(resident, n_counters);
+    if (n_counters > ctx->qcap) {
+        if (ctx->queue) AC_HIP(ctx, hipFree(ctx->queue));
+        ctx->queue = nullptr;
+        ctx->qcap = 0;
+        const uint32_t cap = std::max<uint32_t>(n_counters, 1024);
+        const size_t bytes = sizeof(uint32_t) * AC_QUEUE_LINE * 2 * (size_t)cap;
+        AC_HIP(ctx, hipMalloc(&ctx->queue, bytes));
+        AC_HIP(ctx, hipMemsetAsync(ctx->queue, 0, bytes, stream));
+        ctx->qcap = cap;
+        ctx->bank = 0;
+        ctx->dirty[0] = ctx->dirty[1] = 0;
+    }
+    a.queue = ctx->queue;
+    a.qstride = ctx->qcap;
+    a.bank = ctx->bank;
+    a.zero_count = ctx->dirty[ctx->bank ^ 1u];
+    a.n_queues = std::max<uint32_t>(1, n_counters);
+    // Live segments' queue_begin values are increasing; the kernel picks the
+    // last live segment whose queue_begin <= its sub-queue.
     a.total_waves = wave;
     ctx->last_waves = wave;
     ctx->last_wpw = wpw;
     ctx->last_groups = groups_total;
     AC_HIP(ctx, acamd::launch_wm2_count(a, stream));
+    if (wave) {  // the launch dequeued from `bank` and zeroed the other one
+        ctx->dirty[ctx->bank] = n_counters;
+        ctx->dirty[ctx->bank ^ 1u] = 0;
+        ctx->bank ^= 1u;
+    }
     return AC_OK;
 }
 
@@ -180,6 +220,7 @@ void ac_destroy(ac_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     for (void* p : ctx->d_buf)
         if (p) (void)hipFree(p);
+    if (ctx->queue) (void)hipFree(ctx->queue);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }

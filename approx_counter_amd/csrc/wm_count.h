@@ -4,12 +4,16 @@
 #include <stdint.h>
 
 #define AC_MAX_SEGS 4    // segments fused into one launch (start + end ends, shards)
+#define AC_QUEUE_LINE 32  // u32 per queue counter: one 128-B line each (no false sharing between counters)
 #define AC_MAX_PACK 4    // candidates interleaved per 32-bit lane word (P = min(32/k, 4))
 #ifndef AC_WAVE_WORDS
 #define AC_WAVE_WORDS 1  // lane words (independent NFAs) per lane (2 measured slower: profiles/r01_kernel_log.md)
 #endif
+#ifndef AC_BLOCKS_PER_CU
+#define AC_BLOCKS_PER_CU 6  // resident 256-thread blocks per CU (= waves per SIMD), set by the LDS allocation
+#endif
 #ifndef AC_MIN_WAVES_PER_SIMD
-#define AC_MIN_WAVES_PER_SIMD 8  // occupancy the register budget is sized for (<= 64 VGPRs)
+#define AC_MIN_WAVES_PER_SIMD 6  // occupancy the register budget is sized for (<= 80 VGPRs)
 #endif
 
 namespace acamd {
@@ -21,17 +25,27 @@ struct SegDev {
     const uint64_t* start;
     const uint32_t* length;
     uint32_t* counts;
-    uint64_t wave_begin;  // first global wave of this segment
     uint64_t n_bases;     // image size (bases); windows outside it are skipped
     uint32_t n_kmers;
     uint32_t n_windows;
     uint32_t groups;      // candidate groups of cands_per_wave(P) candidates
-    uint32_t wpw;         // windows per wave
+    uint32_t chunk;       // windows per work item of the dynamic queues
+    uint32_t queue_begin; // index of this segment's first sub-queue (groups x subq of them)
+    uint32_t subq;        // sub-queues per candidate group (proportional to n_windows)
 };
 
 struct LaunchArgs {
     SegDev seg[AC_MAX_SEGS];
     uint64_t total_waves;
+    // Work queues: two banks of `qstride` sub-queue counters, one per
+    // AC_QUEUE_LINE-u32 line.  This launch dequeues from bank `bank` (zeroed)
+    // and zeroes the first `zero_count` counters of the other bank for the next
+    // launch.
+    uint32_t* queue;
+    uint32_t qstride;
+    uint32_t bank;
+    uint32_t zero_count;
+    uint32_t n_queues;  // sub-queues over all segments; wave i serves sub-queue i % n_queues
     uint32_t n_segs;
     uint32_t m;  // k-mer length
     uint32_t P;  // candidates per lane word

@@ -58,10 +58,19 @@ constexpr int WAVES_PER_BLOCK = 4;
 // window and at exit; read back with ac_debug_stamps().  No output value is
 // computed from them.
 }  // namespace
-__device__ uint64_t g_stamps[1 << 20];
+__device__ uint64_t g_stamps[1 << 21];
 namespace {
 __device__ __forceinline__ void stamp(uint64_t wave, int i) {
-    if ((threadIdx.x & 63u) == 0 && wave < (1u << 18)) g_stamps[wave * 4 + i] = __builtin_amdgcn_s_memrealtime();
+    if ((threadIdx.x & 63u) == 0 && wave < (1u << 18)) {
+        g_stamps[wave * 8 + i] = __builtin_amdgcn_s_memrealtime();
+        if (i == 0) {
+            uint32_t hw, xcc;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+            g_stamps[wave * 8 + 4] = hw;
+            g_stamps[wave * 8 + 5] = xcc;
+        }
+    }
 }
 #else
 __device__ __forceinline__ void stamp(uint64_t, int) {}
@@ -230,15 +239,17 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, Stage& st) {
     if (wave >= a.total_waves) return;
     stamp(wave, 0);
 
-    // Segment lookup (wave-uniform, <= AC_MAX_SEGS entries).
+    // Wave -> sub-queue q = wave mod n_queues, so every sub-queue is served by
+    // waves of every dispatch age (see the work-queue comment below); q ->
+    // (segment, candidate group g, sub-queue j of that group).
+    const uint32_t q = (uint32_t)(wave % a.n_queues), rank = (uint32_t)(wave / a.n_queues);
     int si = 0;
 #pragma unroll
     for (int i = 1; i < AC_MAX_SEGS; ++i)
-        if (i < (int)a.n_segs && wave >= a.seg[i].wave_begin) si = i;
+        if (i < (int)a.n_segs && q >= a.seg[i].queue_begin) si = i;
     const SegDev& sg = a.seg[si];
-    const uint64_t local = wave - sg.wave_begin;
-    const uint32_t g = (uint32_t)(local % sg.groups);
-    const uint32_t wb = (uint32_t)(local / sg.groups);
+    const uint32_t ql = q - sg.queue_begin;
+    const uint32_t g = ql % sg.groups, j = ql / sg.groups;
     const uint32_t m = a.m;
 
     // Lane constants: character i of pattern p of word w at bit 31 - (i*P + p).
@@ -266,29 +277,88 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, Stage& st) {
         for (int p = 0; p < P; ++p) cnt[w][p] = 0;
 
     stamp(wave, 1);
-    const uint32_t w_begin = wb * sg.wpw;
-    const uint32_t w_end = min(sg.n_windows, w_begin + sg.wpw);
 
-    // Window pipeline: window w+1's first segment is fetched while w is counted.
+    // Counters of the other queue bank are zeroed for the next launch (strided
+    // over the waves; nobody dequeues from that bank in this launch).
+    for (uint64_t z = wave; z < a.zero_count; z += a.total_waves)
+        if (lane == 0)
+            __hip_atomic_exchange(&a.queue[((a.bank ^ 1u) * (uint64_t)a.qstride + z) * AC_QUEUE_LINE], 0u,
+                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+
+    // Dynamic work queues.  VALU issue on a SIMD goes to the oldest wave, so
+    // with a static split the first waves finish early and the last ones run
+    // with few partners (profiles/r01_kernel_log.md).  Instead each candidate
+    // group's items (`chunk` windows each) are spread over `subq` sub-queues
+    // (item j + c*subq belongs to sub-queue j), each a counter on its own
+    // 128-B line; a wave's first item is assigned statically, further ones
+    // are claimed one at a time (below).  Waves are dealt to sub-queues
+    // round-robin, so every sub-queue serves a mix of old and young waves;
+    // the sub-queues drain together and the waves finish within about one
+    // item of each other.
+    // When its sub-queue runs dry a wave steals from the sibling sub-queues of
+    // the same candidate group (same lane masks), probing each counter with a
+    // plain load before claiming.
+    const uint32_t S = sg.subq;
+    const uint32_t chunk = sg.chunk;
+    const uint32_t n_items = (sg.n_windows + chunk - 1u) / chunk;
+    uint32_t jc = j;  // sub-queue currently served
+    auto counter = [&](uint32_t jj) {
+        return a.queue + ((uint64_t)a.bank * a.qstride + sg.queue_begin + g + jj * sg.groups) * AC_QUEUE_LINE;
+    };
+    auto waves_in = [&](uint32_t jj) {  // waves dealt to sub-queue (g, jj): their first items are static
+        const uint32_t qq = sg.queue_begin + g + jj * sg.groups;
+        return (uint32_t)(a.total_waves / a.n_queues) + (qq < a.total_waves % a.n_queues ? 1u : 0u);
+    };
+    auto n_in = [&](uint32_t jj) { return jj < n_items ? (n_items - jj + S - 1u) / S : 0u; };  // items of jj
+    auto item_of = [&](uint32_t c) { return c < n_in(jc) ? jc + c * S : n_items; };
+    auto dequeue_issue = [&]() -> uint32_t {  // lane 0 holds the result; read with readfirstlane
+        uint32_t v = 0;
+        if (lane == 0) v = __hip_atomic_fetch_add(counter(jc), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return v;
+    };
+    auto steal = [&]() -> uint32_t {  // next item from a sibling sub-queue, or n_items
+        for (uint32_t t = 1; t < S; ++t) {
+            const uint32_t jj = (j + t) % S;
+            uint32_t v = 0;
+            if (lane == 0) v = __hip_atomic_load(counter(jj), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (waves_in(jj) + __builtin_amdgcn_readfirstlane(v) >= n_in(jj)) continue;
+            jc = jj;
+            const uint32_t c = waves_in(jj) + __builtin_amdgcn_readfirstlane(dequeue_issue());
+            if (c < n_in(jj)) return jj + c * S;
+        }
+        return n_items;
+    };
+    uint32_t item = j < n_items ? item_of(rank) : n_items;
+    uint32_t pending = 0;
+    uint32_t w = item * chunk, item_end = min(sg.n_windows, w + chunk);
+
+    // Window pipeline: the next window's first segment is fetched while the current one is counted.
     auto valid = [&](uint64_t base, uint32_t len) { return !(base & 31u) && base + len <= sg.n_bases; };
     uint64_t nbase = 0;
     uint32_t nlen = 0;
     Fetch nf = {0u, 0u};
-    if (w_begin < w_end) {
-        nbase = sg.start[w_begin];
-        nlen = sg.length[w_begin];
+    if (item < n_items) {
+        nbase = sg.start[w];
+        nlen = sg.length[w];
         if (valid(nbase, nlen)) nf = fetch(sg.codes + (nbase >> 4), sg.nmask + (nbase >> 5), nlen, 0, lane);
     }
-    for (uint32_t w = w_begin; w < w_end; ++w) {
+    while (item < n_items) {
         const uint64_t base = nbase;
         const uint32_t len = nlen;
         const Fetch f0 = nf;
-        if (w + 1 < w_end) {
-            nbase = sg.start[w + 1];
-            nlen = sg.length[w + 1];
+        // Within an item the next window is fetched while this one is counted.
+        // During an item's last window the next item is claimed (one returning
+        // atomic); it is read after the window, so a wave the arbiter starves
+        // never holds more than the item it is working on.
+        const uint32_t wn = w + 1;
+        if (wn < item_end) {
+            nbase = sg.start[wn];
+            nlen = sg.length[wn];
             if (valid(nbase, nlen)) nf = fetch(sg.codes + (nbase >> 4), sg.nmask + (nbase >> 5), nlen, 0, lane);
+        } else {
+            pending = dequeue_issue();
         }
-        if (!valid(base, len)) continue;  // malformed window: never read outside the image
+        if (valid(base, len)) {  // a malformed window is skipped: never read outside the image
         const uint32_t* __restrict__ codes = sg.codes + (base >> 4);
         const uint32_t* __restrict__ nmask = sg.nmask + (base >> 5);
         Nfa s;
@@ -350,6 +420,19 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, Stage& st) {
                 cnt[x][p] += 3u - ((s.a0[x] >> lb) & 1u) - ((s.a1[x] >> lb) & 1u) - ((s.a2[x] >> lb) & 1u);
             }
         }
+        }  // valid window
+        // advance the cursor; at an item boundary move to the prefetched item and request another
+        if (++w >= item_end) {
+            item = item_of(waves_in(jc) + __builtin_amdgcn_readfirstlane(pending));
+            if (item >= n_items && S > 1) item = steal();
+            if (item < n_items) {
+                w = item * chunk;
+                item_end = min(sg.n_windows, w + chunk);
+                nbase = sg.start[w];
+                nlen = sg.length[w];
+                if (valid(nbase, nlen)) nf = fetch(sg.codes + (nbase >> 4), sg.nmask + (nbase >> 5), nlen, 0, lane);
+            }
+        }
     }
 
     stamp(wave, 2);
@@ -369,7 +452,10 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, Stage& st) {
 
 template <int P>
 __global__ __launch_bounds__(64 * WAVES_PER_BLOCK, AC_MIN_WAVES_PER_SIMD) void wm2_count_kernel(LaunchArgs a) {
-    __shared__ Stage stage[WAVES_PER_BLOCK];
+    // The LDS allocation also caps residency at AC_BLOCKS_PER_CU blocks (6 waves
+    // per SIMD): measured faster than 8 (fewer waves starved by the oldest-first
+    // VALU arbitration; profiles/r01_kernel_log.md).
+    __shared__ Stage stage[(160 * 1024 / AC_BLOCKS_PER_CU) / sizeof(Stage)];
     count_body<P>(a, stage[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)]);
 }
 

@@ -36,11 +36,12 @@ def main():
     torch.cuda.synchronize()
     geo = c.last_launch()
     n = int(geo["waves"])
-    buf = np.zeros(4 * (1 << 18), dtype=np.uint64)
+    buf = np.zeros(8 * (1 << 18), dtype=np.uint64)
     L = _lib.load()
     L.ac_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
     assert L.ac_debug_stamps(buf.ctypes.data, buf.nbytes) == 0
-    st = buf[: 4 * n].reshape(n, 4).astype(np.int64)
+    raw = buf[: 8 * n].reshape(n, 8).astype(np.int64)
+    st = raw[:, :4]
     t0 = st[:, 0].min()
     us = (st - t0) / 100.0  # 100 MHz
     pct = lambda x: " ".join(f"{np.percentile(x, q):7.1f}" for q in (0, 10, 50, 90, 100))
@@ -51,6 +52,32 @@ def main():
     print("main len     ", pct(us[:, 2] - us[:, 1]))
     print("atomics len  ", pct(us[:, 3] - us[:, 2]))
     print("end          ", pct(us[:, 3]))
+    # per-SIMD view: HW_ID (gfx9 layout) wave[3:0] simd[5:4] cu[11:8] sh[12] se[15:13]; + XCC id
+    hw, xcc = raw[:, 4], raw[:, 5]
+    simd_key = xcc * 100000 + ((hw >> 13) & 7) * 10000 + ((hw >> 12) & 1) * 1000 + ((hw >> 8) & 15) * 10 + ((hw >> 4) & 3)
+    keys, inv, cnt = np.unique(simd_key, return_inverse=True, return_counts=True)
+    print(f"SIMDs used: {keys.size}; waves per SIMD: min {cnt.min()} max {cnt.max()} mean {cnt.mean():.2f}")
+    span = np.zeros(keys.size)
+    last = np.zeros(keys.size)
+    first = np.full(keys.size, 1e18)
+    for i in range(n):
+        first[inv[i]] = min(first[inv[i]], us[i, 0])
+        last[inv[i]] = max(last[inv[i]], us[i, 3])
+    span = last - first
+    print("SIMD span    ", pct(span))
+    # active-wave profile of the slowest SIMD
+    j = int(np.argmax(last))
+    w = np.nonzero(inv == j)[0]
+    print(f"slowest SIMD {keys[j]}: {w.size} waves, (start, end) us:",
+          sorted((round(float(us[i, 0]), 1), round(float(us[i, 3]), 1)) for i in w))
+    # time-weighted number of resident waves per SIMD, over the kernel
+    T = us[:, 3].max()
+    grid = np.linspace(0, T, 200)
+    active = np.zeros((keys.size, grid.size))
+    for i in range(n):
+        active[inv[i]] += (grid >= us[i, 0]) & (grid < us[i, 3])
+    print("mean resident waves per SIMD at 10%..90% of the kernel:",
+          [round(float(active[:, int(f * 199)].mean()), 2) for f in (0.1, 0.3, 0.5, 0.7, 0.8, 0.9, 0.95)])
 
 
 if __name__ == "__main__":
