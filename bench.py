@@ -122,10 +122,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # AC_BENCH_BACKEND=gloo rehearses the N > 1 code path on a box with fewer
+    # GPUs than ranks (ranks share devices, the count vector is reduced on the
+    # host); the real multi-GPU run uses RCCL ("nccl") over xGMI.
+    backend = os.environ.get("AC_BENCH_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count()) if backend != "nccl" else local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     import approx_counter_amd as ac
     from tools import workload
@@ -157,7 +165,12 @@ def main():
         if i is not None:
             evs[i][1].record(stream)
         if world > 1:
-            dist.all_reduce(counts)
+            if backend == "nccl":
+                dist.all_reduce(counts)
+            else:
+                host = counts.cpu()
+                dist.all_reduce(host)
+                counts.copy_(host)
 
     for _ in range(args.warmup):
         step()
@@ -172,7 +185,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
@@ -211,8 +224,8 @@ def main():
             "data": "synthetic (seeded reads, SURVEY.md 8(d)); inputs resident in HBM",
             "config": {"workload": workload_name, "k": args.k, "sn_per_rank": args.sn, "sl": args.sl,
                        "lim": args.lim, "candidates": n_c, "kmer_bp_per_rank_step": units,
-                       "parallelism": f"window shards x{world}, RCCL all-reduce of counts" if world > 1
-                       else "1 GPU"},
+                       "parallelism": f"window shards x{world}, {'RCCL' if backend == 'nccl' else backend} "
+                                      f"all-reduce of counts" if world > 1 else "1 GPU"},
             "kernel_ms": kern_ms,
             "kernel_kmer_bp_per_s": units / (kern_ms * 1e-3),
             "launch": geo,
