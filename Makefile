@@ -12,8 +12,8 @@ LIBDIR := $(PKG)/lib
 LIB := $(LIBDIR)/libapprox_counter_amd.so
 OBJDIR := build/obj
 
-DEV_SRC := $(CSRC)/wm_count.hip $(CSRC)/capi.cpp
-HDRS := include/approx_counter_amd.h $(CSRC)/wm_count.h
+DEV_SRC := $(CSRC)/wm_count.hip $(CSRC)/exact_count.hip $(CSRC)/capi.cpp
+HDRS := include/approx_counter_amd.h $(CSRC)/wm_count.h $(CSRC)/exact_count.h
 
 CXX ?= g++
 HOST_CXXFLAGS ?= -O3 -std=c++17 -fPIC -Wall -Wextra
@@ -34,7 +34,7 @@ $(OBJDIR)/capi.o: $(CSRC)/capi.cpp $(HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -x hip -Iinclude -I$(CSRC) -c $< -o $@
 
-$(LIB): $(OBJDIR)/wm_count.o $(OBJDIR)/capi.o
+$(LIB): $(OBJDIR)/wm_count.o $(OBJDIR)/exact_count.o $(OBJDIR)/capi.o
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
 

@@ -81,6 +81,15 @@ def load():
     L.ac_pack_windows.restype = ctypes.c_int
     L.ac_last_launch.argtypes = [vp, p64, p32, p32]
     L.ac_last_launch.restype = ctypes.c_int
+    L.ac_sample_upload.argtypes = [vp, ctypes.POINTER(ACWindows), ctypes.POINTER(ACWindows)]
+    L.ac_sample_upload.restype = ctypes.c_int
+    exact = [vp, ctypes.c_uint32, ctypes.POINTER(ACWindows), ctypes.c_float, p64, ctypes.c_uint32, ctypes.c_uint64,
+             ctypes.c_uint64, p64, p64, ctypes.c_uint64, p64, p64, p64]
+    for fn in (L.ac_exact_count, L.ac_exact_count_device):
+        fn.argtypes = exact
+        fn.restype = ctypes.c_int
+    L.ac_error_count_sample.argtypes = [vp, ctypes.c_uint32, p64, ctypes.c_uint32, ctypes.POINTER(ACWindows), p64]
+    L.ac_error_count_sample.restype = ctypes.c_int
     _lib = L
     return L
 

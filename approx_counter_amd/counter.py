@@ -132,6 +132,29 @@ class ApproxCounter:
         check(st, self._h)
         return counts[: kmers.size]
 
+    def exact_count(self, k: int, sample: PackedSample, lc_threshold: float, forbidden=(), limit: int = 500,
+                    solid: int = 0):
+        """ac_exact_count: count_kmers (approx_counter.cpp:487-519) + get_most_frequent /
+        get_solid_kmers on the GPU.  Returns ([(kmer, count), ...] in CompareCount order,
+        n_distinct, had_n)."""
+        fb = np.ascontiguousarray(np.asarray(list(forbidden) or [0], dtype=np.uint64))
+        cap = max(1, int(limit) if not solid else 1024)
+        ws = sample.as_struct()
+        while True:
+            km = np.zeros(cap, np.uint64)
+            ct = np.zeros(cap, np.uint64)
+            n_out, n_dist, had_n = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+            st = self._L.ac_exact_count(self._h, int(k), ctypes.byref(ws), float(lc_threshold),
+                                        _ptr(fb, ctypes.c_uint64), len(forbidden), int(limit), int(solid),
+                                        _ptr(km, ctypes.c_uint64), _ptr(ct, ctypes.c_uint64), cap,
+                                        ctypes.byref(n_out), ctypes.byref(n_dist), ctypes.byref(had_n))
+            if st == _lib.AC_ERR_INVALID and n_out.value > cap:
+                cap = int(n_out.value)
+                continue
+            check(st, self._h)
+            n = int(n_out.value)
+            return [(int(a), int(b)) for a, b in zip(km[:n], ct[:n])], int(n_dist.value), int(had_n.value)
+
     def count_device(self, k: int, segments, stream=None, accumulate: bool = False) -> None:
         """ac_error_count_device over DeviceSegment objects (asynchronous)."""
         arr = (ACSegment * len(segments))(*[s.as_struct() for s in segments])

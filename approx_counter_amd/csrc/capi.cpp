@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "approx_counter_amd.h"
+#include "exact_count.h"
 #include "wm_count.h"
 
 struct ac_ctx {
@@ -25,6 +26,12 @@ struct ac_ctx {
     void* d_buf[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     size_t d_cap[6] = {0, 0, 0, 0, 0, 0};
     std::vector<uint32_t> h_counts;
+    // ac_sample_upload buffers (codes, nmask, start, length) and the exact-count
+    // working set (table keys, table counts, small scalars + histogram, forbidden, gather out)
+    void* s_buf[4] = {nullptr, nullptr, nullptr, nullptr};
+    size_t s_cap[4] = {0, 0, 0, 0};
+    void* e_buf[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    size_t e_cap[6] = {0, 0, 0, 0, 0, 0};
     // work-queue counters: two banks of qcap u32; dirty[b] =
     // counters of bank b used by the last launch on it (zeroed by the next launch)
     uint32_t* queue = nullptr;
@@ -63,14 +70,37 @@ ac_status check_k(ac_ctx* ctx, uint32_t k) {
     return AC_OK;
 }
 
-ac_status ensure(ac_ctx* ctx, int slot, size_t bytes) {
+ac_status grow(ac_ctx* ctx, void** buf, size_t* cap, size_t bytes) {
     if (bytes == 0) bytes = 16;
-    if (ctx->d_cap[slot] >= bytes) return AC_OK;
-    if (ctx->d_buf[slot]) (void)hipFree(ctx->d_buf[slot]);
-    ctx->d_buf[slot] = nullptr;
-    ctx->d_cap[slot] = 0;
-    AC_HIP(ctx, hipMalloc(&ctx->d_buf[slot], bytes));
-    ctx->d_cap[slot] = bytes;
+    if (*cap >= bytes) return AC_OK;
+    if (*buf) (void)hipFree(*buf);
+    *buf = nullptr;
+    *cap = 0;
+    AC_HIP(ctx, hipMalloc(buf, bytes));
+    *cap = bytes;
+    return AC_OK;
+}
+
+ac_status ensure(ac_ctx* ctx, int slot, size_t bytes) { return grow(ctx, &ctx->d_buf[slot], &ctx->d_cap[slot], bytes); }
+
+// getComplexity (approx_counter.cpp:247-267) and CompareCount (275-305), for the
+// final ranking of the exact count's short list.
+float complexity(uint64_t kmer, uint32_t k) {
+    uint64_t counts[16] = {0};
+    for (uint32_t i = 0; i + 1 < k; ++i) {
+        counts[kmer & 15u]++;
+        kmer >>= 2;
+    }
+    size_t sum = 0;
+    for (uint64_t v : counts) sum += v * (v - 1);
+    return (float)sum / float(2 * ((int)k - 2));
+}
+
+ac_status check_sample(ac_ctx* ctx, const ac_windows* s) {
+    if (!s) return fail(ctx, AC_ERR_INVALID, "sample is NULL");
+    if (s->n_bases % 32) return fail(ctx, AC_ERR_INVALID, "sample n_bases must be a multiple of 32");
+    if (s->n_windows && (!s->codes || !s->nmask || !s->start || !s->length))
+        return fail(ctx, AC_ERR_INVALID, "sample has a NULL array");
     return AC_OK;
 }
 
@@ -221,6 +251,10 @@ void ac_destroy(ac_ctx* ctx) {
     for (void* p : ctx->d_buf)
         if (p) (void)hipFree(p);
     if (ctx->queue) (void)hipFree(ctx->queue);
+    for (void* p : ctx->s_buf)
+        if (p) (void)hipFree(p);
+    for (void* p : ctx->e_buf)
+        if (p) (void)hipFree(p);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -281,6 +315,190 @@ ac_status ac_error_count(ac_ctx* ctx, uint32_t k, const uint64_t* kmers, uint32_
     if (ac_status rc = launch(ctx, k, &seg, 1, st, true)) return rc;
     ctx->h_counts.resize(n_kmers);
     AC_HIP(ctx, hipMemcpyAsync(ctx->h_counts.data(), ctx->d_buf[5], sz[5], hipMemcpyDeviceToHost, st));
+    AC_HIP(ctx, hipStreamSynchronize(st));
+    for (uint32_t i = 0; i < n_kmers; ++i) counts[i] = ctx->h_counts[i];
+    return AC_OK;
+}
+
+ac_status ac_sample_upload(ac_ctx* ctx, const ac_windows* host, ac_windows* dev) {
+    if (!ctx || !dev) return fail(ctx, AC_ERR_INVALID, "ctx or dev is NULL");
+    if (ac_status st = check_sample(ctx, host)) return st;
+    // layout check on the host copy: every window inside the image, 32-aligned
+    for (uint32_t i = 0; i < host->n_windows; ++i)
+        if (host->start[i] % 32 || host->start[i] + host->length[i] > host->n_bases)
+            return fail(ctx, AC_ERR_INVALID, "window " + std::to_string(i) + " is misaligned or outside the image");
+    AC_HIP(ctx, hipSetDevice(ctx->device));
+    const size_t sz[4] = {sizeof(uint32_t) * (host->n_bases / 16), sizeof(uint32_t) * (host->n_bases / 32),
+                          sizeof(uint64_t) * host->n_windows, sizeof(uint32_t) * host->n_windows};
+    const void* src[4] = {host->codes, host->nmask, host->start, host->length};
+    for (int i = 0; i < 4; ++i) {
+        if (ac_status st = grow(ctx, &ctx->s_buf[i], &ctx->s_cap[i], sz[i])) return st;
+        if (sz[i]) AC_HIP(ctx, hipMemcpyAsync(ctx->s_buf[i], src[i], sz[i], hipMemcpyHostToDevice, ctx->stream));
+    }
+    AC_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    dev->codes = (const uint32_t*)ctx->s_buf[0];
+    dev->nmask = (const uint32_t*)ctx->s_buf[1];
+    dev->start = (const uint64_t*)ctx->s_buf[2];
+    dev->length = (const uint32_t*)ctx->s_buf[3];
+    dev->n_windows = host->n_windows;
+    dev->n_bases = host->n_bases;
+    return AC_OK;
+}
+
+ac_status ac_exact_count_device(ac_ctx* ctx, uint32_t k, const ac_windows* dev, float lc_threshold,
+                                const uint64_t* forbidden, uint32_t n_forbidden, uint64_t limit, uint64_t solid,
+                                uint64_t* kmers_out, uint64_t* counts_out, uint64_t capacity, uint64_t* n_out,
+                                uint64_t* n_distinct, uint64_t* had_n) {
+    if (!ctx) return fail(nullptr, AC_ERR_INVALID, "ctx is NULL");
+    if (ac_status st = check_k(ctx, k)) return st;
+    if (ac_status st = check_sample(ctx, dev)) return st;
+    if (!n_out || (capacity && (!kmers_out || !counts_out)) || (n_forbidden && !forbidden))
+        return fail(ctx, AC_ERR_INVALID, "NULL output or forbidden array");
+    AC_HIP(ctx, hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    // Table: a power of two >= 2 x the image size (an upper bound on k-mer positions): load <= 1/2.
+    uint64_t slots = 1024;
+    while (slots < 2 * dev->n_bases) slots <<= 1;
+    // small block: special[0..1] u32, had_n u64, n_out u64, hist[EXACT_HIST_BINS] u32
+    const size_t small_bytes = 64 + sizeof(uint32_t) * EXACT_HIST_BINS;
+    std::vector<uint64_t> fb(forbidden, forbidden + n_forbidden);
+    std::sort(fb.begin(), fb.end());
+    fb.erase(std::unique(fb.begin(), fb.end()), fb.end());
+    if (ac_status s2 = grow(ctx, &ctx->e_buf[0], &ctx->e_cap[0], sizeof(uint64_t) * slots)) return s2;
+    if (ac_status s2 = grow(ctx, &ctx->e_buf[1], &ctx->e_cap[1], sizeof(uint32_t) * slots)) return s2;
+    if (ac_status s2 = grow(ctx, &ctx->e_buf[2], &ctx->e_cap[2], small_bytes)) return s2;
+    if (ac_status s2 = grow(ctx, &ctx->e_buf[3], &ctx->e_cap[3], sizeof(uint64_t) * std::max<size_t>(1, fb.size())))
+        return s2;
+    AC_HIP(ctx, hipMemsetAsync(ctx->e_buf[0], 0xff, sizeof(uint64_t) * slots, st));
+    AC_HIP(ctx, hipMemsetAsync(ctx->e_buf[1], 0, sizeof(uint32_t) * slots, st));
+    AC_HIP(ctx, hipMemsetAsync(ctx->e_buf[2], 0, small_bytes, st));
+    if (!fb.empty())
+        AC_HIP(ctx, hipMemcpyAsync(ctx->e_buf[3], fb.data(), sizeof(uint64_t) * fb.size(), hipMemcpyHostToDevice, st));
+    char* small = (char*)ctx->e_buf[2];
+    acamd::ExactArgs a;
+    std::memset(&a, 0, sizeof a);
+    a.codes = dev->codes;
+    a.nmask = dev->nmask;
+    a.start = dev->start;
+    a.length = dev->length;
+    a.n_bases = dev->n_bases;
+    a.n_windows = dev->n_windows;
+    a.k = k;
+    a.keys = (uint64_t*)ctx->e_buf[0];
+    a.cnts = (uint32_t*)ctx->e_buf[1];
+    a.slots = slots;
+    a.mask = slots - 1;
+    a.special = (uint32_t*)small;
+    a.had_n = (unsigned long long*)(small + 16);
+    a.n_out = (unsigned long long*)(small + 24);
+    a.hist = (uint32_t*)(small + 64);
+    a.lc_threshold = lc_threshold;
+    a.forbidden = (const uint64_t*)ctx->e_buf[3];
+    a.n_forbidden = (uint32_t)fb.size();
+    AC_HIP(ctx, acamd::launch_exact_insert(a, st));
+    AC_HIP(ctx, acamd::launch_exact_scan(a, st));
+    std::vector<char> h_small(small_bytes);
+    AC_HIP(ctx, hipMemcpyAsync(h_small.data(), small, small_bytes, hipMemcpyDeviceToHost, st));
+    AC_HIP(ctx, hipStreamSynchronize(st));
+    const uint32_t* hist = (const uint32_t*)(h_small.data() + 64);
+    uint64_t kept = 0;
+    for (int i = 0; i < EXACT_HIST_BINS; ++i) kept += hist[i];
+    if (n_distinct) *n_distinct = kept;
+    if (had_n) *had_n = *(const unsigned long long*)(h_small.data() + 16);
+    // Threshold: solid mode keeps count >= solid; otherwise the largest count c
+    // such that at least `limit` kept entries have count >= c (all if fewer).
+    uint64_t thr = 1, due = kept;
+    if (solid) {
+        thr = solid;
+        due = 0;
+        for (uint64_t c = std::min<uint64_t>(solid, EXACT_HIST_BINS - 1); c < EXACT_HIST_BINS; ++c) due += hist[c];
+    } else if (limit < kept) {
+        uint64_t acc = 0;
+        for (int c = EXACT_HIST_BINS - 1; c >= 1; --c) {
+            acc += hist[c];
+            if (acc >= limit) {
+                thr = (uint64_t)c;
+                due = acc;
+                break;
+            }
+        }
+    }
+    // (a solid threshold past the last bin is applied exactly on the gathered list)
+    const uint64_t gather_cap = std::max<uint64_t>(1, due);
+    if (ac_status s2 = grow(ctx, &ctx->e_buf[4], &ctx->e_cap[4], sizeof(uint64_t) * gather_cap)) return s2;
+    if (ac_status s2 = grow(ctx, &ctx->e_buf[5], &ctx->e_cap[5], sizeof(uint32_t) * gather_cap)) return s2;
+    a.threshold = (uint32_t)std::min<uint64_t>(thr, 0xffffffffu);
+    a.out_keys = (uint64_t*)ctx->e_buf[4];
+    a.out_cnts = (uint32_t*)ctx->e_buf[5];
+    a.out_cap = gather_cap;
+    AC_HIP(ctx, acamd::launch_exact_gather(a, st));
+    unsigned long long got = 0;
+    AC_HIP(ctx, hipMemcpyAsync(&got, a.n_out, sizeof got, hipMemcpyDeviceToHost, st));
+    AC_HIP(ctx, hipStreamSynchronize(st));
+    if (got > gather_cap) return fail(ctx, AC_ERR_INTERNAL, "exact count: gathered more entries than the histogram");
+    std::vector<uint64_t> gk(got);
+    std::vector<uint32_t> gc(got);
+    if (got) {
+        AC_HIP(ctx, hipMemcpyAsync(gk.data(), a.out_keys, sizeof(uint64_t) * got, hipMemcpyDeviceToHost, st));
+        AC_HIP(ctx, hipMemcpyAsync(gc.data(), a.out_cnts, sizeof(uint32_t) * got, hipMemcpyDeviceToHost, st));
+        AC_HIP(ctx, hipStreamSynchronize(st));
+    }
+    struct Entry {
+        uint64_t count, kmer;
+        float comp;
+    };
+    std::vector<Entry> v;
+    v.reserve(got);
+    for (uint64_t i = 0; i < got; ++i)
+        if (!solid || gc[i] >= solid) v.push_back({gc[i], gk[i], complexity(gk[i], k)});
+    auto less = [](const Entry& x, const Entry& y) {  // CompareCount: a strict total order
+        if (x.count != y.count) return x.count > y.count;
+        if (x.comp != y.comp) return x.comp < y.comp;
+        return x.kmer > y.kmer;
+    };
+    const size_t n = solid ? v.size() : std::min<size_t>(v.size(), limit);
+    std::partial_sort(v.begin(), v.begin() + n, v.end(), less);
+    *n_out = n;
+    if (n > capacity) return fail(ctx, AC_ERR_INVALID, "exact count: capacity too small (n_out holds the size needed)");
+    for (size_t i = 0; i < n; ++i) {
+        kmers_out[i] = v[i].kmer;
+        counts_out[i] = v[i].count;
+    }
+    return AC_OK;
+}
+
+ac_status ac_exact_count(ac_ctx* ctx, uint32_t k, const ac_windows* host, float lc_threshold,
+                         const uint64_t* forbidden, uint32_t n_forbidden, uint64_t limit, uint64_t solid,
+                         uint64_t* kmers_out, uint64_t* counts_out, uint64_t capacity, uint64_t* n_out,
+                         uint64_t* n_distinct, uint64_t* had_n) {
+    if (!ctx) return fail(nullptr, AC_ERR_INVALID, "ctx is NULL");
+    if (ac_status st = check_k(ctx, k)) return st;
+    ac_windows dev;
+    if (ac_status st = ac_sample_upload(ctx, host, &dev)) return st;
+    return ac_exact_count_device(ctx, k, &dev, lc_threshold, forbidden, n_forbidden, limit, solid, kmers_out,
+                                 counts_out, capacity, n_out, n_distinct, had_n);
+}
+
+ac_status ac_error_count_sample(ac_ctx* ctx, uint32_t k, const uint64_t* kmers, uint32_t n_kmers,
+                                const ac_windows* dev, uint64_t* counts) {
+    if (!ctx) return fail(nullptr, AC_ERR_INVALID, "ctx is NULL");
+    if (ac_status st = check_k(ctx, k)) return st;
+    if (n_kmers == 0) return AC_OK;
+    if (!kmers || !counts) return fail(ctx, AC_ERR_INVALID, "NULL argument");
+    if (ac_status st = check_sample(ctx, dev)) return st;
+    AC_HIP(ctx, hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    if (ac_status s2 = ensure(ctx, 0, sizeof(uint64_t) * n_kmers)) return s2;
+    if (ac_status s2 = ensure(ctx, 5, sizeof(uint32_t) * n_kmers)) return s2;
+    AC_HIP(ctx, hipMemcpyAsync(ctx->d_buf[0], kmers, sizeof(uint64_t) * n_kmers, hipMemcpyHostToDevice, st));
+    ac_segment seg;
+    seg.kmers = (const uint64_t*)ctx->d_buf[0];
+    seg.n_kmers = n_kmers;
+    seg.sample = *dev;
+    seg.counts = (uint32_t*)ctx->d_buf[5];
+    if (ac_status rc = launch(ctx, k, &seg, 1, st, true)) return rc;
+    ctx->h_counts.resize(n_kmers);
+    AC_HIP(ctx, hipMemcpyAsync(ctx->h_counts.data(), ctx->d_buf[5], sizeof(uint32_t) * n_kmers, hipMemcpyDeviceToHost, st));
     AC_HIP(ctx, hipStreamSynchronize(st));
     for (uint32_t i = 0; i < n_kmers; ++i) counts[i] = ctx->h_counts[i];
     return AC_OK;

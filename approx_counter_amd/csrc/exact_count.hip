@@ -1,0 +1,259 @@
+// exact_count.hip -- exact k-mer count of the sampled windows on MI355X.
+//
+// Replaces count_kmers (approx_counter.cpp:487-519) and the heavy part of the
+// candidate selection get_most_frequent / get_solid_kmers (396-405, 372-388):
+// SURVEY.md §8(f) rank 1.  Works on the same packed window image as the
+// approximate count (2-bit codes + N mask, include/approx_counter_amd.h), so a
+// sample is uploaded once for both stages.
+//
+//  1. insert: every k-mer position of every window with no N in it becomes a
+//     key (dna2int layout) counted in an open-addressing hash table in HBM.
+//     Each workgroup first aggregates its batch of windows in an LDS table
+//     (adapter k-mers occur in most windows, so hot keys are summed locally),
+//     then flushes the aggregated (key, count) pairs with global atomics.
+//  2. scan: every occupied slot passes the low-complexity filter (the float
+//     DUST score of approx_counter.cpp:247-267, computed exactly as the
+//     reference does) and the forbidden set (binary search); kept entries feed
+//     a count histogram.
+//  3. gather: entries with count >= a threshold chosen on the host from the
+//     histogram (the smallest count that still yields `limit` entries, or
+//     the solid threshold) are compacted; the host ranks that short list with
+//     CompareCount (approx_counter.cpp:275-305).
+// HBM-bound integer work (random atomics + streaming scans), no MFMA.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "exact_count.h"
+
+#include <algorithm>
+
+namespace acamd {
+namespace {
+
+constexpr int EXACT_THREADS = 256;
+constexpr uint32_t LDS_SLOTS = 4096;        // per-workgroup aggregation table
+constexpr uint32_t LDS_PROBES = 32;         // beyond this a key goes straight to the global table
+constexpr uint64_t EMPTY = ~0ull;           // never a k-mer value except the all-T 32-mer (kept apart)
+
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {  // murmur3 finaliser
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdull;
+    x ^= x >> 33;
+    x *= 0xc4ceb9fe1a85ec53ull;
+    x ^= x >> 33;
+    return x;
+}
+
+// 64-bit value of bases [b, b + k) of the image with base b in the LOW bits.
+__device__ __forceinline__ uint64_t gather_bits(const uint32_t* __restrict__ words, uint64_t b, uint32_t bits_per,
+                                                uint32_t nbits, uint64_t n_words) {
+    const uint64_t bit = b * bits_per;
+    const uint64_t w0 = bit >> 5;
+    const uint32_t off = (uint32_t)(bit & 31u);
+    const uint64_t last = (bit + nbits - 1u) >> 5;  // last word holding a wanted bit
+    uint64_t v = words[w0];
+    if (w0 + 1 <= last && w0 + 1 < n_words) v |= (uint64_t)words[w0 + 1] << 32;
+    v >>= off;
+    if (off && w0 + 2 <= last && w0 + 2 < n_words) v |= (uint64_t)words[w0 + 2] << (64u - off);
+    return v;
+}
+
+// Little-endian 2-bit bases -> dna2int (first base in the most significant used bits).
+__device__ __forceinline__ uint64_t to_dna2int(uint64_t le, uint32_t k) {
+    uint64_t r = __builtin_bitreverse64(le);
+    r = ((r >> 1) & 0x5555555555555555ull) | ((r & 0x5555555555555555ull) << 1);  // restore bit order in each base
+    return r >> (64u - 2u * k);
+}
+
+__device__ __forceinline__ void global_insert(const ExactArgs& a, uint64_t key, uint32_t c) {
+    if (key == EMPTY) {  // the all-T 32-mer
+        atomicAdd(&a.special[0], c);
+        return;
+    }
+    uint64_t h = mix64(key) & a.mask;
+    for (;;) {
+        uint64_t cur = a.keys[h];
+        if (cur == EMPTY) {
+            cur = atomicCAS((unsigned long long*)&a.keys[h], (unsigned long long)EMPTY, (unsigned long long)key);
+            if (cur == EMPTY) cur = key;
+        }
+        if (cur == key) {
+            atomicAdd(&a.cnts[h], c);
+            return;
+        }
+        h = (h + 1u) & a.mask;
+    }
+}
+
+__global__ __launch_bounds__(EXACT_THREADS) void exact_insert_kernel(ExactArgs a) {
+    __shared__ unsigned long long lkeys[LDS_SLOTS];
+    __shared__ uint32_t lcnt[LDS_SLOTS];
+    __shared__ uint32_t wpos[EXACT_WINDOWS_PER_BLOCK + 1];  // prefix sums of k-mer positions per window
+    __shared__ uint32_t n_had;
+    const uint32_t t = threadIdx.x;
+    for (uint32_t s = t; s < LDS_SLOTS; s += EXACT_THREADS) {
+        lkeys[s] = EMPTY;
+        lcnt[s] = 0;
+    }
+    const uint32_t w0 = blockIdx.x * EXACT_WINDOWS_PER_BLOCK;
+    const uint32_t nw = min((uint32_t)EXACT_WINDOWS_PER_BLOCK, a.n_windows - w0);
+    if (t == 0) {
+        uint32_t acc = 0;
+        for (uint32_t i = 0; i < nw; ++i) {
+            wpos[i] = acc;
+            const uint64_t st = a.start[w0 + i];
+            const uint32_t len = a.length[w0 + i];
+            const bool ok = !(st & 31u) && st + len <= a.n_bases;  // malformed windows hold no k-mers
+            acc += (ok && len >= a.k) ? len - a.k + 1u : 0u;
+        }
+        wpos[nw] = acc;
+        n_had = 0;
+    }
+    __syncthreads();
+    const uint32_t total = wpos[nw];
+    const uint64_t kmask = (1ull << a.k) - 1ull;  // N flags of the k bases (k <= 32)
+    uint32_t had = 0;
+    for (uint32_t p = t; p < total; p += EXACT_THREADS) {
+        uint32_t i = 0;
+        while (wpos[i + 1] <= p) ++i;  // <= EXACT_WINDOWS_PER_BLOCK steps
+        const uint64_t b = a.start[w0 + i] + (p - wpos[i]);
+        const uint64_t nbits = gather_bits(a.nmask, b, 1u, a.k, a.n_bases >> 5) & kmask;
+        if (nbits) {  // count_kmers skips k-mers holding an N (approx_counter.cpp:498, 513-517)
+            ++had;
+            continue;
+        }
+        const uint64_t key = to_dna2int(gather_bits(a.codes, b, 2u, 2u * a.k, a.n_bases >> 4), a.k);
+        if (key == EMPTY) {
+            atomicAdd(&a.special[0], 1u);
+            continue;
+        }
+        uint32_t h = (uint32_t)mix64(key) & (LDS_SLOTS - 1u);
+        bool done = false;
+        for (uint32_t probe = 0; probe < LDS_PROBES; ++probe) {
+            unsigned long long cur = lkeys[h];
+            if (cur == EMPTY) {
+                cur = atomicCAS(&lkeys[h], (unsigned long long)EMPTY, (unsigned long long)key);
+                if (cur == EMPTY) cur = key;
+            }
+            if (cur == key) {
+                atomicAdd(&lcnt[h], 1u);
+                done = true;
+                break;
+            }
+            h = (h + 1u) & (LDS_SLOTS - 1u);
+        }
+        if (!done) global_insert(a, key, 1u);
+    }
+    if (had) atomicAdd(&n_had, had);
+    __syncthreads();
+    for (uint32_t s = t; s < LDS_SLOTS; s += EXACT_THREADS)
+        if (lkeys[s] != EMPTY) global_insert(a, lkeys[s], lcnt[s]);
+    if (t == 0 && n_had) atomicAdd(a.had_n, (unsigned long long)n_had);
+}
+
+// getComplexity (approx_counter.cpp:247-267): dimer counts (16 bins, 8 bits
+// each, packed in two registers: no scratch-indexed array), their sum of
+// v*(v-1), then one float division exactly as the reference.
+__device__ __forceinline__ float complexity(uint64_t kmer, uint32_t k) {
+    uint64_t lo = 0, hi = 0;  // bins 0..7 / 8..15
+    for (uint32_t i = 0; i + 1 < k; ++i) {
+        const uint32_t d = (uint32_t)(kmer & 15u);
+        const uint64_t one = 1ull << (8u * (d & 7u));
+        if (d < 8u) lo += one;
+        else hi += one;
+        kmer >>= 2;
+    }
+    uint32_t sum = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint32_t a = (uint32_t)(lo >> (8 * i)) & 0xffu, b = (uint32_t)(hi >> (8 * i)) & 0xffu;
+        sum += a * (a - 1u) + b * (b - 1u);  // 0 * (0 - 1) wraps to 0, as in the reference
+    }
+    return (float)sum / (float)(2 * ((int)k - 2));
+}
+
+__device__ __forceinline__ bool is_forbidden(const ExactArgs& a, uint64_t key) {
+    uint32_t lo = 0, hi = a.n_forbidden;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        const uint64_t v = a.forbidden[mid];
+        if (v == key) return true;
+        if (v < key) lo = mid + 1;
+        else hi = mid;
+    }
+    return false;
+}
+
+// Kept (not low-complexity, not forbidden) entry count at slot s, 0 if none.
+// Slot a.slots is the all-T 32-mer kept apart from the table.
+__device__ __forceinline__ uint32_t kept_count(const ExactArgs& a, uint64_t s, uint64_t& key) {
+    uint32_t c;
+    if (s == a.slots) {
+        key = EMPTY;
+        c = a.special[0];
+    } else {
+        key = a.keys[s];
+        if (key == EMPTY) return 0;
+        c = a.cnts[s];
+    }
+    if (!c) return 0;
+    if (complexity(key, a.k) >= a.lc_threshold) return 0;  // haveLowComplexity (214-234)
+    if (is_forbidden(a, key)) return 0;                    // isForbiddenKmer (330-332)
+    return c;
+}
+
+__global__ __launch_bounds__(EXACT_THREADS) void exact_scan_kernel(ExactArgs a) {
+    __shared__ uint32_t hist[EXACT_HIST_BINS];
+    for (uint32_t i = threadIdx.x; i < EXACT_HIST_BINS; i += EXACT_THREADS) hist[i] = 0;
+    __syncthreads();
+    const uint64_t n = a.slots + 1;
+    for (uint64_t s = (uint64_t)blockIdx.x * EXACT_THREADS + threadIdx.x; s < n; s += (uint64_t)gridDim.x * EXACT_THREADS) {
+        uint64_t key;
+        const uint32_t c = kept_count(a, s, key);
+        if (c) atomicAdd(&hist[min(c, (uint32_t)EXACT_HIST_BINS - 1u)], 1u);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < EXACT_HIST_BINS; i += EXACT_THREADS)
+        if (hist[i]) atomicAdd(&a.hist[i], hist[i]);
+}
+
+__global__ __launch_bounds__(EXACT_THREADS) void exact_gather_kernel(ExactArgs a) {
+    const uint64_t n = a.slots + 1;
+    for (uint64_t s = (uint64_t)blockIdx.x * EXACT_THREADS + threadIdx.x; s < n; s += (uint64_t)gridDim.x * EXACT_THREADS) {
+        uint64_t key;
+        const uint32_t c = kept_count(a, s, key);
+        if (c && c >= a.threshold) {
+            const unsigned long long i = atomicAdd(a.n_out, 1ull);
+            if (i < a.out_cap) {
+                a.out_keys[i] = key;
+                a.out_cnts[i] = c;
+            }
+        }
+    }
+}
+
+}  // namespace
+
+hipError_t launch_exact_insert(const ExactArgs& a, hipStream_t stream) {
+    const uint32_t blocks = (a.n_windows + EXACT_WINDOWS_PER_BLOCK - 1) / EXACT_WINDOWS_PER_BLOCK;
+    if (!blocks) return hipSuccess;
+    hipLaunchKernelGGL(exact_insert_kernel, dim3(blocks), dim3(EXACT_THREADS), 0, stream, a);
+    return hipGetLastError();
+}
+
+static uint32_t scan_blocks(const ExactArgs& a) {
+    const uint64_t n = a.slots + 1;
+    return (uint32_t)std::min<uint64_t>(4096, (n + EXACT_THREADS - 1) / EXACT_THREADS);
+}
+
+hipError_t launch_exact_scan(const ExactArgs& a, hipStream_t stream) {
+    hipLaunchKernelGGL(exact_scan_kernel, dim3(scan_blocks(a)), dim3(EXACT_THREADS), 0, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_exact_gather(const ExactArgs& a, hipStream_t stream) {
+    hipLaunchKernelGGL(exact_gather_kernel, dim3(scan_blocks(a)), dim3(EXACT_THREADS), 0, stream, a);
+    return hipGetLastError();
+}
+
+}  // namespace acamd

@@ -115,6 +115,45 @@ ac_status ac_error_count_device_accumulate(ac_ctx* ctx, uint32_t k, const ac_seg
                                            uint32_t n_segments, void* hip_stream);
 
 /*
+ * Device copy of a packed sample, owned by the context (valid until the next
+ * ac_sample_upload on ctx or ac_destroy).  Lets one upload serve both the
+ * exact count and the approximate count of one read end.  The closest
+ * reference step is the index build over the sample (approx_counter.cpp:537-541).
+ * `dev` receives the device pointers.
+ */
+ac_status ac_sample_upload(ac_ctx* ctx, const ac_windows* host, ac_windows* dev);
+
+/*
+ * count_kmers (approx_counter.cpp:487-519) + get_most_frequent (396-405) or,
+ * with solid > 0, get_solid_kmers (372-388), on the GPU over a device sample:
+ * exact counts of the k-mers of every window that hold no N, pass the
+ * low-complexity filter (float DUST score >= lc_threshold is dropped,
+ * 214-234; lc_threshold already adjusted for k, 183-186) and are not in
+ * `forbidden` (host array, any order, 330-332).  Writes the kept k-mers in
+ * CompareCount order (275-305): the first `limit` of them, or all with count >=
+ * solid when solid > 0 (the reference does not truncate solid k-mers).
+ * *n_out = number written; if more than `capacity` are due, nothing is written,
+ * *n_out = the number needed and AC_ERR_INVALID is returned.  *n_distinct =
+ * distinct kept k-mers (the reference's count.size(), 883), *had_n = k-mer
+ * positions skipped for holding an N (513-517).  Synchronous.
+ */
+ac_status ac_exact_count_device(ac_ctx* ctx, uint32_t k, const ac_windows* dev, float lc_threshold,
+                                const uint64_t* forbidden, uint32_t n_forbidden, uint64_t limit, uint64_t solid,
+                                uint64_t* kmers_out, uint64_t* counts_out, uint64_t capacity, uint64_t* n_out,
+                                uint64_t* n_distinct, uint64_t* had_n);
+
+/* Same with a host sample (uploads it with ac_sample_upload first). */
+ac_status ac_exact_count(ac_ctx* ctx, uint32_t k, const ac_windows* host, float lc_threshold,
+                         const uint64_t* forbidden, uint32_t n_forbidden, uint64_t limit, uint64_t solid,
+                         uint64_t* kmers_out, uint64_t* counts_out, uint64_t capacity, uint64_t* n_out,
+                         uint64_t* n_distinct, uint64_t* had_n);
+
+/* ac_error_count over a device sample from ac_sample_upload: host k-mers in,
+ * host counts out, synchronous (errorCount, approx_counter.cpp:531-601). */
+ac_status ac_error_count_sample(ac_ctx* ctx, uint32_t k, const uint64_t* kmers, uint32_t n_kmers,
+                                const ac_windows* dev, uint64_t* counts);
+
+/*
  * Host packing of Dna5 windows into a window image (no reference counterpart:
  * SeqAn keeps 1 byte per base; this is the boundary's wire format).
  *   dna5     : window bytes, ordValues 0..3 for ACGT, >= 4 for N

@@ -11,7 +11,9 @@ while [ $# -gt 1 ]; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Iinclude -Iapprox_counter_amd/csrc $flags \
     -c approx_counter_amd/csrc/wm_count.hip -o $out/wm_count.o
   /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Iinclude -Iapprox_counter_amd/csrc $flags \
+    -c approx_counter_amd/csrc/exact_count.hip -o $out/exact_count.o
+  /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Iinclude -Iapprox_counter_amd/csrc $flags \
     -x hip -c approx_counter_amd/csrc/capi.cpp -o $out/capi.o
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $out/libapprox_counter_amd.so $out/wm_count.o $out/capi.o
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $out/libapprox_counter_amd.so $out/wm_count.o $out/exact_count.o $out/capi.o
   echo "built $out"
 done
