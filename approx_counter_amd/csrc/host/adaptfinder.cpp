@@ -70,6 +70,7 @@ const Opt OPTS[] = {
     {"o", "out_file", Kind::String, "path to the output file, default is ./out.txt"},
     {"g", "gpus", Kind::Int, "[MI355X build] number of GPUs of this node to shard the count over, default 1"},
     {"", "seed", Kind::Int, "[MI355X build] seed of the read sampling, default: std::random_device"},
+    {"", "host-exact", Kind::Flag, "[MI355X build] exact k-mer count on the host CPU instead of the GPU"},
 };
 
 struct Args {
@@ -267,6 +268,43 @@ pair_vector error_count(Devices& dev, const SeqSet& sample, const pair_vector& f
     return out;
 }
 
+// Opens one context per shard (-g N: shard g on device g mod visible devices).
+void open_devices(Devices& dev, uint64_t n_gpus) {
+    if (!dev.ctx.empty()) return;
+    if (n_gpus < 1) n_gpus = 1;
+    const int n_dev = ac_device_count();
+    if (n_dev < 1) throw std::runtime_error("no HIP device available (the approximate count runs on the GPU only)");
+    if ((int)n_gpus > n_dev)
+        std::cerr << "/!\\ WARNING: " << n_gpus << " shards requested on " << n_dev << " visible GPU(s)\n";
+    for (uint64_t g = 0; g < n_gpus; ++g) {
+        ac_ctx* c = nullptr;
+        if (ac_create(&c, (int)(g % (uint64_t)n_dev)) != AC_OK) throw std::runtime_error(ac_last_error(nullptr));
+        dev.ctx.push_back(c);
+    }
+}
+
+// count_kmers + get_most_frequent / get_solid_kmers (approx_counter.cpp:874-899)
+// on the GPU over a sample already uploaded to ctx (ac_exact_count_device).
+pair_vector exact_count_gpu(ac_ctx* ctx, const ac_windows& dsample, uint32_t k, float lc, const kmer_set& forbidden,
+                            uint64_t limit, uint64_t solid, uint64_t* n_distinct, uint64_t* had_n) {
+    std::vector<uint64_t> fb(forbidden.begin(), forbidden.end());
+    uint64_t cap = std::max<uint64_t>(1, solid ? 4096 : limit);
+    for (;;) {
+        std::vector<uint64_t> km(cap), ct(cap);
+        uint64_t n_out = 0;
+        const ac_status st = ac_exact_count_device(ctx, k, &dsample, lc, fb.data(), (uint32_t)fb.size(), limit, solid,
+                                                   km.data(), ct.data(), cap, &n_out, n_distinct, had_n);
+        if (st == AC_ERR_INVALID && n_out > cap) {  // solid mode: more solid k-mers than room
+            cap = n_out;
+            continue;
+        }
+        if (st != AC_OK) throw std::runtime_error(std::string("exact count failed: ") + ac_last_error(ctx));
+        pair_vector out(n_out);
+        for (uint64_t i = 0; i < n_out; ++i) out[i] = {km[i], ct[i]};
+        return out;
+    }
+}
+
 }  // namespace
 
 int main(int argc, char const** argv) {
@@ -316,6 +354,7 @@ int main(int argc, char const** argv) {
     get_option(args, "gpus", n_gpus);
     get_option(args, "seed", seed_str);
     skip_end = skip_end || args.val.count("skip_end");
+    const bool host_exact = args.val.count("host-exact") > 0;
     const std::string input_file = args.input;
 
     kmer_set forbidden;
@@ -375,22 +414,36 @@ int main(int argc, char const** argv) {
             SeqSet sample = sample_sequences(seqs, sn, sl, bottom, rng);
             if (mr_v > 0) print("Sampled " + std::to_string(sample.size()) + " sequences", 1);
             if (mr_v > 0) print("Exact k-mer count", tab_level);
-            uint64_t had_n = 0;
-            pair_vector count = count_kmers(sample, (uint32_t)k, lc, forbidden, &had_n);
+            uint64_t had_n = 0, n_found = 0;
+            pair_vector first_n;
+            Packed packed;
+            ac_windows dsample{};
+            if (host_exact) {  // the reference's host stages (approx_counter.cpp:874-899)
+                pair_vector count = count_kmers(sample, (uint32_t)k, lc, forbidden, &had_n);
+                n_found = count.size();
+                first_n = solid_km != 0 ? get_solid_kmers(std::move(count), solid_km, (uint32_t)k)
+                                        : get_most_frequent(std::move(count), limit, (uint32_t)k);
+            } else {  // the same on GPU 0; the uploaded sample also serves the approximate count
+                try {
+                    open_devices(dev, n_gpus);
+                    packed = pack(sample, 0, sample.size());
+                    const ac_windows hw = packed.view();
+                    if (ac_sample_upload(dev.ctx[0], &hw, &dsample) != AC_OK)
+                        throw std::runtime_error(ac_last_error(dev.ctx[0]));
+                    first_n = exact_count_gpu(dev.ctx[0], dsample, (uint32_t)k, lc, forbidden, limit, solid_km,
+                                              &n_found, &had_n);
+                } catch (const std::exception& e) {
+                    std::cerr << error_pref << "exact count failed: " << e.what() << std::endl;
+                    return 1;
+                }
+            }
             if (had_n > 0) {
                 std::cerr << "/!\\ WARNING: This dataset contained sequences with 'N' symbols. ";
                 std::cerr << "/!\\ WARNING: Current implementation ignores k-mers containing 'N'.";
                 std::cerr << "/!\\ WARNING: A total of " << had_n << " k-mers were ignored." << std::endl;
             }
-            if (mr_v > 0) print("Number of kmer found: " + std::to_string(count.size()), tab_level);
-            pair_vector first_n;
-            if (solid_km != 0) {
-                if (mr_v > 0) print("Keeping solid k-mer", tab_level);
-                first_n = get_solid_kmers(std::move(count), solid_km, (uint32_t)k);
-            } else {
-                if (mr_v > 0) print("Keeping most frequent k-mer", tab_level);
-                first_n = get_most_frequent(std::move(count), limit, (uint32_t)k);
-            }
+            if (mr_v > 0) print("Number of kmer found: " + std::to_string(n_found), tab_level);
+            if (mr_v > 0) print(solid_km != 0 ? "Keeping solid k-mer" : "Keeping most frequent k-mer", tab_level);
             if (mr_v > 0) print("Number of kmer kept:  " + std::to_string(first_n.size()), tab_level);
             if (!exact_out.empty()) {
                 if (mr_v > 0) print("Exporting exact kmer count", tab_level);
@@ -403,21 +456,18 @@ int main(int argc, char const** argv) {
             if (mr_v > 0) print("Approximate k-mer count", tab_level);
             pair_vector error_counter;
             try {
-                if (dev.ctx.empty()) {
-                    // -g N: N window shards, shard g on device g mod (visible devices).
-                    if (n_gpus < 1) n_gpus = 1;
-                    const int n_dev = ac_device_count();
-                    if (n_dev < 1) throw std::runtime_error("no HIP device available (the approximate count runs on the GPU only)");
-                    if ((int)n_gpus > n_dev)
-                        std::cerr << warning << n_gpus << " shards requested on " << n_dev << " visible GPU(s)\n";
-                    for (uint64_t g = 0; g < n_gpus; ++g) {
-                        ac_ctx* c = nullptr;
-                        if (ac_create(&c, (int)(g % (uint64_t)n_dev)) != AC_OK)
-                            throw std::runtime_error(ac_last_error(nullptr));
-                        dev.ctx.push_back(c);
-                    }
+                open_devices(dev, n_gpus);
+                if (!host_exact && dev.ctx.size() == 1) {  // one GPU: count on the sample uploaded above
+                    std::vector<uint64_t> km(first_n.size()), ct(first_n.size());
+                    for (size_t i = 0; i < first_n.size(); ++i) km[i] = first_n[i].first;
+                    if (!km.empty() && ac_error_count_sample(dev.ctx[0], (uint32_t)k, km.data(), (uint32_t)km.size(),
+                                                             &dsample, ct.data()) != AC_OK)
+                        throw std::runtime_error(ac_last_error(dev.ctx[0]));
+                    error_counter.resize(km.size());
+                    for (size_t i = 0; i < km.size(); ++i) error_counter[i] = {km[i], ct[i]};
+                } else {
+                    error_counter = error_count(dev, sample, first_n, (uint32_t)k);
                 }
-                error_counter = error_count(dev, sample, first_n, (uint32_t)k);
             } catch (const std::exception& e) {
                 std::cerr << error_pref << "approximate count failed: " << e.what() << std::endl;
                 return 1;

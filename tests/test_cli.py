@@ -58,10 +58,22 @@ def _params():
 def test_exact_file_then_loud_gpu_failure(tmp_path):
     p = _params()
     r = run([os.path.join(CFG1, "reads.fa"), "-k", p["k"], "-sn", p["n_reads"], "-sl", p["sl"], "-lim", p["lim"],
-             "-e", "exact", "-o", "out.txt"], tmp_path)
+             "-e", "exact", "-o", "out.txt", "--host-exact"], tmp_path)
     assert r.returncode == 1
     assert "no HIP device" in r.stderr
     assert open(tmp_path / "exact_0.start").read() == open(os.path.join(CFG1, "exact_0.start")).read()
+    assert not (tmp_path / "out.txt_0.start").exists()
+
+
+@pytest.mark.skipif(_has_gpu(), reason="checks the no-GPU failure path")
+def test_gpu_exact_count_fails_loudly_without_gpu(tmp_path):
+    # default: the exact count runs on the GPU too, so nothing is written and no host fallback is taken
+    p = _params()
+    r = run([os.path.join(CFG1, "reads.fa"), "-k", p["k"], "-sn", p["n_reads"], "-sl", p["sl"], "-lim", p["lim"],
+             "-e", "exact", "-o", "out.txt"], tmp_path)
+    assert r.returncode == 1
+    assert "exact count failed" in r.stderr and "no HIP device" in r.stderr
+    assert not (tmp_path / "exact_0.start").exists()
     assert not (tmp_path / "out.txt_0.start").exists()
 
 
@@ -71,7 +83,7 @@ def test_config_file_and_cli_precedence(tmp_path):
     conf = tmp_path / "ac.conf"
     # config sets everything; the CLI overrides lim (approx_counter.cpp:744-755)
     conf.write_text(f"# comment\nk = {p['k']}\nsn={p['n_reads']}\nsl={p['sl']}\nlim=7\ne=fromconf\nv=0\n")
-    r = run([os.path.join(CFG1, "reads.fa"), "-conf", conf, "-lim", p["lim"]], tmp_path)
+    r = run([os.path.join(CFG1, "reads.fa"), "-conf", conf, "-lim", p["lim"], "--host-exact"], tmp_path)
     assert r.returncode == 1
     assert open(tmp_path / "fromconf_0.start").read() == open(os.path.join(CFG1, "exact_0.start")).read()
     assert r.stdout == ""  # v=0 from the config silences the parameter dump
@@ -89,7 +101,7 @@ def test_forbidden_kmers_and_fastq(tmp_path):
         for i, s in zip(ids, seqs):
             fh.write(f"@{i}\n{s}\n+\n{'I' * len(s)}\n")
     r = run([tmp_path / "reads.fq", "-k", p["k"], "-sn", p["n_reads"], "-sl", p["sl"], "-lim", p["lim"],
-             "-e", "exact", "-fk", "fk.txt"], tmp_path)
+             "-e", "exact", "-fk", "fk.txt", "--host-exact"], tmp_path)
     assert r.returncode == 1
     got = open(tmp_path / "exact_0.start").read().splitlines()
     assert not any(g.split("\t")[0] in banned for g in got)

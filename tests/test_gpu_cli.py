@@ -61,3 +61,36 @@ def test_solid_mode(tmp_path):
         exact, approx, _ = host_ref.run_end(seqs, P["k"], P["sl"], P["lim"], 1.0, bottom, solid=solid)
         assert open(tmp_path / f"se_0.{end}").read() == host_ref.export_lines(exact, P["k"])
         assert open(tmp_path / f"s_0.{end}").read() == host_ref.export_lines(approx, P["k"])
+
+
+@pytest.mark.parametrize("extra", [
+    [],
+    ["-lc", "1.5", "-k", 12],
+    ["-sk", 25],
+    ["-lim", 2000, "-k", 8],
+])
+def test_gpu_exact_stage_equals_host_stage(tmp_path, extra):
+    """The default (GPU exact count + selection, sample uploaded once) writes the same
+    files as --host-exact (the reference's host stages, approx_counter.cpp:874-899),
+    here with N symbols, forbidden k-mers and FASTQ input."""
+    _, seqs = host_ref.read_fasta(os.path.join(CFG1, "reads.fa"))
+    with open(tmp_path / "reads.fq", "w") as fh:
+        for i, s in enumerate(seqs):
+            if i % 7 == 0:
+                s = s[:30] + "N" + s[31:]
+            if i % 11 == 0:
+                s = "A" * 40 + s[40:]  # low-complexity prefix for -lc
+            fh.write(f"@r{i}\n{s}\n+\n{'I' * len(s)}\n")
+    banned = golden("exact_0.start").splitlines()[2].split("\t")[0]
+    (tmp_path / "fk.txt").write_text(banned + "\n")
+    args = ["reads.fq", "-k", P["k"], "-sn", P["n_reads"], "-sl", P["sl"], "-lim", P["lim"], "-fk", "fk.txt"] + extra
+    a = run(args + ["-e", "ge", "-o", "go"], tmp_path)
+    b = run(args + ["-e", "he", "-o", "ho", "--host-exact"], tmp_path)
+    assert a.returncode == 0 and b.returncode == 0, (a.stderr, b.stderr)
+    assert "A total of" in a.stderr and a.stderr.count("WARNING") == b.stderr.count("WARNING")
+    for end in ("start", "end"):
+        assert open(tmp_path / f"ge_0.{end}").read() == open(tmp_path / f"he_0.{end}").read(), end
+        assert open(tmp_path / f"go_0.{end}").read() == open(tmp_path / f"ho_0.{end}").read(), end
+    found = [l for l in a.stdout.splitlines() if "Number of kmer found" in l]
+    assert found and [l.split("]")[-1] for l in found] == \
+        [l.split("]")[-1] for l in b.stdout.splitlines() if "Number of kmer found" in l]
