@@ -356,21 +356,24 @@ ac_status ac_exact_count_device(ac_ctx* ctx, uint32_t k, const ac_windows* dev, 
         return fail(ctx, AC_ERR_INVALID, "NULL output or forbidden array");
     AC_HIP(ctx, hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
-    // Table: a power of two >= 2 x the image size (an upper bound on k-mer positions): load <= 1/2.
+    // Table: a power of two >= 1.5 x the image size (an upper bound on k-mer
+    // positions): load <= 2/3 even when every position is a new k-mer.
     uint64_t slots = 1024;
-    while (slots < 2 * dev->n_bases) slots <<= 1;
-    // small block: special[0..1] u32, had_n u64, n_out u64, hist[EXACT_HIST_BINS] u32
+    while (slots < dev->n_bases + dev->n_bases / 2) slots <<= 1;
+    // Kept entries seen >= EXACT_LIST_MIN (2) times: at most n_bases / 2 (+ the all-T 32-mer).
+    const uint64_t list_cap = dev->n_bases / 2 + 2;
+    // small block: special[0..1] u32, had_n u64 @16, n_out u64 @24, n_list u64 @32, hist[EXACT_HIST_BINS] u32 @64
     const size_t small_bytes = 64 + sizeof(uint32_t) * EXACT_HIST_BINS;
     std::vector<uint64_t> fb(forbidden, forbidden + n_forbidden);
     std::sort(fb.begin(), fb.end());
     fb.erase(std::unique(fb.begin(), fb.end()), fb.end());
-    if (ac_status s2 = grow(ctx, &ctx->e_buf[0], &ctx->e_cap[0], sizeof(uint64_t) * slots)) return s2;
-    if (ac_status s2 = grow(ctx, &ctx->e_buf[1], &ctx->e_cap[1], sizeof(uint32_t) * slots)) return s2;
+    if (ac_status s2 = grow(ctx, &ctx->e_buf[0], &ctx->e_cap[0], sizeof(acamd::ExactSlot) * slots)) return s2;
+    if (ac_status s2 = grow(ctx, &ctx->e_buf[1], &ctx->e_cap[1], (sizeof(uint64_t) + sizeof(uint32_t)) * list_cap))
+        return s2;
     if (ac_status s2 = grow(ctx, &ctx->e_buf[2], &ctx->e_cap[2], small_bytes)) return s2;
     if (ac_status s2 = grow(ctx, &ctx->e_buf[3], &ctx->e_cap[3], sizeof(uint64_t) * std::max<size_t>(1, fb.size())))
         return s2;
-    AC_HIP(ctx, hipMemsetAsync(ctx->e_buf[0], 0xff, sizeof(uint64_t) * slots, st));
-    AC_HIP(ctx, hipMemsetAsync(ctx->e_buf[1], 0, sizeof(uint32_t) * slots, st));
+    AC_HIP(ctx, hipMemsetAsync(ctx->e_buf[0], 0, sizeof(acamd::ExactSlot) * slots, st));
     AC_HIP(ctx, hipMemsetAsync(ctx->e_buf[2], 0, small_bytes, st));
     if (!fb.empty())
         AC_HIP(ctx, hipMemcpyAsync(ctx->e_buf[3], fb.data(), sizeof(uint64_t) * fb.size(), hipMemcpyHostToDevice, st));
@@ -384,14 +387,17 @@ ac_status ac_exact_count_device(ac_ctx* ctx, uint32_t k, const ac_windows* dev, 
     a.n_bases = dev->n_bases;
     a.n_windows = dev->n_windows;
     a.k = k;
-    a.keys = (uint64_t*)ctx->e_buf[0];
-    a.cnts = (uint32_t*)ctx->e_buf[1];
+    a.table = (acamd::ExactSlot*)ctx->e_buf[0];
     a.slots = slots;
     a.mask = slots - 1;
     a.special = (uint32_t*)small;
     a.had_n = (unsigned long long*)(small + 16);
     a.n_out = (unsigned long long*)(small + 24);
+    a.n_list = (unsigned long long*)(small + 32);
     a.hist = (uint32_t*)(small + 64);
+    a.list_keys = (uint64_t*)ctx->e_buf[1];
+    a.list_cnts = (uint32_t*)((char*)ctx->e_buf[1] + sizeof(uint64_t) * list_cap);
+    a.list_cap = list_cap;
     a.lc_threshold = lc_threshold;
     a.forbidden = (const uint64_t*)ctx->e_buf[3];
     a.n_forbidden = (uint32_t)fb.size();
@@ -405,6 +411,8 @@ ac_status ac_exact_count_device(ac_ctx* ctx, uint32_t k, const ac_windows* dev, 
     for (int i = 0; i < EXACT_HIST_BINS; ++i) kept += hist[i];
     if (n_distinct) *n_distinct = kept;
     if (had_n) *had_n = *(const unsigned long long*)(h_small.data() + 16);
+    const uint64_t n_list = *(const unsigned long long*)(h_small.data() + 32);
+    if (n_list > list_cap) return fail(ctx, AC_ERR_INTERNAL, "exact count: candidate list overflow");
     // Threshold: solid mode keeps count >= solid; otherwise the largest count c
     // such that at least `limit` kept entries have count >= c (all if fewer).
     uint64_t thr = 1, due = kept;
@@ -431,7 +439,7 @@ ac_status ac_exact_count_device(ac_ctx* ctx, uint32_t k, const ac_windows* dev, 
     a.out_keys = (uint64_t*)ctx->e_buf[4];
     a.out_cnts = (uint32_t*)ctx->e_buf[5];
     a.out_cap = gather_cap;
-    AC_HIP(ctx, acamd::launch_exact_gather(a, st));
+    AC_HIP(ctx, acamd::launch_exact_gather(a, thr >= EXACT_LIST_MIN, n_list, st));
     unsigned long long got = 0;
     AC_HIP(ctx, hipMemcpyAsync(&got, a.n_out, sizeof got, hipMemcpyDeviceToHost, st));
     AC_HIP(ctx, hipStreamSynchronize(st));

@@ -3,10 +3,19 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#ifndef EXACT_WINDOWS_PER_BLOCK
 #define EXACT_WINDOWS_PER_BLOCK 16  // windows aggregated per workgroup in LDS
+#endif
 #define EXACT_HIST_BINS 4096        // count histogram (last bin collects larger counts)
+#define EXACT_LIST_MIN 2            // the scan compacts kept entries with at least this count
 
 namespace acamd {
+
+struct alignas(16) ExactSlot {
+    uint64_t key;  // k-mer + 1; 0 = empty
+    uint32_t cnt;
+    uint32_t pad;
+};
 
 struct ExactArgs {
     // window image (device)
@@ -17,10 +26,11 @@ struct ExactArgs {
     uint64_t n_bases;
     uint32_t n_windows;
     uint32_t k;
-    // hash table: `slots` (a power of two) keys + counts; slot index `slots`
-    // (past the table) stands for the all-T 32-mer, counted in special[0]
-    uint64_t* keys;
-    uint32_t* cnts;
+    // hash table: `slots` (a power of two) 16-byte slots {k-mer + 1, count};
+    // stored key 0 = empty, so a zero memset clears it.  Slot index `slots`
+    // (past the table) stands for the all-T 32-mer (whose key + 1 wraps to 0),
+    // counted in special[0].
+    ExactSlot* table;
     uint64_t slots;
     uint64_t mask;
     uint32_t* special;
@@ -29,8 +39,15 @@ struct ExactArgs {
     float lc_threshold;
     const uint64_t* forbidden;  // sorted
     uint32_t n_forbidden;
-    // scan / gather
+    // scan: count histogram of the kept entries, and the kept entries with
+    // count >= EXACT_LIST_MIN compacted into list_keys/list_cnts
     uint32_t* hist;  // EXACT_HIST_BINS
+    uint64_t* list_keys;
+    uint32_t* list_cnts;
+    unsigned long long* n_list;
+    uint64_t list_cap;
+    // gather: entries with count >= threshold, from the list (threshold >=
+    // EXACT_LIST_MIN) or from the whole table
     uint32_t threshold;
     uint64_t* out_keys;
     uint32_t* out_cnts;
@@ -40,6 +57,7 @@ struct ExactArgs {
 
 hipError_t launch_exact_insert(const ExactArgs& a, hipStream_t stream);
 hipError_t launch_exact_scan(const ExactArgs& a, hipStream_t stream);
-hipError_t launch_exact_gather(const ExactArgs& a, hipStream_t stream);
+// from_list: gather from the scan's compacted list of n_list entries, else from the table
+hipError_t launch_exact_gather(const ExactArgs& a, bool from_list, uint64_t n_list, hipStream_t stream);
 
 }  // namespace acamd

@@ -14,10 +14,12 @@
 //  2. scan: every occupied slot passes the low-complexity filter (the float
 //     DUST score of approx_counter.cpp:247-267, computed exactly as the
 //     reference does) and the forbidden set (binary search); kept entries feed
-//     a count histogram.
+//     a count histogram, and those seen at least twice (EXACT_LIST_MIN) are
+//     compacted into a list -- most distinct k-mers of a read sample occur once.
 //  3. gather: entries with count >= a threshold chosen on the host from the
-//     histogram (the smallest count that still yields `limit` entries, or
-//     the solid threshold) are compacted; the host ranks that short list with
+//     histogram (the largest count that still yields `limit` entries, or
+//     the solid threshold) are compacted from that list (from the table only
+//     when the threshold is 1); the host ranks the short result with
 //     CompareCount (approx_counter.cpp:275-305).
 // HBM-bound integer work (random atomics + streaming scans), no MFMA.
 #include <hip/hip_runtime.h>
@@ -31,7 +33,10 @@ namespace acamd {
 namespace {
 
 constexpr int EXACT_THREADS = 256;
-constexpr uint32_t LDS_SLOTS = 4096;        // per-workgroup aggregation table
+#ifndef EXACT_LDS_SLOTS
+#define EXACT_LDS_SLOTS 4096
+#endif
+constexpr uint32_t LDS_SLOTS = EXACT_LDS_SLOTS;  // per-workgroup aggregation table
 constexpr uint32_t LDS_PROBES = 32;         // beyond this a key goes straight to the global table
 constexpr uint64_t EMPTY = ~0ull;           // never a k-mer value except the all-T 32-mer (kept apart)
 
@@ -65,20 +70,19 @@ __device__ __forceinline__ uint64_t to_dna2int(uint64_t le, uint32_t k) {
     return r >> (64u - 2u * k);
 }
 
+// One CAS claims or finds the slot, one add on the same 16-byte slot counts.
 __device__ __forceinline__ void global_insert(const ExactArgs& a, uint64_t key, uint32_t c) {
     if (key == EMPTY) {  // the all-T 32-mer
         atomicAdd(&a.special[0], c);
         return;
     }
+    const unsigned long long stored = (unsigned long long)key + 1ull;
     uint64_t h = mix64(key) & a.mask;
     for (;;) {
-        uint64_t cur = a.keys[h];
-        if (cur == EMPTY) {
-            cur = atomicCAS((unsigned long long*)&a.keys[h], (unsigned long long)EMPTY, (unsigned long long)key);
-            if (cur == EMPTY) cur = key;
-        }
-        if (cur == key) {
-            atomicAdd(&a.cnts[h], c);
+        ExactSlot* sl = &a.table[h];
+        const unsigned long long cur = atomicCAS((unsigned long long*)&sl->key, 0ull, stored);
+        if (cur == 0ull || cur == stored) {
+            atomicAdd(&sl->cnt, c);
             return;
         }
         h = (h + 1u) & a.mask;
@@ -146,8 +150,10 @@ __global__ __launch_bounds__(EXACT_THREADS) void exact_insert_kernel(ExactArgs a
     }
     if (had) atomicAdd(&n_had, had);
     __syncthreads();
+#ifndef EXACT_TIMING_NO_GLOBAL  // timing-only builds: measure the LDS phase alone
     for (uint32_t s = t; s < LDS_SLOTS; s += EXACT_THREADS)
         if (lkeys[s] != EMPTY) global_insert(a, lkeys[s], lcnt[s]);
+#endif
     if (t == 0 && n_had) atomicAdd(a.had_n, (unsigned long long)n_had);
 }
 
@@ -184,17 +190,25 @@ __device__ __forceinline__ bool is_forbidden(const ExactArgs& a, uint64_t key) {
     return false;
 }
 
-// Kept (not low-complexity, not forbidden) entry count at slot s, 0 if none.
-// Slot a.slots is the all-T 32-mer kept apart from the table.
-__device__ __forceinline__ uint32_t kept_count(const ExactArgs& a, uint64_t s, uint64_t& key) {
+// One 16-byte load of slot s.
+// Unconditional (clamped address) so a thread's loads issue back to back; for
+// s >= slots the value is ignored by kept_count.
+__device__ __forceinline__ uint4 load_slot(const ExactArgs& a, uint64_t s) {
+    return *reinterpret_cast<const uint4*>(&a.table[s < a.slots ? s : a.slots - 1u]);
+}
+
+// Kept (not low-complexity, not forbidden) entry count of a loaded slot, 0 if
+// none; slot index a.slots is the all-T 32-mer kept apart from the table.
+__device__ __forceinline__ uint32_t kept_count(const ExactArgs& a, uint64_t s, uint4 v, uint64_t& key) {
     uint32_t c;
     if (s == a.slots) {
         key = EMPTY;
         c = a.special[0];
     } else {
-        key = a.keys[s];
-        if (key == EMPTY) return 0;
-        c = a.cnts[s];
+        const uint64_t stored = ((uint64_t)v.y << 32) | v.x;
+        if (!stored) return 0;
+        key = stored - 1ull;
+        c = v.z;
     }
     if (!c) return 0;
     if (complexity(key, a.k) >= a.lc_threshold) return 0;  // haveLowComplexity (214-234)
@@ -202,34 +216,121 @@ __device__ __forceinline__ uint32_t kept_count(const ExactArgs& a, uint64_t s, u
     return c;
 }
 
+// Block-level compaction: lanes append (key, count) to an LDS buffer; the
+// buffer goes to the global list with one atomic per flush, so the list
+// counter sees a few hundred atomics per launch instead of one per wave.
+constexpr uint32_t APPEND_BUF = 2048;
+
+struct BlockAppender {
+    uint64_t* keys;
+    uint32_t* cnts;
+    unsigned long long* n;
+    uint64_t cap;
+    uint64_t* lk;  // LDS
+    uint32_t* lc;  // LDS
+    uint32_t* ln;  // LDS
+    unsigned long long* lbase;
+
+    __device__ void push(bool want, uint64_t key, uint32_t c) {
+        if (want) {
+            const uint32_t i = atomicAdd(ln, 1u);
+            lk[i] = key;
+            lc[i] = c;
+        }
+    }
+    // Call from every thread of the block; flushes when `force` or nearly full.
+    __device__ void sync_flush(bool force) {
+        __syncthreads();
+        const uint32_t m = *ln;
+        if (!m || (!force && m + EXACT_THREADS <= APPEND_BUF)) return;  // block-uniform
+        if (threadIdx.x == 0) *lbase = atomicAdd(n, (unsigned long long)m);
+        __syncthreads();
+        const uint64_t b = *lbase;
+        for (uint32_t i = threadIdx.x; i < m; i += EXACT_THREADS)
+            if (b + i < cap) {
+                keys[b + i] = lk[i];
+                cnts[b + i] = lc[i];
+            }
+        __syncthreads();
+        if (threadIdx.x == 0) *ln = 0;
+        __syncthreads();
+    }
+};
+
+#define DECLARE_APPENDER(name, K, C, N, CAP)                                              \
+    __shared__ uint64_t name##_k[APPEND_BUF];                                             \
+    __shared__ uint32_t name##_c[APPEND_BUF];                                             \
+    __shared__ uint32_t name##_n;                                                         \
+    __shared__ unsigned long long name##_b;                                               \
+    if (threadIdx.x == 0) name##_n = 0;                                                   \
+    __syncthreads();                                                                      \
+    BlockAppender name{K, C, N, CAP, name##_k, name##_c, &name##_n, &name##_b};
+
+constexpr uint32_t SCAN_UNROLL = 4;  // slots per thread per trip: four 16-byte loads in flight
+
 __global__ __launch_bounds__(EXACT_THREADS) void exact_scan_kernel(ExactArgs a) {
     __shared__ uint32_t hist[EXACT_HIST_BINS];
+    DECLARE_APPENDER(app, a.list_keys, a.list_cnts, a.n_list, a.list_cap)
     for (uint32_t i = threadIdx.x; i < EXACT_HIST_BINS; i += EXACT_THREADS) hist[i] = 0;
     __syncthreads();
     const uint64_t n = a.slots + 1;
-    for (uint64_t s = (uint64_t)blockIdx.x * EXACT_THREADS + threadIdx.x; s < n; s += (uint64_t)gridDim.x * EXACT_THREADS) {
-        uint64_t key;
-        const uint32_t c = kept_count(a, s, key);
-        if (c) atomicAdd(&hist[min(c, (uint32_t)EXACT_HIST_BINS - 1u)], 1u);
+    const uint64_t step = (uint64_t)EXACT_THREADS * SCAN_UNROLL;
+    const uint64_t stride = (uint64_t)gridDim.x * step;
+    uint32_t ones = 0;  // kept entries seen once (the bulk): one LDS add per wave at the end
+    for (uint64_t s0 = (uint64_t)blockIdx.x * step; s0 < n; s0 += stride) {  // block-uniform trips
+        uint4 v[SCAN_UNROLL];
+        uint64_t key[SCAN_UNROLL];
+        uint32_t c[SCAN_UNROLL];
+#pragma unroll
+        for (uint32_t j = 0; j < SCAN_UNROLL; ++j) v[j] = load_slot(a, s0 + j * EXACT_THREADS + threadIdx.x);
+#pragma unroll
+        for (uint32_t j = 0; j < SCAN_UNROLL; ++j) {
+            const uint64_t s = s0 + j * EXACT_THREADS + threadIdx.x;
+            key[j] = 0;
+            c[j] = s < n ? kept_count(a, s, v[j], key[j]) : 0u;
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < SCAN_UNROLL; ++j) {
+            if (c[j] == 1u) ++ones;
+            else if (c[j]) atomicAdd(&hist[min(c[j], (uint32_t)EXACT_HIST_BINS - 1u)], 1u);
+            app.push(c[j] >= EXACT_LIST_MIN, key[j], c[j]);
+        }
+        app.sync_flush(false);
     }
+    app.sync_flush(true);
+    for (int off = 32; off; off >>= 1) ones += __shfl_xor(ones, off);
+    if (__lane_id() == 0 && ones) atomicAdd(&hist[1], ones);
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < EXACT_HIST_BINS; i += EXACT_THREADS)
         if (hist[i]) atomicAdd(&a.hist[i], hist[i]);
 }
 
-__global__ __launch_bounds__(EXACT_THREADS) void exact_gather_kernel(ExactArgs a) {
+// Entries with count >= threshold from the whole table (threshold below EXACT_LIST_MIN).
+__global__ __launch_bounds__(EXACT_THREADS) void exact_gather_table_kernel(ExactArgs a) {
+    DECLARE_APPENDER(app, a.out_keys, a.out_cnts, a.n_out, a.out_cap)
     const uint64_t n = a.slots + 1;
-    for (uint64_t s = (uint64_t)blockIdx.x * EXACT_THREADS + threadIdx.x; s < n; s += (uint64_t)gridDim.x * EXACT_THREADS) {
-        uint64_t key;
-        const uint32_t c = kept_count(a, s, key);
-        if (c && c >= a.threshold) {
-            const unsigned long long i = atomicAdd(a.n_out, 1ull);
-            if (i < a.out_cap) {
-                a.out_keys[i] = key;
-                a.out_cnts[i] = c;
-            }
-        }
+    const uint64_t stride = (uint64_t)gridDim.x * EXACT_THREADS;
+    for (uint64_t s0 = (uint64_t)blockIdx.x * EXACT_THREADS; s0 < n; s0 += stride) {
+        const uint64_t s = s0 + threadIdx.x;
+        uint64_t key = 0;
+        const uint32_t c = s < n ? kept_count(a, s, load_slot(a, s), key) : 0u;
+        app.push(c && c >= a.threshold, key, c);
+        app.sync_flush(false);
     }
+    app.sync_flush(true);
+}
+
+// Entries with count >= threshold from the scan's list (already filtered).
+__global__ __launch_bounds__(EXACT_THREADS) void exact_gather_list_kernel(ExactArgs a, uint64_t n) {
+    DECLARE_APPENDER(app, a.out_keys, a.out_cnts, a.n_out, a.out_cap)
+    const uint64_t stride = (uint64_t)gridDim.x * EXACT_THREADS;
+    for (uint64_t s0 = (uint64_t)blockIdx.x * EXACT_THREADS; s0 < n; s0 += stride) {
+        const uint64_t s = s0 + threadIdx.x;
+        const uint32_t c = s < n ? a.list_cnts[s] : 0u;
+        app.push(c >= a.threshold, s < n ? a.list_keys[s] : 0ull, c);
+        app.sync_flush(false);
+    }
+    app.sync_flush(true);
 }
 
 }  // namespace
@@ -241,18 +342,25 @@ hipError_t launch_exact_insert(const ExactArgs& a, hipStream_t stream) {
     return hipGetLastError();
 }
 
-static uint32_t scan_blocks(const ExactArgs& a) {
+static uint32_t scan_blocks(const ExactArgs& a, uint32_t per_thread) {
     const uint64_t n = a.slots + 1;
-    return (uint32_t)std::min<uint64_t>(4096, (n + EXACT_THREADS - 1) / EXACT_THREADS);
+    const uint64_t per_block = (uint64_t)EXACT_THREADS * per_thread;
+    return (uint32_t)std::min<uint64_t>(4096, (n + per_block - 1) / per_block);
 }
 
 hipError_t launch_exact_scan(const ExactArgs& a, hipStream_t stream) {
-    hipLaunchKernelGGL(exact_scan_kernel, dim3(scan_blocks(a)), dim3(EXACT_THREADS), 0, stream, a);
+    hipLaunchKernelGGL(exact_scan_kernel, dim3(scan_blocks(a, SCAN_UNROLL)), dim3(EXACT_THREADS), 0, stream, a);
     return hipGetLastError();
 }
 
-hipError_t launch_exact_gather(const ExactArgs& a, hipStream_t stream) {
-    hipLaunchKernelGGL(exact_gather_kernel, dim3(scan_blocks(a)), dim3(EXACT_THREADS), 0, stream, a);
+hipError_t launch_exact_gather(const ExactArgs& a, bool from_list, uint64_t n_list, hipStream_t stream) {
+    if (from_list) {
+        if (!n_list) return hipSuccess;
+        const uint32_t blocks = (uint32_t)std::min<uint64_t>(4096, (n_list + EXACT_THREADS - 1) / EXACT_THREADS);
+        hipLaunchKernelGGL(exact_gather_list_kernel, dim3(blocks), dim3(EXACT_THREADS), 0, stream, a, n_list);
+    } else {
+        hipLaunchKernelGGL(exact_gather_table_kernel, dim3(scan_blocks(a, 1)), dim3(EXACT_THREADS), 0, stream, a);
+    }
     return hipGetLastError();
 }
 
