@@ -70,7 +70,10 @@ const Opt OPTS[] = {
     {"o", "out_file", Kind::String, "path to the output file, default is ./out.txt"},
     {"g", "gpus", Kind::Int, "[MI355X build] number of GPUs of this node to shard the count over, default 1"},
     {"", "seed", Kind::Int, "[MI355X build] seed of the read sampling, default: std::random_device"},
-    {"", "host-exact", Kind::Flag, "[MI355X build] exact k-mer count on the host CPU instead of the GPU"},
+    {"", "host-exact", Kind::Flag,
+     "[MI355X build] the reference's host stages: whole reads in memory, exact k-mer count on the CPU"},
+    {"", "dump-sample", Kind::String,
+     "[MI355X build] write each sampled window image to <path>_<run>.<end> and stop before counting"},
 };
 
 struct Args {
@@ -185,34 +188,8 @@ void get_option(const Args& a, const char* n, std::string& out) {
 // errorCount (approx_counter.cpp:531-601) through the C ABI, windows sharded
 // over n_gpus devices (contiguous ranges balanced by bases), counts summed.
 // ---------------------------------------------------------------------------
-struct Packed {
-    std::vector<uint32_t> codes, nmask, length;
-    std::vector<uint64_t> start;
-    uint64_t n_bases = 32;
-    ac_windows view() const {
-        return ac_windows{codes.data(), nmask.data(), start.data(), length.data(), (uint32_t)length.size(), n_bases};
-    }
-};
-
-Packed pack(const SeqSet& s, size_t lo, size_t hi) {
-    Packed p;
-    std::vector<uint64_t> src(hi - lo);
-    std::vector<uint32_t> len(hi - lo);
-    for (size_t i = lo; i < hi; ++i) {
-        src[i - lo] = s.offset[i];
-        len[i - lo] = s.length[i];
-    }
-    p.n_bases = ac_image_bases(len.data(), (uint32_t)len.size());
-    p.codes.assign(p.n_bases / 16, 0);
-    p.nmask.assign(p.n_bases / 32, 0);
-    p.start.assign(std::max<size_t>(hi - lo, 1), 0);
-    p.length.assign(std::max<size_t>(hi - lo, 1), 0);
-    if (ac_pack_windows(s.bases.data(), src.data(), len.data(), (uint32_t)len.size(), p.codes.data(), p.nmask.data(),
-                        p.start.data(), p.length.data(), p.n_bases) != AC_OK)
-        throw std::runtime_error(std::string("window packing failed: ") + ac_last_error(nullptr));
-    p.start.resize(hi - lo);
-    p.length.resize(hi - lo);
-    return p;
+ac_windows view(const PackedImage& p) {
+    return ac_windows{p.codes.data(), p.nmask.data(), p.start.data(), p.length.data(), (uint32_t)p.size(), p.n_bases};
 }
 
 struct Devices {
@@ -222,7 +199,7 @@ struct Devices {
     }
 };
 
-pair_vector error_count(Devices& dev, const SeqSet& sample, const pair_vector& first_n, uint32_t k) {
+pair_vector error_count(Devices& dev, const PackedImage& img, const pair_vector& first_n, uint32_t k) {
     const size_t n = first_n.size();
     pair_vector out(n);
     if (n == 0) return out;
@@ -231,14 +208,14 @@ pair_vector error_count(Devices& dev, const SeqSet& sample, const pair_vector& f
     const size_t G = dev.ctx.size();
     // shard boundaries balanced by Σ window length
     uint64_t total = 0;
-    for (uint32_t l : sample.length) total += l;
-    std::vector<size_t> cut(G + 1, sample.size());
+    for (uint32_t l : img.length) total += l;
+    std::vector<size_t> cut(G + 1, img.size());
     cut[0] = 0;
     {
         uint64_t acc = 0;
         size_t g = 1;
-        for (size_t i = 0; i < sample.size() && g < G; ++i) {
-            acc += sample.length[i];
+        for (size_t i = 0; i < img.size() && g < G; ++i) {
+            acc += img.length[i];
             while (g < G && acc * G >= total * g) cut[g++] = i + 1;
         }
     }
@@ -248,8 +225,15 @@ pair_vector error_count(Devices& dev, const SeqSet& sample, const pair_vector& f
     for (size_t g = 0; g < G; ++g) {
         th.emplace_back([&, g] {
             try {
-                Packed p = pack(sample, cut[g], cut[g + 1]);
-                const ac_windows w = p.view();
+                // shard g = windows [lo, hi): a slice of the image, starts rebased
+                const size_t lo = cut[g], hi = cut[g + 1];
+                const uint64_t b0 = lo < img.size() ? img.start[lo] : img.n_bases;
+                const uint64_t b1 = hi < img.size() ? img.start[hi] : img.n_bases;
+                if (hi == lo || b1 == b0) return;  // nothing but empty windows: no k-mer occurrences
+                std::vector<uint64_t> st(hi - lo);
+                for (size_t i = lo; i < hi; ++i) st[i - lo] = img.start[i] - b0;
+                const ac_windows w{img.codes.data() + b0 / 16, img.nmask.data() + b0 / 32, st.data(),
+                                   img.length.data() + lo, (uint32_t)(hi - lo), b1 - b0};
                 if (ac_error_count(dev.ctx[g], k, kmers.data(), (uint32_t)n, &w, part[g].data()) != AC_OK)
                     err[g] = ac_last_error(dev.ctx[g]);
             } catch (const std::exception& e) {
@@ -266,6 +250,20 @@ pair_vector error_count(Devices& dev, const SeqSet& sample, const pair_vector& f
         out[i] = {kmers[i], s};
     }
     return out;
+}
+
+// --dump-sample: u64 n_windows, u64 n_bases, start[n] u64, length[n] u32,
+// codes[n_bases/16] u32, nmask[n_bases/32] u32 (little endian).
+bool write_image(const PackedImage& p, const std::string& path) {
+    std::FILE* f = std::fopen(path.c_str(), "wb");
+    if (!f) return false;
+    const uint64_t hdr[2] = {p.size(), p.n_bases};
+    bool ok = std::fwrite(hdr, sizeof hdr, 1, f) == 1;
+    ok = ok && std::fwrite(p.start.data(), sizeof(uint64_t), p.size(), f) == p.size();
+    ok = ok && std::fwrite(p.length.data(), sizeof(uint32_t), p.size(), f) == p.size();
+    ok = ok && std::fwrite(p.codes.data(), sizeof(uint32_t), p.codes.size(), f) == p.codes.size();
+    ok = ok && std::fwrite(p.nmask.data(), sizeof(uint32_t), p.nmask.size(), f) == p.nmask.size();
+    return std::fclose(f) == 0 && ok;
 }
 
 // Opens one context per shard (-g N: shard g on device g mod visible devices).
@@ -355,6 +353,8 @@ int main(int argc, char const** argv) {
     get_option(args, "seed", seed_str);
     skip_end = skip_end || args.val.count("skip_end");
     const bool host_exact = args.val.count("host-exact") > 0;
+    std::string dump_sample;
+    get_option(args, "dump-sample", dump_sample);
     const std::string input_file = args.input;
 
     kmer_set forbidden;
@@ -386,11 +386,18 @@ int main(int argc, char const** argv) {
     int tab_level = 0;
     if (v > 0 && nb_of_runs > 1) std::cout << "\nA total of " << nb_of_runs << " runs will be performed." << std::endl;
 
+    // Reads: by default only their sampling windows are kept, packed while the
+    // file is parsed (read_windows); --host-exact keeps whole reads as the
+    // reference does.  Both throw (uncaught, like SeqAn's IOError) on an
+    // unreadable file.
     std::vector<std::string> ids;
     SeqSet seqs;
+    WindowStore store;
     if (v > 0) print("Parsing FASTA file", tab_level);
-    read_records(input_file, ids, seqs);  // throws (uncaught, like SeqAn's IOError) on an unreadable file
-    if (v > 0) print("Number of sequences found: " + std::to_string(seqs.size()) + ".", tab_level);
+    if (host_exact) read_records(input_file, ids, seqs);
+    else read_windows(input_file, sl, store);
+    const uint64_t n_reads = host_exact ? seqs.size() : store.size();
+    if (v > 0) print("Number of sequences found: " + std::to_string(n_reads) + ".", tab_level);
 
     // The GPU contexts (the reference builds its index inside errorCount; the
     // device set is opened once here).
@@ -400,10 +407,10 @@ int main(int argc, char const** argv) {
     for (uint64_t run = 0; run < nb_of_runs; ++run) {
         const std::string run_suffix = "_" + std::to_string(run);
         if (nb_of_runs > 1 && v > 0) std::cout << "Starting run number " << run + 1 << std::endl;
-        if (sn > seqs.size()) {
+        if (sn > n_reads) {
             std::cerr << warning << "Sequence set too small for the requested sample size\n";
             std::cerr << warning << "The whole set will be used.\n";
-            sn = seqs.size();
+            sn = n_reads;
         }
         bool bottom = false;
         tab_level += 1;
@@ -411,12 +418,27 @@ int main(int argc, char const** argv) {
             if (v > 0) print("Working on sequence " + which_end + ".", tab_level - 1);
             if (mr_v > 0) print("Sampling", tab_level);
             if (mr_v > 0) print(bottom ? "Sampling the ends of reads" : "Sampling the start of reads", 1);
-            SeqSet sample = sample_sequences(seqs, sn, sl, bottom, rng);
-            if (mr_v > 0) print("Sampled " + std::to_string(sample.size()) + " sequences", 1);
+            SeqSet sample;
+            PackedImage img;
+            if (host_exact) {
+                sample = sample_sequences(seqs, sn, sl, bottom, rng);
+                img = pack_sample(sample, 0, sample.size());
+            } else {
+                img = sample_windows(store, sn, bottom, rng);
+            }
+            if (mr_v > 0) print("Sampled " + std::to_string(img.size()) + " sequences", 1);
+            if (!dump_sample.empty()) {
+                if (!write_image(img, dump_sample + run_suffix + "." + which_end)) {
+                    std::cerr << error_pref << "could not write " << dump_sample + run_suffix + "." + which_end << "\n";
+                    return 1;
+                }
+                if (!skip_end) bottom = true;
+                else if (mr_v > 0) break;  // the -se quirk below
+                continue;
+            }
             if (mr_v > 0) print("Exact k-mer count", tab_level);
             uint64_t had_n = 0, n_found = 0;
             pair_vector first_n;
-            Packed packed;
             ac_windows dsample{};
             if (host_exact) {  // the reference's host stages (approx_counter.cpp:874-899)
                 pair_vector count = count_kmers(sample, (uint32_t)k, lc, forbidden, &had_n);
@@ -426,8 +448,7 @@ int main(int argc, char const** argv) {
             } else {  // the same on GPU 0; the uploaded sample also serves the approximate count
                 try {
                     open_devices(dev, n_gpus);
-                    packed = pack(sample, 0, sample.size());
-                    const ac_windows hw = packed.view();
+                    const ac_windows hw = view(img);
                     if (ac_sample_upload(dev.ctx[0], &hw, &dsample) != AC_OK)
                         throw std::runtime_error(ac_last_error(dev.ctx[0]));
                     first_n = exact_count_gpu(dev.ctx[0], dsample, (uint32_t)k, lc, forbidden, limit, solid_km,
@@ -466,7 +487,7 @@ int main(int argc, char const** argv) {
                     error_counter.resize(km.size());
                     for (size_t i = 0; i < km.size(); ++i) error_counter[i] = {km[i], ct[i]};
                 } else {
-                    error_counter = error_count(dev, sample, first_n, (uint32_t)k);
+                    error_counter = error_count(dev, img, first_n, (uint32_t)k);
                 }
             } catch (const std::exception& e) {
                 std::cerr << error_pref << "approximate count failed: " << e.what() << std::endl;

@@ -66,16 +66,36 @@ struct LineReader {
     }
 };
 
-void append_bases(std::vector<uint8_t>& out, const std::string& line) {
-    for (char c : line) {
-        if (c == ' ' || c == '\t' || c == '\r') continue;  // SeqAn skips blanks inside sequence lines
-        out.push_back(dna5(c));
+// dna5() as a table; 0xff marks the blanks SeqAn skips inside sequence lines.
+struct Dna5Table {
+    uint8_t v[256];
+    Dna5Table() {
+        for (int c = 0; c < 256; ++c) v[c] = dna5((char)c);
+        v[(unsigned char)' '] = v[(unsigned char)'\t'] = v[(unsigned char)'\r'] = 0xff;
     }
+};
+const Dna5Table DNA5_TABLE;
+
+void append_bases(std::vector<uint8_t>& out, const std::string& line) {
+    const size_t n0 = out.size();
+    out.resize(n0 + line.size());
+    uint8_t* o = out.data() + n0;
+    for (char c : line) {
+        const uint8_t v = DNA5_TABLE.v[(unsigned char)c];
+        *o = v;
+        o += v != 0xff;
+    }
+    out.resize((size_t)(o - out.data()));
 }
 
 }  // namespace
 
-void read_records(const std::string& path, std::vector<std::string>& ids, SeqSet& seqs) {
+namespace {
+
+// Record loop of readRecords: FASTA or FASTQ chosen by the first record
+// marker; calls emit(id, dna5 bases, n) per record in file order.
+template <typename Emit>
+void for_each_record(const std::string& path, Emit&& emit) {
     std::FILE* f = std::fopen(path.c_str(), "rb");
     if (!f) throw std::runtime_error("Could not open input file: " + path);
     LineReader r{f};
@@ -94,8 +114,7 @@ void read_records(const std::string& path, std::vector<std::string>& ids, SeqSet
         for (;;) {
             const bool more = r.get(line);
             if (!more || (!line.empty() && line[0] == '>')) {
-                ids.push_back(id);
-                seqs.add(cur.data(), (uint32_t)cur.size());
+                emit(id, cur.data(), cur.size());
                 cur.clear();
                 if (!more) break;
                 id = line.substr(1);
@@ -131,8 +150,7 @@ void read_records(const std::string& path, std::vector<std::string>& ids, SeqSet
             // quality lines: as many characters as the sequence holds
             size_t q = 0;
             while (q < cur.size() && r.get(line)) q += line.size();
-            ids.push_back(id);
-            seqs.add(cur.data(), (uint32_t)cur.size());
+            emit(id, cur.data(), cur.size());
             if (!r.get(line)) break;
         }
     } else {
@@ -140,6 +158,101 @@ void read_records(const std::string& path, std::vector<std::string>& ids, SeqSet
         throw std::runtime_error("Unknown sequence file format (expected FASTA or FASTQ): " + path);
     }
     std::fclose(f);
+}
+
+}  // namespace
+
+void read_records(const std::string& path, std::vector<std::string>& ids, SeqSet& seqs) {
+    for_each_record(path, [&](const std::string& id, const uint8_t* b, size_t n) {
+        ids.push_back(id);
+        seqs.add(b, (uint32_t)n);
+    });
+}
+
+namespace {
+
+uint64_t round32(uint64_t n) { return (n + 31) / 32 * 32; }
+
+// Packs n Dna5 bases at image base `pos` (a multiple of 32) of codes/nmask,
+// which hold zeros there (ac_pack_windows's layout).
+void pack_into(uint32_t* codes, uint32_t* nmask, uint64_t pos, const uint8_t* src, uint64_t n) {
+    for (uint64_t j = 0; j < n; ++j) {
+        const uint64_t b = pos + j;
+        const uint8_t v = src[j];
+        if (v < 4) codes[b >> 4] |= (uint32_t)v << (2 * (b & 15));
+        else nmask[b >> 5] |= 1u << (b & 31);
+    }
+}
+
+}  // namespace
+
+void read_windows(const std::string& path, uint64_t cut, WindowStore& ws) {
+    ws = WindowStore();
+    ws.cut = cut;
+    ws.prefix_bases = round32(cut);
+    ws.suffix_bases = round32(cut + 1);
+    const uint64_t pair = ws.prefix_bases + ws.suffix_bases;
+    for_each_record(path, [&](const std::string&, const uint8_t* b, size_t n) {
+        ws.length.push_back((uint32_t)n);
+        if (n < 2 * cut) {  // never sampled (sample_sequences)
+            ws.slot.push_back(~0u);
+            return;
+        }
+        const uint64_t j = ws.n_slots++;
+        ws.slot.push_back((uint32_t)j);
+        ws.codes.resize((j + 1) * pair / 16, 0u);
+        ws.nmask.resize((j + 1) * pair / 32, 0u);
+        pack_into(ws.codes.data(), ws.nmask.data(), j * pair, b, cut);
+        if (n >= cut + 1)
+            pack_into(ws.codes.data(), ws.nmask.data(), j * pair + ws.prefix_bases, b + (n - 1 - cut), cut + 1);
+    });
+}
+
+PackedImage sample_windows(const WindowStore& ws, uint64_t nb_sample, bool bot, std::mt19937& rng) {
+    std::vector<int> vec(ws.size());
+    std::iota(vec.begin(), vec.end(), 0);
+    std::shuffle(vec.begin(), vec.end(), rng);  // the same draws as sample_sequences
+    const uint64_t pair = ws.prefix_bases + ws.suffix_bases;
+    const uint64_t wbases = bot ? ws.suffix_bases : ws.prefix_bases;
+    const uint64_t off = bot ? ws.prefix_bases : 0;
+    const uint32_t wlen = (uint32_t)(bot ? ws.cut + 1 : ws.cut);
+    std::vector<uint32_t> picked;
+    for (size_t i = 0; picked.size() < nb_sample && i < vec.size(); ++i) {
+        const size_t id = (size_t)vec[i];
+        if (ws.slot[id] != ~0u && (!bot || ws.length[id] >= ws.cut + 1)) picked.push_back(ws.slot[id]);
+    }
+    PackedImage p;
+    p.n_bases = std::max<uint64_t>(32, wbases * picked.size());
+    p.codes.assign(p.n_bases / 16, 0u);
+    p.nmask.assign(p.n_bases / 32, 0u);
+    p.start.resize(picked.size());
+    p.length.assign(picked.size(), wlen);
+    for (size_t i = 0; i < picked.size(); ++i) {
+        const uint64_t src = (uint64_t)picked[i] * pair + off, dst = (uint64_t)i * wbases;
+        p.start[i] = dst;
+        std::memcpy(&p.codes[dst / 16], &ws.codes[src / 16], wbases / 16 * sizeof(uint32_t));
+        std::memcpy(&p.nmask[dst / 32], &ws.nmask[src / 32], wbases / 32 * sizeof(uint32_t));
+    }
+    return p;
+}
+
+PackedImage pack_sample(const SeqSet& s, size_t lo, size_t hi) {
+    PackedImage p;
+    uint64_t total = 0;
+    for (size_t i = lo; i < hi; ++i) total += round32(s.length[i]);
+    p.n_bases = std::max<uint64_t>(32, total);
+    p.codes.assign(p.n_bases / 16, 0u);
+    p.nmask.assign(p.n_bases / 32, 0u);
+    p.start.resize(hi - lo);
+    p.length.resize(hi - lo);
+    uint64_t pos = 0;
+    for (size_t i = lo; i < hi; ++i) {
+        p.start[i - lo] = pos;
+        p.length[i - lo] = s.length[i];
+        pack_into(p.codes.data(), p.nmask.data(), pos, s.seq(i), s.length[i]);
+        pos += round32(s.length[i]);
+    }
+    return p;
 }
 
 uint64_t dna2int(const uint8_t* s, uint32_t k) {
@@ -195,7 +308,7 @@ SeqSet sample_sequences(const SeqSet& seqs, uint64_t nb_sample, uint64_t cut, bo
         const size_t id = (size_t)vec[i];
         const uint64_t len = seqs.length[id];
         const uint64_t cur_cut = std::min<uint64_t>(len, cut);
-        if (len >= cut * 2) {
+        if (len >= cut * 2 && (!bot || len >= cur_cut + 1)) {  // (an empty read has no end window at cut 0)
             if (bot) {
                 const uint64_t from = len - 1 - cur_cut;  // suffix(seq, len - 1 - cut): cut + 1 bases
                 sample.add(seqs.seq(id) + from, (uint32_t)(len - from));

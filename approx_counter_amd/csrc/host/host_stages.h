@@ -61,6 +61,39 @@ struct CompareCount {
     uint32_t k;
 };
 
+// A window image in the C ABI's layout (ac_windows, include/approx_counter_amd.h):
+// 2-bit codes + N bitmap, every window starting at a multiple of 32 bases.
+struct PackedImage {
+    std::vector<uint32_t> codes, nmask, length;
+    std::vector<uint64_t> start;
+    uint64_t n_bases = 32;
+    size_t size() const { return length.size(); }
+};
+
+// ac_pack_windows over sequences [lo, hi) of a SeqSet.
+PackedImage pack_sample(const SeqSet& s, size_t lo, size_t hi);
+
+// The reads of a FASTA/FASTQ file kept as their sampling windows only
+// (the reader packs on the fly, so no 1 B/base copy of
+// the whole file is held).  For every record: its length; for every record
+// sample_sequences could pick (length >= 2 cut), its first `cut` bases and its
+// last cut + 1 bases, packed at 32-base-aligned offsets.
+struct WindowStore {
+    uint64_t cut = 0;
+    uint64_t prefix_bases = 0, suffix_bases = 32;  // round-ups to 32 of cut and cut + 1
+    uint64_t n_slots = 0;
+    std::vector<uint32_t> length;        // every record, file order
+    std::vector<uint32_t> slot;          // record -> stored window pair, ~0u if never sampled
+    std::vector<uint32_t> codes, nmask;  // window pairs: prefix then suffix
+    size_t size() const { return length.size(); }
+};
+void read_windows(const std::string& path, uint64_t cut, WindowStore& out);
+
+// sample_sequences + pack_sample over a WindowStore built with the same cut:
+// the same shuffle draws and picks, written straight into a window image
+// (identical to pack_sample(sample_sequences(...)) word for word).
+PackedImage sample_windows(const WindowStore& ws, uint64_t nb_sample, bool bot, std::mt19937& rng);
+
 // sampleSequences (approx_counter.cpp:415-476): walks a shuffled permutation
 // of the reads and keeps, for up to nb_sample reads of length >= 2*cut, the
 // first `cut` bases (start) or the last cut+1 bases (end, `bot`).
