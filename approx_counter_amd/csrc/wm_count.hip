@@ -72,8 +72,12 @@ __device__ __forceinline__ void stamp(uint64_t wave, int i) {
         }
     }
 }
+__device__ __forceinline__ void stamp_val(uint64_t wave, int i, uint64_t v) {
+    if ((threadIdx.x & 63u) == 0 && wave < (1u << 18)) g_stamps[wave * 8 + i] = v;
+}
 #else
 __device__ __forceinline__ void stamp(uint64_t, int) {}
+__device__ __forceinline__ void stamp_val(uint64_t, int, uint64_t) {}
 #endif
 constexpr int W = AC_WAVE_WORDS;
 constexpr uint32_t SEG = 256;  // window bases staged in LDS per pass (4 per lane)
@@ -316,17 +320,32 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, Stage& st) {
         if (lane == 0) v = __hip_atomic_fetch_add(counter(jc), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return v;
     };
-    auto steal = [&]() -> uint32_t {  // next item from a sibling sub-queue, or n_items
-        for (uint32_t t = 1; t < S; ++t) {
-            const uint32_t jj = (j + t) % S;
-            uint32_t v = 0;
-            if (lane == 0) v = __hip_atomic_load(counter(jj), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (waves_in(jj) + __builtin_amdgcn_readfirstlane(v) >= n_in(jj)) continue;
+    // Next item from a sibling sub-queue, or n_items.  One wave-wide probe
+    // reads up to 63 sibling counters at once (a sequential probe costs one
+    // ~2 µs device-scope round trip per sibling, which used to stretch the
+    // launch tail); the wave then claims from the first sibling that still had
+    // items.  A failed claim means that sibling is dry for good (counters only
+    // grow), so the loop ends after at most S - 1 failed claims, and a wave
+    // exits only once every sub-queue of its group has been seen dry.
+    auto steal = [&]() -> uint32_t {
+        for (;;) {
+            uint32_t found = S;
+            for (uint32_t b = 1; b < S && found == S; b += 63u) {  // siblings j+b .. j+b+62
+                bool have = false;
+                if (lane < 63u && b + lane < S) {
+                    const uint32_t jj = (j + b + lane) % S;
+                    const uint32_t v = __hip_atomic_load(counter(jj), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    have = waves_in(jj) + v < n_in(jj);
+                }
+                const uint64_t mk = __ballot(have);
+                if (mk) found = b + (uint32_t)__builtin_ctzll(mk);
+            }
+            if (found == S) return n_items;
+            const uint32_t jj = (j + found) % S;
             jc = jj;
             const uint32_t c = waves_in(jj) + __builtin_amdgcn_readfirstlane(dequeue_issue());
             if (c < n_in(jj)) return jj + c * S;
         }
-        return n_items;
     };
     uint32_t item = j < n_items ? item_of(rank) : n_items;
     uint32_t pending = 0;
@@ -436,6 +455,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, Stage& st) {
     }
 
     stamp(wave, 2);
+    stamp_val(wave, 6, ((uint64_t)si << 32) | ((uint64_t)g << 16) | j);
 #pragma unroll
     for (int x = 0; x < W; ++x)
 #pragma unroll

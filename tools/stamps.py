@@ -52,6 +52,12 @@ def main():
     print("main len     ", pct(us[:, 2] - us[:, 1]))
     print("atomics len  ", pct(us[:, 3] - us[:, 2]))
     print("end          ", pct(us[:, 3]))
+    # per candidate group: end times (a group's waves only steal within the group)
+    grp = raw[:, 6] >> 16
+    print("per group (seg<<16|g): waves, end p0/p50/p100 us")
+    for gv in np.unique(grp):
+        e = us[grp == gv, 3]
+        print(f"  {int(gv):#8x} {e.size:5d}  {e.min():7.1f} {np.median(e):7.1f} {e.max():7.1f}")
     # per-SIMD view: HW_ID (gfx9 layout) wave[3:0] simd[5:4] cu[11:8] sh[12] se[15:13]; + XCC id
     hw, xcc = raw[:, 4], raw[:, 5]
     simd_key = xcc * 100000 + ((hw >> 13) & 7) * 10000 + ((hw >> 12) & 1) * 1000 + ((hw >> 8) & 15) * 10 + ((hw >> 4) & 3)
