@@ -84,8 +84,8 @@ constexpr uint32_t SEG = 256;  // window bases staged in LDS per pass (4 per lan
 
 // Per-wave LDS staging of one window segment (3 KB).
 struct Stage {
-    uint4 hl[SEG / 2];  // (H, L) of bases 2q and 2q+1
-    uint32_t n[SEG];    // N mask of each base (0 or ~0)
+    uint4 hl[SEG / 2 + 1];  // (H, L) of bases 2q and 2q+1; one pad pair for the read-ahead past the end
+    uint32_t n[SEG];        // N mask of each base (0 or ~0)
 };
 
 // v_bitop3_b32 truth tables over (s0, s1, s2) = (0xf0, 0xcc, 0xaa).
@@ -142,7 +142,7 @@ __device__ __forceinline__ void run(Nfa& s, const uint32_t (&ph)[W], const uint3
     uint4 cur = st.hl[q];
 #pragma unroll
     for (int j = 0; j < NB; j += 2) {
-        const uint4 nxt = st.hl[min(q + j / 2 + 1, SEG / 2 - 1)];
+        const uint4 nxt = st.hl[q + j / 2 + 1];  // base + immediate offset (the pad pair absorbs the last read)
         uint32_t n0 = 0, n1 = 0;
         if constexpr (HAS_N) {
             n0 = st.n[2 * (q + j / 2)];
