@@ -3,10 +3,17 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <numeric>
 #include <stdexcept>
+#include <thread>
+
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 namespace achost {
 
@@ -92,23 +99,41 @@ void append_bases(std::vector<uint8_t>& out, const std::string& line) {
 
 namespace {
 
-// Record loop of readRecords: FASTA or FASTQ chosen by the first record
-// marker; calls emit(id, dna5 bases, n) per record in file order.
-template <typename Emit>
-void for_each_record(const std::string& path, Emit&& emit) {
-    std::FILE* f = std::fopen(path.c_str(), "rb");
-    if (!f) throw std::runtime_error("Could not open input file: " + path);
-    LineReader r{f};
-    std::string line;
+constexpr uint64_t NO_STOP = ~0ull;
+
+// Line source over a memory range [base + begin, base + end) (an mmap'd file):
+// the same lines as LineReader, plus the file offset of the last line read.
+struct MemLines {
+    const char* base;
+    const char* p;
+    const char* end;
+    uint64_t start = 0;  // offset of the last line returned
+    bool get(std::string& line) {
+        if (p >= end) return false;
+        start = (uint64_t)(p - base);
+        const char* nl = static_cast<const char*>(std::memchr(p, '\n', (size_t)(end - p)));
+        const char* e = nl ? nl : end;
+        line.assign(p, (size_t)(e - p));
+        if (!line.empty() && line.back() == '\r') line.pop_back();
+        p = nl ? nl + 1 : end;
+        return true;
+    }
+    uint64_t last_start() const { return start; }
+};
+
+struct FileLines {  // non-mappable inputs (pipes): offsets are not tracked
+    LineReader r;
+    bool get(std::string& line) { return r.get(line); }
+    uint64_t last_start() const { return 0; }
+};
+
+// Record loop of readRecords from `line`, a record-start line just read: FASTA
+// ('>') or FASTQ ('@'); calls emit(id, dna5 bases, n) per record in order.
+// Stops before the first record whose start line lies at offset >= stop and
+// returns that offset (NO_STOP at the end of the input).
+template <typename Lines, typename Emit>
+uint64_t parse_records(Lines& r, std::string& line, Emit&& emit, uint64_t stop, const std::string& path) {
     std::vector<uint8_t> cur;
-    // Skip leading empty lines, find the format from the first record marker.
-    bool have = false;
-    while ((have = r.get(line)) && line.empty()) {
-    }
-    if (!have) {
-        std::fclose(f);
-        return;  // empty file: no records
-    }
     if (line[0] == '>') {
         std::string id = line.substr(1);
         for (;;) {
@@ -116,48 +141,117 @@ void for_each_record(const std::string& path, Emit&& emit) {
             if (!more || (!line.empty() && line[0] == '>')) {
                 emit(id, cur.data(), cur.size());
                 cur.clear();
-                if (!more) break;
+                if (!more) return NO_STOP;
+                if (r.last_start() >= stop) return r.last_start();
                 id = line.substr(1);
                 continue;
             }
             append_bases(cur, line);
         }
-    } else if (line[0] == '@') {
-        for (;;) {
-            if (line.empty()) {
-                if (!r.get(line)) break;
-                continue;
-            }
-            if (line[0] != '@') {
-                std::fclose(f);
-                throw std::runtime_error("Malformed FASTQ record in " + path);
-            }
-            const std::string id = line.substr(1);
-            cur.clear();
-            // sequence lines until the '+' separator
-            bool ok = false;
-            while (r.get(line)) {
-                if (!line.empty() && line[0] == '+') {
-                    ok = true;
-                    break;
-                }
-                append_bases(cur, line);
-            }
-            if (!ok) {
-                std::fclose(f);
-                throw std::runtime_error("Truncated FASTQ record in " + path);
-            }
-            // quality lines: as many characters as the sequence holds
-            size_t q = 0;
-            while (q < cur.size() && r.get(line)) q += line.size();
-            emit(id, cur.data(), cur.size());
-            if (!r.get(line)) break;
+    }
+    if (line[0] != '@') throw std::runtime_error("Unknown sequence file format (expected FASTA or FASTQ): " + path);
+    for (;;) {
+        if (line.empty()) {
+            if (!r.get(line)) return NO_STOP;
+            continue;
         }
-    } else {
+        if (r.last_start() >= stop) return r.last_start();
+        if (line[0] != '@') throw std::runtime_error("Malformed FASTQ record in " + path);
+        const std::string id = line.substr(1);
+        cur.clear();
+        // sequence lines until the '+' separator
+        bool ok = false;
+        while (r.get(line)) {
+            if (!line.empty() && line[0] == '+') {
+                ok = true;
+                break;
+            }
+            append_bases(cur, line);
+        }
+        if (!ok) throw std::runtime_error("Truncated FASTQ record in " + path);
+        // quality lines: as many characters as the sequence holds
+        size_t q = 0;
+        while (q < cur.size() && r.get(line)) q += line.size();
+        emit(id, cur.data(), cur.size());
+        if (!r.get(line)) return NO_STOP;
+    }
+}
+
+// First record-start line of a source: leading empty lines skipped.  False for an empty input.
+template <typename Lines>
+bool first_record_line(Lines& r, std::string& line) {
+    bool have = false;
+    while ((have = r.get(line)) && line.empty()) {
+    }
+    return have;
+}
+
+// Read-only mapping of a regular file (empty or unmappable: data == nullptr).
+struct Mapped {
+    const char* data = nullptr;
+    size_t size = 0;
+    int fd = -1;
+    explicit Mapped(const std::string& path) {
+        fd = ::open(path.c_str(), O_RDONLY);
+        if (fd < 0) return;
+        struct stat st;
+        if (::fstat(fd, &st) != 0 || !S_ISREG(st.st_mode) || st.st_size == 0) return;
+        void* m = ::mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_PRIVATE, fd, 0);
+        if (m == MAP_FAILED) return;
+        data = static_cast<const char*>(m);
+        size = (size_t)st.st_size;
+    }
+    ~Mapped() {
+        if (data) ::munmap(const_cast<char*>(data), size);
+        if (fd >= 0) ::close(fd);
+    }
+    Mapped(const Mapped&) = delete;
+    Mapped& operator=(const Mapped&) = delete;
+};
+
+// Sequential parse with buffered reads (faster than faulting in a mapping
+// page by page on one thread; also reads pipes).
+template <typename Emit>
+void for_each_record(const std::string& path, Emit&& emit) {
+    std::string line;
+    std::FILE* f = std::fopen(path.c_str(), "rb");
+    if (!f) throw std::runtime_error("Could not open input file: " + path);
+    FileLines r{LineReader{f}};
+    try {
+        if (first_record_line(r, line)) parse_records(r, line, emit, NO_STOP, path);
+    } catch (...) {
         std::fclose(f);
-        throw std::runtime_error("Unknown sequence file format (expected FASTA or FASTQ): " + path);
+        throw;
     }
     std::fclose(f);
+}
+
+// Offset of the first plausible record start at or after `from`: a line
+// starting with '>' (FASTA) or, for FASTQ, a line starting with '@' whose
+// next-but-one line starts with '+' and whose sequence and quality lines have
+// equal lengths.  A wrong guess (a quality line starting with '@') is caught
+// by the boundary check of read_windows.  Returns size if there is none.
+size_t next_record_start(const char* d, size_t size, size_t from, char marker) {
+    size_t p = from;
+    if (p > 0) {  // move to the start of the next line
+        const char* nl = static_cast<const char*>(std::memchr(d + p - 1, '\n', size - (p - 1)));
+        if (!nl) return size;
+        p = (size_t)(nl + 1 - d);
+    }
+    while (p < size) {
+        if (d[p] == marker) {
+            if (marker == '>') return p;
+            MemLines r{d, d + p, d + size};
+            std::string l0, l1, l2, l3;
+            if (r.get(l0) && r.get(l1) && r.get(l2) && r.get(l3) && !l2.empty() && l2[0] == '+' &&
+                l1.size() == l3.size())
+                return p;
+        }
+        const char* nl = static_cast<const char*>(std::memchr(d + p, '\n', size - p));
+        if (!nl) return size;
+        p = (size_t)(nl + 1 - d);
+    }
+    return size;
 }
 
 }  // namespace
@@ -186,13 +280,13 @@ void pack_into(uint32_t* codes, uint32_t* nmask, uint64_t pos, const uint8_t* sr
 
 }  // namespace
 
-void read_windows(const std::string& path, uint64_t cut, WindowStore& ws) {
-    ws = WindowStore();
-    ws.cut = cut;
-    ws.prefix_bases = round32(cut);
-    ws.suffix_bases = round32(cut + 1);
-    const uint64_t pair = ws.prefix_bases + ws.suffix_bases;
-    for_each_record(path, [&](const std::string&, const uint8_t* b, size_t n) {
+namespace {
+
+// Keeps a record's length and, if sample_sequences could pick it, its packed windows.
+struct WindowPacker {
+    WindowStore& ws;
+    void operator()(const std::string&, const uint8_t* b, size_t n) {
+        const uint64_t cut = ws.cut, pair = ws.prefix_bases + ws.suffix_bases;
         ws.length.push_back((uint32_t)n);
         if (n < 2 * cut) {  // never sampled (sample_sequences)
             ws.slot.push_back(~0u);
@@ -205,7 +299,101 @@ void read_windows(const std::string& path, uint64_t cut, WindowStore& ws) {
         pack_into(ws.codes.data(), ws.nmask.data(), j * pair, b, cut);
         if (n >= cut + 1)
             pack_into(ws.codes.data(), ws.nmask.data(), j * pair + ws.prefix_bases, b + (n - 1 - cut), cut + 1);
-    });
+    }
+};
+
+WindowStore empty_store(uint64_t cut) {
+    WindowStore ws;
+    ws.cut = cut;
+    ws.prefix_bases = round32(cut);
+    ws.suffix_bases = round32(cut + 1);
+    return ws;
+}
+
+// Chunked parse of a mapped file: chunk t starts at a plausible record start
+// A_t and stops before the first record starting at or after A_{t+1}.  The
+// result is taken only if every chunk stopped exactly at the next chunk's start
+// (then, by induction from the file start, every A_t is a true record boundary
+// of the sequential parse and the fragments are its pieces); false otherwise.
+bool read_windows_chunked(const Mapped& m, const std::string& path, uint64_t cut, unsigned threads,
+                          WindowStore& ws) {
+    const char* d = m.data;
+    MemLines head{d, d, d + m.size};
+    std::string line;
+    if (!first_record_line(head, line) || (line[0] != '>' && line[0] != '@')) return false;
+    const char marker = line[0];
+    std::vector<size_t> at{(size_t)head.last_start()};
+    for (unsigned t = 1; t < threads; ++t) {
+        const size_t a = next_record_start(d, m.size, std::max(m.size / threads * t, at.back() + 1), marker);
+        if (a >= m.size) break;
+        at.push_back(a);
+    }
+    const size_t n = at.size();
+    std::vector<WindowStore> part(n, empty_store(cut));
+    std::vector<uint64_t> stopped(n, NO_STOP);
+    std::vector<char> ok(n, 1);
+    std::vector<std::thread> pool;
+    for (size_t t = 0; t < n; ++t)
+        pool.emplace_back([&, t] {
+            try {
+                MemLines r{d, d + at[t], d + m.size};
+                std::string l;
+                if (!r.get(l)) return;
+                WindowPacker pk{part[t]};
+                stopped[t] = parse_records(r, l, pk, t + 1 < n ? (uint64_t)at[t + 1] : NO_STOP, path);
+            } catch (...) {
+                ok[t] = 0;
+            }
+        });
+    for (auto& th : pool) th.join();
+    for (size_t t = 0; t < n; ++t)
+        if (!ok[t] || stopped[t] != (t + 1 < n ? (uint64_t)at[t + 1] : NO_STOP)) return false;
+    ws = empty_store(cut);
+    size_t recs = 0, words = 0, masks = 0;
+    for (const auto& f : part) {
+        recs += f.size();
+        words += f.codes.size();
+        masks += f.nmask.size();
+    }
+    ws.length.reserve(recs);
+    ws.slot.reserve(recs);
+    ws.codes.reserve(words);
+    ws.nmask.reserve(masks);
+    for (const auto& f : part) {
+        ws.length.insert(ws.length.end(), f.length.begin(), f.length.end());
+        for (uint32_t sl : f.slot) ws.slot.push_back(sl == ~0u ? ~0u : sl + (uint32_t)ws.n_slots);
+        ws.codes.insert(ws.codes.end(), f.codes.begin(), f.codes.end());
+        ws.nmask.insert(ws.nmask.end(), f.nmask.begin(), f.nmask.end());
+        ws.n_slots += f.n_slots;
+    }
+    return true;
+}
+
+}  // namespace
+
+void read_windows(const std::string& path, uint64_t cut, WindowStore& ws, unsigned threads) {
+    if (threads == 0) {
+        const char* env = std::getenv("AC_READ_THREADS");  // override, e.g. 1 for the sequential reader
+        threads = env ? (unsigned)std::strtoul(env, nullptr, 10)
+                      : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    }
+    {
+        Mapped m(path);
+        // below ~8 MB per thread the threads cost more than they save (AC_READ_MIN_CHUNK overrides, for tests)
+        const char* mc = std::getenv("AC_READ_MIN_CHUNK");
+        const size_t min_chunk = std::max<size_t>(1, mc ? (size_t)std::strtoull(mc, nullptr, 10) : (8u << 20));
+        const unsigned t = (unsigned)std::min<size_t>(threads, m.size / min_chunk);
+        const bool debug = std::getenv("AC_READ_DEBUG") != nullptr;
+        if (m.data && t > 1) {
+            if (read_windows_chunked(m, path, cut, t, ws)) {
+                if (debug) std::fprintf(stderr, "[reader] chunked parse, %u threads\n", t);
+                return;
+            }
+            if (debug) std::fprintf(stderr, "[reader] chunk boundaries not confirmed: sequential parse\n");
+        }
+    }
+    ws = empty_store(cut);
+    for_each_record(path, WindowPacker{ws});
 }
 
 PackedImage sample_windows(const WindowStore& ws, uint64_t nb_sample, bool bot, std::mt19937& rng) {

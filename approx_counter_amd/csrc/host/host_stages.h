@@ -87,7 +87,10 @@ struct WindowStore {
     std::vector<uint32_t> codes, nmask;  // window pairs: prefix then suffix
     size_t size() const { return length.size(); }
 };
-void read_windows(const std::string& path, uint64_t cut, WindowStore& out);
+// `threads` (0 = up to 16 hardware threads) parse large regular files in
+// chunks; the result is identical to the sequential parse, which is used
+// whenever the chunk boundaries cannot be confirmed.
+void read_windows(const std::string& path, uint64_t cut, WindowStore& out, unsigned threads = 0);
 
 // sample_sequences + pack_sample over a WindowStore built with the same cut:
 // the same shuffle draws and picks, written straight into a window image

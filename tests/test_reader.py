@@ -125,3 +125,64 @@ def test_empty_and_unreadable_input(tmp_path):
         assert len(start) == 0 and len(codes) == 2 and len(nmask) == 1
     r = subprocess.run([CLI, str(tmp_path / "missing.fa"), "--dump-sample", "x"], capture_output=True, timeout=60)
     assert r.returncode == -6  # uncaught like SeqAn's IOError (test_cli.py)
+
+
+def chunked_env(threads, min_chunk=2048):
+    env = dict(os.environ)
+    env.update(AC_READ_THREADS=str(threads), AC_READ_MIN_CHUNK=str(min_chunk), AC_READ_DEBUG="1")
+    return env
+
+
+def dump_env(tmp_path, inp, tag, extra, env):
+    r = subprocess.run([CLI, str(inp), "--dump-sample", str(tmp_path / tag), "-v", "0"] + [str(a) for a in extra],
+                       cwd=tmp_path, capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, r.stderr
+    if env.get("AC_READ_THREADS", "1") != "1":
+        assert "[reader] chunked parse" in r.stderr, r.stderr
+    return sorted(p for p in os.listdir(tmp_path) if p.startswith(tag + "_"))
+
+
+@pytest.mark.parametrize("fmt,width,crlf,at_quality", [("fa", 0, False, False), ("fa", 61, True, False),
+                                                        ("fq", 0, False, False), ("fq", 0, True, True)])
+def test_chunked_reader_equals_sequential(tmp_path, fmt, width, crlf, at_quality):
+    """read_windows with several threads parses chunks that start at guessed
+    record boundaries; the result must be the sequential parse's, including
+    FASTQ whose quality lines start with '@' (false boundary candidates)."""
+    sl = 30
+    seqs = rand_reads(zlib.crc32(f"chunk{fmt}{width}{crlf}{at_quality}".encode()), 1500, sl)
+    inp = tmp_path / f"reads.{fmt}"
+    if fmt == "fq" and at_quality:
+        nl = "\r\n" if crlf else "\n"
+        with open(inp, "w", newline="") as fh:
+            for i, s in enumerate(seqs):
+                q = ("@" + "I" * (len(s) - 1)) if s and i % 3 else "I" * len(s)
+                fh.write(f"@r{i}{nl}{s}{nl}+{nl}{q}{nl}")
+    else:
+        write_reads(inp, seqs, fmt, width, crlf)
+    args = ["-sl", sl, "-k", 8, "-sn", 10**6, "--seed", 4]
+    seq = dump_env(tmp_path, inp, "seq", args, chunked_env(1))
+    for t in (2, 7, 16):
+        par = dump_env(tmp_path, inp, f"par{t}", args, chunked_env(t))
+        assert len(par) == len(seq) == 2
+        for a, b in zip(par, seq):
+            assert open(tmp_path / a, "rb").read() == open(tmp_path / b, "rb").read(), (t, a)
+
+
+def test_chunked_reader_falls_back_on_a_false_boundary(tmp_path):
+    """Quality lines "@x" followed by an empty-sequence record look like record
+    starts to the boundary guess ('+' two lines below, equal lengths); a chunk
+    that starts there misparses and the sequential parse is used instead."""
+    # 40-byte units after a 36-byte first record: 4 of the 7 chunk starts of an 8-way split land on "@x" lines
+    recs = "@pp\n" + "A" * 14 + "\n+\n" + "I" * 14 + "\n"
+    recs += "".join(f"@r{i:04d}\nACGTACGTAC\n+\n@xxxxxxxxx\n@s{i:04d}\n+\n" for i in range(3000))
+    (tmp_path / "tricky.fq").write_text(recs)
+    args = ["-sl", 4, "-k", 4, "-sn", 10**6, "--seed", 2]
+    r = subprocess.run([CLI, str(tmp_path / "tricky.fq"), "--dump-sample", str(tmp_path / "par"), "-v", "0"] +
+                       [str(a) for a in args], cwd=tmp_path, capture_output=True, text=True, timeout=60,
+                       env=chunked_env(8, min_chunk=512))
+    assert r.returncode == 0, r.stderr
+    assert "not confirmed" in r.stderr, r.stderr
+    seq = dump_env(tmp_path, tmp_path / "tricky.fq", "seq", args, chunked_env(1))
+    assert len(seq) == 2
+    for e in ("start", "end"):
+        assert open(tmp_path / f"par_0.{e}", "rb").read() == open(tmp_path / f"seq_0.{e}", "rb").read()
