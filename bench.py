@@ -145,9 +145,10 @@ def main():
     n_c = [int(wl[e]["kmers"].size) for e in ends]
     counts = torch.zeros(sum(n_c), dtype=torch.int32, device=dev)
     segs = []
+    packed = {e: ac.pack_windows(wl[e]["windows"]) for e in ends}
     off = 0
     for e, n in zip(ends, n_c):
-        seg = ac.DeviceSegment.upload(wl[e]["kmers"], ac.pack_windows(wl[e]["windows"]), device=dev)
+        seg = ac.DeviceSegment.upload(wl[e]["kmers"], packed[e], device=dev)
         seg.counts = counts[off:off + n]
         off += n
         segs.append(seg)
@@ -240,6 +241,21 @@ def main():
                              "frac": sample_bytes / (kern_ms * 1e-3) / HBM_PEAK,
                              "algorithmic_bytes_per_launch": sample_bytes},
         }
+        if world == 1:
+            # The drop-in entry point hands over host buffers (ac_error_count: H2D of the packed
+            # sample and candidates, the kernel, D2H of the counts), one call per read end.  Reported
+            # beside `value`, never as it.
+            reps = max(5, args.steps // 5)
+            for e in ends:
+                counter.count(args.k, wl[e]["kmers"], packed[e])
+            t_h = time.perf_counter()
+            for _ in range(reps):
+                for e in ends:
+                    counter.count(args.k, wl[e]["kmers"], packed[e])
+            host_s = (time.perf_counter() - t_h) / reps
+            out["host_boundary"] = {"value": units / host_s, "unit": "kmer*bp/s", "ms_per_step": host_s * 1e3,
+                                    "note": "ac_error_count with host buffers (PCIe-inclusive: H2D of the 2-bit "
+                                            "sample + candidates, kernel, D2H of counts), both ends, synchronous"}
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(wl, args.k, args.cpu_seconds)
         print(json.dumps(out), flush=True)
