@@ -90,6 +90,11 @@ def load():
         fn.restype = ctypes.c_int
     L.ac_error_count_sample.argtypes = [vp, ctypes.c_uint32, p64, ctypes.c_uint32, ctypes.POINTER(ACWindows), p64]
     L.ac_error_count_sample.restype = ctypes.c_int
+    L.ac_create_multi.argtypes = [ctypes.POINTER(vp), ctypes.c_int]
+    L.ac_create_multi.restype = ctypes.c_int
+    L.ac_count.argtypes = [vp, ctypes.c_uint32, p64, ctypes.c_uint32, p32, p32, p64,
+                           ctypes.POINTER(ctypes.c_uint16), ctypes.c_uint32, p64]
+    L.ac_count.restype = ctypes.c_int
     _lib = L
     return L
 

@@ -94,13 +94,17 @@ def pack_windows(windows) -> PackedSample:
 
 
 class ApproxCounter:
-    """One device context (ac_create / ac_destroy)."""
+    """One device context (ac_create / ac_destroy), or with n_gpus a context
+    whose host-buffer counts are sharded over that many devices (ac_create_multi)."""
 
-    def __init__(self, device: int = -1):
+    def __init__(self, device: int = -1, n_gpus: int = 0):
         L = _lib.load()
         self._L = L
         h = ctypes.c_void_p()
-        check(L.ac_create(ctypes.byref(h), device))
+        if n_gpus:
+            check(L.ac_create_multi(ctypes.byref(h), int(n_gpus)))
+        else:
+            check(L.ac_create(ctypes.byref(h), device))
         self._h = h
 
     def close(self) -> None:
@@ -129,6 +133,22 @@ class ApproxCounter:
         st = self._L.ac_error_count(self._h, int(k),
                                     _ptr(kmers if kmers.size else np.zeros(1, np.uint64), ctypes.c_uint64),
                                     int(kmers.size), ctypes.byref(ws), _ptr(counts, ctypes.c_uint64))
+        check(st, self._h)
+        return counts[: kmers.size]
+
+    def count_words(self, k: int, kmers, win_bits, win_nmask, win_word_offset, win_len) -> np.ndarray:
+        """ac_count (SURVEY.md 8(b) layout): 2-bit words, N bitmap, per-window word offset
+        (even) and uint16 length."""
+        kmers = np.ascontiguousarray(np.asarray(kmers, dtype=np.uint64))
+        bits = np.ascontiguousarray(win_bits, dtype=np.uint32)
+        nm = np.ascontiguousarray(win_nmask, dtype=np.uint32)
+        off = np.ascontiguousarray(win_word_offset, dtype=np.uint64)
+        ln = np.ascontiguousarray(win_len, dtype=np.uint16)
+        counts = np.zeros(max(kmers.size, 1), dtype=np.uint64)
+        one = lambda a, t: _ptr(a if a.size else np.zeros(1, a.dtype), t)  # noqa: E731
+        st = self._L.ac_count(self._h, int(k), one(kmers, ctypes.c_uint64), int(kmers.size), one(bits, ctypes.c_uint32),
+                              one(nm, ctypes.c_uint32), one(off, ctypes.c_uint64), one(ln, ctypes.c_uint16),
+                              int(ln.size), _ptr(counts, ctypes.c_uint64))
         check(st, self._h)
         return counts[: kmers.size]
 

@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "approx_counter_amd.h"
@@ -41,6 +42,8 @@ struct ac_ctx {
     // last launch geometry
     uint64_t last_waves = 0;
     uint32_t last_wpw = 0, last_groups = 0;
+    // ac_create_multi: contexts of shards 1..n-1 (this context is shard 0)
+    std::vector<ac_ctx*> peers;
 };
 
 namespace {
@@ -247,6 +250,7 @@ ac_status ac_create(ac_ctx** out, int device) {
 
 void ac_destroy(ac_ctx* ctx) {
     if (!ctx) return;
+    for (ac_ctx* p : ctx->peers) ac_destroy(p);
     (void)hipSetDevice(ctx->device);
     for (void* p : ctx->d_buf)
         if (p) (void)hipFree(p);
@@ -273,8 +277,12 @@ ac_status ac_error_count_device_accumulate(ac_ctx* ctx, uint32_t k, const ac_seg
     return launch(ctx, k, segments, n_segments, (hipStream_t)hip_stream, false);
 }
 
-ac_status ac_error_count(ac_ctx* ctx, uint32_t k, const uint64_t* kmers, uint32_t n_kmers,
-                         const ac_windows* sample, uint64_t* counts) {
+}  // extern "C"
+
+namespace {
+
+ac_status error_count_one(ac_ctx* ctx, uint32_t k, const uint64_t* kmers, uint32_t n_kmers,
+                          const ac_windows* sample, uint64_t* counts) {
     if (!ctx) return fail(nullptr, AC_ERR_INVALID, "ctx is NULL");
     if (ac_status st = check_k(ctx, k)) return st;
     if (n_kmers == 0) return AC_OK;
@@ -318,6 +326,109 @@ ac_status ac_error_count(ac_ctx* ctx, uint32_t k, const uint64_t* kmers, uint32_
     AC_HIP(ctx, hipStreamSynchronize(st));
     for (uint32_t i = 0; i < n_kmers; ++i) counts[i] = ctx->h_counts[i];
     return AC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+ac_status ac_error_count(ac_ctx* ctx, uint32_t k, const uint64_t* kmers, uint32_t n_kmers,
+                         const ac_windows* sample, uint64_t* counts) {
+    if (!ctx || ctx->peers.empty()) return error_count_one(ctx, k, kmers, n_kmers, sample, counts);
+    if (ac_status st = check_k(ctx, k)) return st;
+    if (n_kmers == 0) return AC_OK;
+    if (!kmers || !counts || !sample) return fail(ctx, AC_ERR_INVALID, "NULL argument");
+    if (ac_status st = check_sample(ctx, sample)) return st;
+    const ac_windows& s = *sample;
+    for (uint32_t i = 0; i < s.n_windows; ++i)
+        if (s.start[i] % 32 || s.start[i] + s.length[i] > s.n_bases)
+            return fail(ctx, AC_ERR_INVALID, "window " + std::to_string(i) + " is misaligned or outside the image");
+    // Shards: contiguous window ranges balanced by bases; shard g is a slice of
+    // the image (codes/nmask from its first window's start), starts rebased.
+    const size_t G = ctx->peers.size() + 1;
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < s.n_windows; ++i) total += s.length[i];
+    std::vector<uint32_t> cut(G + 1, s.n_windows);
+    cut[0] = 0;
+    {
+        uint64_t acc = 0;
+        size_t g = 1;
+        for (uint32_t i = 0; i < s.n_windows && g < G; ++i) {
+            acc += s.length[i];
+            while (g < G && acc * G >= total * g) cut[g++] = i + 1;
+        }
+    }
+    std::vector<std::vector<uint64_t>> part(G, std::vector<uint64_t>(n_kmers, 0));
+    std::vector<ac_status> rc(G, AC_OK);
+    auto run = [&](size_t g) {
+        ac_ctx* c = g == 0 ? ctx : ctx->peers[g - 1];
+        const uint32_t lo = cut[g], hi = cut[g + 1];
+        if (hi == lo) return;
+        const uint64_t b0 = s.start[lo];
+        uint64_t b1 = b0;
+        for (uint32_t i = lo; i < hi; ++i) b1 = std::max<uint64_t>(b1, s.start[i] + s.length[i]);
+        b1 = (b1 + 31) / 32 * 32;
+        if (b1 == b0) return;  // only empty windows: no occurrences
+        std::vector<uint64_t> st(hi - lo);
+        for (uint32_t i = lo; i < hi; ++i) st[i - lo] = s.start[i] - b0;
+        const ac_windows w{s.codes + b0 / 16, s.nmask + b0 / 32, st.data(), s.length + lo, hi - lo, b1 - b0};
+        rc[g] = error_count_one(c, k, kmers, n_kmers, &w, part[g].data());
+    };
+    std::vector<std::thread> th;
+    for (size_t g = 1; g < G; ++g) th.emplace_back(run, g);
+    run(0);
+    for (auto& t : th) t.join();
+    for (size_t g = 0; g < G; ++g)
+        if (rc[g] != AC_OK) {
+            ac_ctx* c = g == 0 ? ctx : ctx->peers[g - 1];
+            return fail(ctx, rc[g], "shard " + std::to_string(g) + ": " + c->err);
+        }
+    for (uint32_t i = 0; i < n_kmers; ++i) {
+        uint64_t v = 0;
+        for (size_t g = 0; g < G; ++g) v += part[g][i];
+        counts[i] = v;
+    }
+    return AC_OK;
+}
+
+ac_status ac_create_multi(ac_ctx** out, int n_gpus) {
+    if (!out) return fail(nullptr, AC_ERR_INVALID, "out is NULL");
+    *out = nullptr;
+    if (n_gpus < 1) return fail(nullptr, AC_ERR_INVALID, "n_gpus must be >= 1");
+    const int n_dev = ac_device_count();
+    if (n_dev < 1) return fail(nullptr, AC_ERR_DEVICE, "no HIP device available (the approximate count runs on the GPU only)");
+    ac_ctx* root = nullptr;
+    if (ac_status st = ac_create(&root, 0)) return st;
+    for (int g = 1; g < n_gpus; ++g) {
+        ac_ctx* c = nullptr;
+        if (ac_status st = ac_create(&c, g % n_dev)) {
+            ac_destroy(root);
+            return st;
+        }
+        root->peers.push_back(c);
+    }
+    *out = root;
+    return AC_OK;
+}
+
+ac_status ac_count(ac_ctx* ctx, uint32_t k, const uint64_t* kmers, uint32_t n_kmers, const uint32_t* win_bits,
+                   const uint32_t* win_nmask, const uint64_t* win_word_offset, const uint16_t* win_len,
+                   uint32_t n_windows, uint64_t* counts_out) {
+    if (!ctx) return fail(nullptr, AC_ERR_INVALID, "ctx is NULL");
+    if (n_windows && (!win_bits || !win_nmask || !win_word_offset || !win_len))
+        return fail(ctx, AC_ERR_INVALID, "NULL window array");
+    std::vector<uint64_t> start(n_windows);
+    std::vector<uint32_t> len(n_windows);
+    uint64_t n_bases = 32;
+    for (uint32_t i = 0; i < n_windows; ++i) {
+        if (win_word_offset[i] % 2)
+            return fail(ctx, AC_ERR_INVALID, "window " + std::to_string(i) + " starts at an odd 2-bit word");
+        start[i] = win_word_offset[i] * 16;
+        len[i] = win_len[i];
+        n_bases = std::max<uint64_t>(n_bases, (start[i] + len[i] + 31) / 32 * 32);
+    }
+    const ac_windows w{win_bits, win_nmask, start.data(), len.data(), n_windows, n_bases};
+    return ac_error_count(ctx, k, kmers, n_kmers, &w, counts_out);
 }
 
 ac_status ac_sample_upload(ac_ctx* ctx, const ac_windows* host, ac_windows* dev) {

@@ -18,7 +18,6 @@
 #include <random>
 #include <stdexcept>
 #include <string>
-#include <thread>
 #include <vector>
 
 #include "approx_counter_amd.h"
@@ -192,63 +191,25 @@ ac_windows view(const PackedImage& p) {
     return ac_windows{p.codes.data(), p.nmask.data(), p.start.data(), p.length.data(), (uint32_t)p.size(), p.n_bases};
 }
 
+// The device context: -g N opens N shards (device g mod the visible devices,
+// ac_create_multi); the exact count and the one-GPU approximate count use the
+// first device, the sharded count goes through ac_error_count.
 struct Devices {
-    std::vector<ac_ctx*> ctx;
-    ~Devices() {
-        for (ac_ctx* c : ctx) ac_destroy(c);
-    }
+    ac_ctx* ctx = nullptr;
+    uint64_t shards = 1;
+    ~Devices() { ac_destroy(ctx); }
 };
 
+// errorCount (approx_counter.cpp:531-601) through the C ABI on a host image.
 pair_vector error_count(Devices& dev, const PackedImage& img, const pair_vector& first_n, uint32_t k) {
-    const size_t n = first_n.size();
-    pair_vector out(n);
-    if (n == 0) return out;
-    std::vector<uint64_t> kmers(n);
-    for (size_t i = 0; i < n; ++i) kmers[i] = first_n[i].first;
-    const size_t G = dev.ctx.size();
-    // shard boundaries balanced by Σ window length
-    uint64_t total = 0;
-    for (uint32_t l : img.length) total += l;
-    std::vector<size_t> cut(G + 1, img.size());
-    cut[0] = 0;
-    {
-        uint64_t acc = 0;
-        size_t g = 1;
-        for (size_t i = 0; i < img.size() && g < G; ++i) {
-            acc += img.length[i];
-            while (g < G && acc * G >= total * g) cut[g++] = i + 1;
-        }
-    }
-    std::vector<std::vector<uint64_t>> part(G, std::vector<uint64_t>(n, 0));
-    std::vector<std::string> err(G);
-    std::vector<std::thread> th;
-    for (size_t g = 0; g < G; ++g) {
-        th.emplace_back([&, g] {
-            try {
-                // shard g = windows [lo, hi): a slice of the image, starts rebased
-                const size_t lo = cut[g], hi = cut[g + 1];
-                const uint64_t b0 = lo < img.size() ? img.start[lo] : img.n_bases;
-                const uint64_t b1 = hi < img.size() ? img.start[hi] : img.n_bases;
-                if (hi == lo || b1 == b0) return;  // nothing but empty windows: no k-mer occurrences
-                std::vector<uint64_t> st(hi - lo);
-                for (size_t i = lo; i < hi; ++i) st[i - lo] = img.start[i] - b0;
-                const ac_windows w{img.codes.data() + b0 / 16, img.nmask.data() + b0 / 32, st.data(),
-                                   img.length.data() + lo, (uint32_t)(hi - lo), b1 - b0};
-                if (ac_error_count(dev.ctx[g], k, kmers.data(), (uint32_t)n, &w, part[g].data()) != AC_OK)
-                    err[g] = ac_last_error(dev.ctx[g]);
-            } catch (const std::exception& e) {
-                err[g] = e.what();
-            }
-        });
-    }
-    for (auto& t : th) t.join();
-    for (size_t g = 0; g < G; ++g)
-        if (!err[g].empty()) throw std::runtime_error("approximate count failed on GPU " + std::to_string(g) + ": " + err[g]);
-    for (size_t i = 0; i < n; ++i) {
-        uint64_t s = 0;
-        for (size_t g = 0; g < G; ++g) s += part[g][i];
-        out[i] = {kmers[i], s};
-    }
+    pair_vector out(first_n.size());
+    if (first_n.empty()) return out;
+    std::vector<uint64_t> kmers(first_n.size()), counts(first_n.size());
+    for (size_t i = 0; i < first_n.size(); ++i) kmers[i] = first_n[i].first;
+    const ac_windows w = view(img);
+    if (ac_error_count(dev.ctx, k, kmers.data(), (uint32_t)kmers.size(), &w, counts.data()) != AC_OK)
+        throw std::runtime_error(ac_last_error(dev.ctx));
+    for (size_t i = 0; i < kmers.size(); ++i) out[i] = {kmers[i], counts[i]};
     return out;
 }
 
@@ -266,19 +227,15 @@ bool write_image(const PackedImage& p, const std::string& path) {
     return std::fclose(f) == 0 && ok;
 }
 
-// Opens one context per shard (-g N: shard g on device g mod visible devices).
 void open_devices(Devices& dev, uint64_t n_gpus) {
-    if (!dev.ctx.empty()) return;
+    if (dev.ctx) return;
     if (n_gpus < 1) n_gpus = 1;
     const int n_dev = ac_device_count();
     if (n_dev < 1) throw std::runtime_error("no HIP device available (the approximate count runs on the GPU only)");
     if ((int)n_gpus > n_dev)
         std::cerr << "/!\\ WARNING: " << n_gpus << " shards requested on " << n_dev << " visible GPU(s)\n";
-    for (uint64_t g = 0; g < n_gpus; ++g) {
-        ac_ctx* c = nullptr;
-        if (ac_create(&c, (int)(g % (uint64_t)n_dev)) != AC_OK) throw std::runtime_error(ac_last_error(nullptr));
-        dev.ctx.push_back(c);
-    }
+    if (ac_create_multi(&dev.ctx, (int)n_gpus) != AC_OK) throw std::runtime_error(ac_last_error(nullptr));
+    dev.shards = n_gpus;
 }
 
 // count_kmers + get_most_frequent / get_solid_kmers (approx_counter.cpp:874-899)
@@ -449,9 +406,9 @@ int main(int argc, char const** argv) {
                 try {
                     open_devices(dev, n_gpus);
                     const ac_windows hw = view(img);
-                    if (ac_sample_upload(dev.ctx[0], &hw, &dsample) != AC_OK)
-                        throw std::runtime_error(ac_last_error(dev.ctx[0]));
-                    first_n = exact_count_gpu(dev.ctx[0], dsample, (uint32_t)k, lc, forbidden, limit, solid_km,
+                    if (ac_sample_upload(dev.ctx, &hw, &dsample) != AC_OK)
+                        throw std::runtime_error(ac_last_error(dev.ctx));
+                    first_n = exact_count_gpu(dev.ctx, dsample, (uint32_t)k, lc, forbidden, limit, solid_km,
                                               &n_found, &had_n);
                 } catch (const std::exception& e) {
                     std::cerr << error_pref << "exact count failed: " << e.what() << std::endl;
@@ -478,12 +435,12 @@ int main(int argc, char const** argv) {
             pair_vector error_counter;
             try {
                 open_devices(dev, n_gpus);
-                if (!host_exact && dev.ctx.size() == 1) {  // one GPU: count on the sample uploaded above
+                if (!host_exact && dev.shards == 1) {  // one GPU: count on the sample uploaded above
                     std::vector<uint64_t> km(first_n.size()), ct(first_n.size());
                     for (size_t i = 0; i < first_n.size(); ++i) km[i] = first_n[i].first;
-                    if (!km.empty() && ac_error_count_sample(dev.ctx[0], (uint32_t)k, km.data(), (uint32_t)km.size(),
+                    if (!km.empty() && ac_error_count_sample(dev.ctx, (uint32_t)k, km.data(), (uint32_t)km.size(),
                                                              &dsample, ct.data()) != AC_OK)
-                        throw std::runtime_error(ac_last_error(dev.ctx[0]));
+                        throw std::runtime_error(ac_last_error(dev.ctx));
                     error_counter.resize(km.size());
                     for (size_t i = 0; i < km.size(); ++i) error_counter[i] = {km[i], ct[i]};
                 } else {

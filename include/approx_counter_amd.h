@@ -80,6 +80,29 @@ typedef struct ac_segment {
  * the index construction + omp_set_num_threads of errorCount (537-547). */
 ac_status ac_create(ac_ctx** out, int device);
 void ac_destroy(ac_ctx* ctx);
+/*
+ * A context over `n_gpus` devices of this node (device g mod the visible
+ * devices for shard g; SURVEY.md §8(b) "ac_create(ac_ctx**, int n_gpus)").
+ * ac_error_count and ac_count on it split the windows into n_gpus contiguous
+ * shards balanced by bases, count each shard on its device concurrently and
+ * sum the counts on the host (errorCount's OpenMP loop, 547-599, spread over
+ * GPUs; integer sums, so bit-identical to one device).  The device-buffer
+ * entry points use the first device only.  n_gpus = 1 is ac_create(out, 0).
+ */
+ac_status ac_create_multi(ac_ctx** out, int n_gpus);
+
+/*
+ * SURVEY.md §8(b)'s count entry point, argument for argument: errorCount
+ * (531-601) over windows given as a 2-bit image (win_bits, 16 bases per
+ * little-endian u32, A0 C1 G2 T3) and an N bitmap (win_nmask, 32 bases per
+ * u32); window i starts at 2-bit word win_word_offset[i] (an even word: 32-base
+ * aligned, so the same offset indexes the bitmap) and holds win_len[i] bases.
+ * counts_out[i] = M1 count of kmers[i].  Synchronous, host buffers.
+ */
+ac_status ac_count(ac_ctx* ctx, uint32_t k, const uint64_t* kmers, uint32_t n_kmers, const uint32_t* win_bits,
+                   const uint32_t* win_nmask, const uint64_t* win_word_offset, const uint16_t* win_len,
+                   uint32_t n_windows, uint64_t* counts_out);
+
 /* Number of HIP devices visible to this process (0 without a GPU).  The
  * reference has no counterpart: its errorCount runs on the host's OpenMP
  * threads (approx_counter.cpp:547); the CLI uses this to map -g shards onto

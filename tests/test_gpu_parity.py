@@ -147,3 +147,27 @@ def test_error_count_mirror_cfg1(counter):
         res = ac.error_count(wins, exact, 4, k, 0)
         ranked = host_ref.get_most_frequent(res, params["lim"], k)
         assert host_ref.export_lines(ranked, k) == open(os.path.join(d, "out.txt_0." + end)).read()
+
+
+def test_survey_ac_count_layout(counter):
+    """ac_count (SURVEY.md 8(b) argument list): the same counts as ac_error_count on
+    the same image, with word offsets and uint16 lengths."""
+    kmers, wins = cases.planted_case(8080, 16, 200, 700, win_len=(0, 260), p_n=0.02)
+    ps = ac.pack_windows(wins)
+    got = counter.count_words(16, kmers, ps.codes, ps.nmask, ps.start // 16, ps.length.astype(np.uint16))
+    assert np.array_equal(got, oracle.count_myers(16, kmers, wins))
+    with pytest.raises(ac.ApproxCounterError):  # odd word offset: not 32-base aligned
+        counter.count_words(16, kmers, ps.codes, ps.nmask, ps.start // 16 + 1, ps.length.astype(np.uint16))
+
+
+@pytest.mark.parametrize("shards", [2, 3, 7])
+def test_multi_gpu_context_shards_equal_one(shards):
+    """ac_create_multi: windows split into `shards` slices (wrapping onto this box's
+    GPUs), counted concurrently, summed on the host: identical to one device,
+    including shards holding only empty windows."""
+    kmers, wins = cases.planted_case(9090 + shards, 13, 150, 40, win_len=(0, 200), p_n=0.01)
+    wins = wins + ["", "", ""]  # trailing empty windows (start == image end)
+    exp = oracle.count_myers(13, kmers, wins)
+    with ac.ApproxCounter(n_gpus=shards) as multi:
+        assert np.array_equal(multi.count(13, kmers, ac.pack_windows(wins)), exp)
+        assert np.array_equal(multi.count(13, kmers, ac.pack_windows(wins[:2])), oracle.count_myers(13, kmers, wins[:2]))
