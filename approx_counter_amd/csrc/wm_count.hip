@@ -281,6 +281,9 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, Stage& st) {
         for (int p = 0; p < P; ++p) cnt[w][p] = 0;
 
     stamp(wave, 1);
+#ifdef AC_TAIL_PRIO
+    __builtin_amdgcn_s_setprio(AC_TAIL_PRIO);
+#endif
 
     // Counters of the other queue bank are zeroed for the next launch (strided
     // over the waves; nobody dequeues from that bank in this launch).
@@ -398,7 +401,22 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, Stage& st) {
             const uint64_t any_n = stage_write(st, f, lane);
             const uint32_t nb = min(SEG, len - sb);
             const uint32_t nfull = nb >> 4;
+#ifdef AC_TAIL_PRIO
+            // Tail scheduling (longest remaining work first): a wave whose claim
+            // came back empty is on its last window (unless it steals) and
+            // yields issue priority to waves that still hold a claimed window.
+            uint32_t ch0 = 0;
+            if (sb == 0 && wn >= item_end && nfull > 2) {
+                run_any<P, 16>(s, ph, pl, st, 0u, (any_n & 0xfu) != 0u);
+                run_any<P, 16>(s, ph, pl, st, 8u, ((any_n >> 4) & 0xfu) != 0u);
+                ch0 = 2;
+                if (item_of(waves_in(jc) + __builtin_amdgcn_readfirstlane(pending)) >= n_items)
+                    __builtin_amdgcn_s_setprio(AC_TAIL_PRIO - 1);
+            }
+            for (uint32_t ch = ch0; ch < nfull; ++ch)
+#else
             for (uint32_t ch = 0; ch < nfull; ++ch)
+#endif
                 run_any<P, 16>(s, ph, pl, st, ch * 8u, ((any_n >> (4u * ch)) & 0xfu) != 0u);
             const uint32_t rem = nb & 15u;
             if (rem) {
@@ -445,6 +463,9 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, Stage& st) {
             item = item_of(waves_in(jc) + __builtin_amdgcn_readfirstlane(pending));
             if (item >= n_items && S > 1) item = steal();
             if (item < n_items) {
+#ifdef AC_TAIL_PRIO
+                __builtin_amdgcn_s_setprio(AC_TAIL_PRIO);
+#endif
                 w = item * chunk;
                 item_end = min(sg.n_windows, w + chunk);
                 nbase = sg.start[w];
