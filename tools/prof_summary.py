@@ -94,7 +94,7 @@ def main():
     if a.title:
         text = f"## {a.title}\n\n" + text
     if a.out:
-        with open(a.out, "a") as fh:
+        with open(a.out, "w") as fh:
             fh.write(text + "\n")
     print(text)
 
