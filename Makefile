@@ -6,6 +6,9 @@
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -Wall
+# wm_count: keep the queue-claim atomic a plain returning atomic (the optimizer's wave-aggregated
+# form waits for the result at once, exposing the claim latency the kernel hides behind a window)
+WM_FLAGS ?= -mllvm -amdgpu-atomic-optimizer-strategy=None
 PKG := approx_counter_amd
 CSRC := $(PKG)/csrc
 LIBDIR := $(PKG)/lib
@@ -25,6 +28,10 @@ BINDIR := $(PKG)/bin
 CLI := $(BINDIR)/adaptFinder
 
 all: $(LIB) $(HOSTLIB) $(CLI) oracle
+
+$(OBJDIR)/wm_count.o: $(CSRC)/wm_count.hip $(CSRC)/wm_tid_blocks.inc $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) $(WM_FLAGS) -Iinclude -I$(CSRC) -c $< -o $@
 
 $(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
@@ -52,7 +59,7 @@ oracle:
 
 asm: $(CSRC)/wm_count.hip $(HDRS)
 	@mkdir -p build/asm
-	$(HIPCC) $(HIPFLAGS) -Iinclude -I$(CSRC) --cuda-device-only -S $< -o build/asm/wm_count.s
+	$(HIPCC) $(HIPFLAGS) $(WM_FLAGS) -Iinclude -I$(CSRC) --cuda-device-only -S $< -o build/asm/wm_count.s
 
 clean:
 	rm -rf build $(LIBDIR) $(BINDIR) oracle/_build

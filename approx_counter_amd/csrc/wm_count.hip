@@ -235,8 +235,67 @@ __device__ __forceinline__ void build_masks(const uint64_t (&km)[P], uint32_t m,
     }
 }
 
+#ifdef AC_TID
+#include "wm_tid_blocks.inc"
+
+// Per-wave ~Eq table: word c*64 + lane = the lane's ~Eq mask for character c
+// (A C G T, then N = all ones), read per base with ds_read_addtid_b32.
+struct TidTable {
+    uint32_t e[5 * 64];
+};
+
+// Lane `lane`'s word of window bases [sb, sb + SEG): lanes 0-15 the 16 code
+// words, lanes 16-23 the 8 N-mask words.  One unconditional load per lane with
+// the index clamped to the window's last word (always inside the image): a word
+// past the window is never read as text (the chunk loop stops at the window
+// length), and a branch-free load keeps hipcc from waiting on it before the
+// window that uses it.
+__device__ __forceinline__ uint32_t tid_fetch(const uint32_t* __restrict__ codes, const uint32_t* __restrict__ nmask,
+                                              uint32_t len, uint32_t sb, uint32_t lane) {
+    const bool is_code = lane < 16u;
+    const uint32_t ci = min((sb >> 4) + lane, (len - 1u) >> 4);
+    const uint32_t ni = min((sb >> 5) + ((lane - 16u) & 7u), (len - 1u) >> 5);
+    const uint32_t* p = is_code ? codes + ci : nmask + ni;
+    return *p;
+}
+
+// The remainder (< 16 bases) of a segment: blocks of 8, 4, 2, 1 bases, N-aware.
 template <int P>
-__device__ __forceinline__ void count_body(const LaunchArgs& a, Stage& st) {
+__device__ __forceinline__ void tid_tail(TidNfa& s, uint32_t code, uint32_t nm, uint32_t rem, uint32_t eb) {
+    if (rem & 8u) {
+        tid_block8n<P>(s, code, nm, eb);
+        code >>= 16;
+        nm >>= 8;
+    }
+    if (rem & 4u) {
+        tid_block4n<P>(s, code, nm, eb);
+        code >>= 8;
+        nm >>= 4;
+    }
+    if (rem & 2u) {
+        tid_block2n<P>(s, code, nm, eb);
+        code >>= 4;
+        nm >>= 2;
+    }
+    if (rem & 1u) tid_block1n<P>(s, code, nm, eb);
+}
+using StageT = TidTable;
+using FetchT = uint32_t;
+__device__ __forceinline__ FetchT fetchw(const uint32_t* __restrict__ codes, const uint32_t* __restrict__ nmask,
+                                         uint32_t len, uint32_t sb, uint32_t lane) {
+    return tid_fetch(codes, nmask, len, sb, lane);
+}
+#else
+using StageT = Stage;
+using FetchT = Fetch;
+__device__ __forceinline__ FetchT fetchw(const uint32_t* __restrict__ codes, const uint32_t* __restrict__ nmask,
+                                         uint32_t len, uint32_t sb, uint32_t lane) {
+    return fetch(codes, nmask, len, sb, lane);
+}
+#endif
+
+template <int P>
+__device__ __forceinline__ void count_body(const LaunchArgs& a, StageT& st) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t wave = (uint64_t)blockIdx.x * WAVES_PER_BLOCK + wib;
@@ -273,6 +332,14 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, Stage& st) {
     }
     // Initial rows (empty text): R1 has character 0 set, R2 characters 0 and 1.
     const uint32_t d1_init = ~first, d2_init = ~(first | (first >> P));
+#ifdef AC_TID
+    static_assert(W == 1, "the table-driven loop runs one lane word");
+#pragma unroll
+    for (int c = 0; c < 4; ++c) st.e[c * 64 + lane] = ((c & 2) ? ~ph[0] : ph[0]) | ((c & 1) ? ~pl[0] : pl[0]);
+    st.e[4 * 64 + lane] = ~0u;
+    const uint32_t eb = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)(&st.e[0]));
+#endif
 
     uint32_t cnt[W][P];
 #pragma unroll
@@ -281,9 +348,6 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, Stage& st) {
         for (int p = 0; p < P; ++p) cnt[w][p] = 0;
 
     stamp(wave, 1);
-#ifdef AC_TAIL_PRIO
-    __builtin_amdgcn_s_setprio(AC_TAIL_PRIO);
-#endif
 
     // Counters of the other queue bank are zeroed for the next launch (strided
     // over the waves; nobody dequeues from that bank in this launch).
@@ -358,16 +422,23 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, Stage& st) {
     auto valid = [&](uint64_t base, uint32_t len) { return !(base & 31u) && base + len <= sg.n_bases; };
     uint64_t nbase = 0;
     uint32_t nlen = 0;
-    Fetch nf = {0u, 0u};
+    FetchT nf{};
     if (item < n_items) {
         nbase = sg.start[w];
         nlen = sg.length[w];
-        if (valid(nbase, nlen)) nf = fetch(sg.codes + (nbase >> 4), sg.nmask + (nbase >> 5), nlen, 0, lane);
+        if (valid(nbase, nlen)) nf = fetchw(sg.codes + (nbase >> 4), sg.nmask + (nbase >> 5), nlen, 0, lane);
     }
     while (item < n_items) {
         const uint64_t base = nbase;
         const uint32_t len = nlen;
-        const Fetch f0 = nf;
+#ifdef AC_TID
+        // Wait for this window's words here, before the next window's fetch is
+        // issued: inside the chunk loop hipcc would otherwise wait for both.
+        FetchT f0 = nf;
+        asm volatile("" : "+v"(f0));
+#else
+        const FetchT f0 = nf;
+#endif
         // Within an item the next window is fetched while this one is counted.
         // During an item's last window the next item is claimed (one returning
         // atomic); it is read after the window, so a wave the arbiter starves
@@ -376,13 +447,41 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, Stage& st) {
         if (wn < item_end) {
             nbase = sg.start[wn];
             nlen = sg.length[wn];
-            if (valid(nbase, nlen)) nf = fetch(sg.codes + (nbase >> 4), sg.nmask + (nbase >> 5), nlen, 0, lane);
+            if (valid(nbase, nlen)) nf = fetchw(sg.codes + (nbase >> 4), sg.nmask + (nbase >> 5), nlen, 0, lane);
         } else {
             pending = dequeue_issue();
         }
         if (valid(base, len)) {  // a malformed window is skipped: never read outside the image
         const uint32_t* __restrict__ codes = sg.codes + (base >> 4);
         const uint32_t* __restrict__ nmask = sg.nmask + (base >> 5);
+#ifdef AC_TID
+        TidNfa s = {~0u, d1_init, d2_init, ~0u >> P, d1_init >> P, d2_init >> P, ~0u, d1_init, d2_init};
+        auto segment = [&](uint32_t f, uint32_t sb) {
+            const uint32_t nb = min(SEG, len - sb);
+            const uint32_t nfull = nb >> 4;
+            for (uint32_t ch = 0; ch < nfull; ++ch) {
+                const uint32_t code = __builtin_amdgcn_readlane(f, ch);
+                const uint32_t nm = (__builtin_amdgcn_readlane(f, 16u + (ch >> 1)) >> ((ch & 1u) * 16u)) & 0xffffu;
+                tid_block16n<P>(s, code, nm, eb);
+            }
+            if (nb & 15u) {
+                const uint32_t code = __builtin_amdgcn_readlane(f, nfull);
+                const uint32_t nm = (__builtin_amdgcn_readlane(f, 16u + (nfull >> 1)) >> ((nfull & 1u) * 16u)) & 0xffffu;
+                tid_tail<P>(s, code, nm, nb & 15u, eb);
+            }
+        };
+        segment(f0, 0u);
+        for (uint32_t sb = SEG; sb < len; sb += SEG) {  // windows longer than one segment
+            uint32_t f = tid_fetch(codes, nmask, len, sb, lane);
+            asm volatile("" : "+v"(f));
+            segment(f, sb);
+        }
+#pragma unroll
+        for (int p = 0; p < P; ++p) {
+            const uint32_t lb = 31u - ((m - 1u) * P + (uint32_t)p);
+            cnt[0][p] += 3u - ((s.a0 >> lb) & 1u) - ((s.a1 >> lb) & 1u) - ((s.a2 >> lb) & 1u);
+        }
+#else
         Nfa s;
 #pragma unroll
         for (int x = 0; x < W; ++x) {
@@ -401,22 +500,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, Stage& st) {
             const uint64_t any_n = stage_write(st, f, lane);
             const uint32_t nb = min(SEG, len - sb);
             const uint32_t nfull = nb >> 4;
-#ifdef AC_TAIL_PRIO
-            // Tail scheduling (longest remaining work first): a wave whose claim
-            // came back empty is on its last window (unless it steals) and
-            // yields issue priority to waves that still hold a claimed window.
-            uint32_t ch0 = 0;
-            if (sb == 0 && wn >= item_end && nfull > 2) {
-                run_any<P, 16>(s, ph, pl, st, 0u, (any_n & 0xfu) != 0u);
-                run_any<P, 16>(s, ph, pl, st, 8u, ((any_n >> 4) & 0xfu) != 0u);
-                ch0 = 2;
-                if (item_of(waves_in(jc) + __builtin_amdgcn_readfirstlane(pending)) >= n_items)
-                    __builtin_amdgcn_s_setprio(AC_TAIL_PRIO - 1);
-            }
-            for (uint32_t ch = ch0; ch < nfull; ++ch)
-#else
             for (uint32_t ch = 0; ch < nfull; ++ch)
-#endif
                 run_any<P, 16>(s, ph, pl, st, ch * 8u, ((any_n >> (4u * ch)) & 0xfu) != 0u);
             const uint32_t rem = nb & 15u;
             if (rem) {
@@ -457,20 +541,18 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, Stage& st) {
                 cnt[x][p] += 3u - ((s.a0[x] >> lb) & 1u) - ((s.a1[x] >> lb) & 1u) - ((s.a2[x] >> lb) & 1u);
             }
         }
+#endif
         }  // valid window
         // advance the cursor; at an item boundary move to the prefetched item and request another
         if (++w >= item_end) {
             item = item_of(waves_in(jc) + __builtin_amdgcn_readfirstlane(pending));
             if (item >= n_items && S > 1) item = steal();
             if (item < n_items) {
-#ifdef AC_TAIL_PRIO
-                __builtin_amdgcn_s_setprio(AC_TAIL_PRIO);
-#endif
                 w = item * chunk;
                 item_end = min(sg.n_windows, w + chunk);
                 nbase = sg.start[w];
                 nlen = sg.length[w];
-                if (valid(nbase, nlen)) nf = fetch(sg.codes + (nbase >> 4), sg.nmask + (nbase >> 5), nlen, 0, lane);
+                if (valid(nbase, nlen)) nf = fetchw(sg.codes + (nbase >> 4), sg.nmask + (nbase >> 5), nlen, 0, lane);
             }
         }
     }
@@ -496,7 +578,7 @@ __global__ __launch_bounds__(64 * WAVES_PER_BLOCK, AC_MIN_WAVES_PER_SIMD) void w
     // The LDS allocation also caps residency at AC_BLOCKS_PER_CU blocks (6 waves
     // per SIMD): measured faster than 8 (fewer waves starved by the oldest-first
     // VALU arbitration; profiles/r01_kernel_log.md).
-    __shared__ Stage stage[(160 * 1024 / AC_BLOCKS_PER_CU) / sizeof(Stage)];
+    __shared__ StageT stage[(160 * 1024 / AC_BLOCKS_PER_CU) / sizeof(StageT)];
     count_body<P>(a, stage[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)]);
 }
 

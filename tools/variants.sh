@@ -9,7 +9,7 @@ while [ $# -gt 1 ]; do
   name=$1; flags=$2; shift 2
   out=build/var/$name; mkdir -p $out
   /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Iinclude -Iapprox_counter_amd/csrc $flags \
-    -c approx_counter_amd/csrc/wm_count.hip -o $out/wm_count.o
+    -mllvm -amdgpu-atomic-optimizer-strategy=None -c approx_counter_amd/csrc/wm_count.hip -o $out/wm_count.o
   /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Iinclude -Iapprox_counter_amd/csrc $flags \
     -c approx_counter_amd/csrc/exact_count.hip -o $out/exact_count.o
   /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Iinclude -Iapprox_counter_amd/csrc $flags \
