@@ -51,7 +51,10 @@
 namespace acamd {
 namespace {
 
-constexpr int WAVES_PER_BLOCK = 4;
+#ifndef AC_WAVES_PER_BLOCK
+#define AC_WAVES_PER_BLOCK 4
+#endif
+constexpr int WAVES_PER_BLOCK = AC_WAVES_PER_BLOCK;
 #ifdef AC_STAMPS
 // Diagnostic build only (tools/variants.sh ... -DAC_STAMPS): per-wave
 // s_memrealtime stamps (100 MHz) at entry, after the prologue, after the last
@@ -259,25 +262,29 @@ __device__ __forceinline__ uint32_t tid_fetch(const uint32_t* __restrict__ codes
     return *p;
 }
 
-// The remainder (< 16 bases) of a segment: blocks of 8, 4, 2, 1 bases, N-aware.
+// With one-wave workgroups the wave's table is the block's only LDS object, at
+// address 0, and M0 needs no per-base add (tools/gen_tid_blocks.py, eb0).
+constexpr bool TID_EB0 = WAVES_PER_BLOCK == 1;
+
+// The remainder (< 16 bases) of a segment: blocks of 8, 4, 2, 1 bases.
 template <int P>
 __device__ __forceinline__ void tid_tail(TidNfa& s, uint32_t code, uint32_t nm, uint32_t rem, uint32_t eb) {
     if (rem & 8u) {
-        tid_block8n<P>(s, code, nm, eb);
+        tid_block8<P, TID_EB0>(s, code, nm & 0xffu, eb);
         code >>= 16;
         nm >>= 8;
     }
     if (rem & 4u) {
-        tid_block4n<P>(s, code, nm, eb);
+        tid_block4<P, TID_EB0>(s, code, nm & 0xfu, eb);
         code >>= 8;
         nm >>= 4;
     }
     if (rem & 2u) {
-        tid_block2n<P>(s, code, nm, eb);
+        tid_block2<P, TID_EB0>(s, code, nm & 0x3u, eb);
         code >>= 4;
         nm >>= 2;
     }
-    if (rem & 1u) tid_block1n<P>(s, code, nm, eb);
+    if (rem & 1u) tid_block1<P, TID_EB0>(s, code, nm & 0x1u, eb);
 }
 using StageT = TidTable;
 using FetchT = uint32_t;
@@ -339,6 +346,10 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, StageT& st) {
     st.e[4 * 64 + lane] = ~0u;
     const uint32_t eb = __builtin_amdgcn_readfirstlane(
         (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)(&st.e[0]));
+    // The eb0 blocks address the table from LDS 0.  Never expected otherwise; if
+    // it were, the wave stops (no fault) and the counts come out short, which
+    // the parity tests catch.
+    if (TID_EB0 && eb != 0u) return;
 #endif
 
     uint32_t cnt[W][P];
@@ -462,7 +473,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, StageT& st) {
             for (uint32_t ch = 0; ch < nfull; ++ch) {
                 const uint32_t code = __builtin_amdgcn_readlane(f, ch);
                 const uint32_t nm = (__builtin_amdgcn_readlane(f, 16u + (ch >> 1)) >> ((ch & 1u) * 16u)) & 0xffffu;
-                tid_block16n<P>(s, code, nm, eb);
+                tid_block16<P, TID_EB0>(s, code, nm, eb);
             }
             if (nb & 15u) {
                 const uint32_t code = __builtin_amdgcn_readlane(f, nfull);

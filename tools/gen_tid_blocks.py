@@ -13,8 +13,10 @@ is wave-uniform: base j's 2-bit code sits at bits 2j..2j+1 of the SGPR `code`
          (a per-wave table of 5 x 64 words built once per wave: no VALU op per
          base for ~Eq; the read is issued three bases ahead)
   VALU   8 ops of NFA + 1.5 of hit accumulation (AND3 over two bases).
-The NFA state alternates between register sets A (operands) and B (scratch) from
-base to base, so no register copies; even NB ends in A, odd NB copies B back.
+The schedule is skewed: step s runs row 0 of base s, row 1 of base s-1 and row 2
+of base s-2, three independent dependency chains per wave (in-order issue would
+otherwise stall on every one of the 8 dependent ops of a base).  Values rotate
+through 4 register slots, so blocks of a multiple of 4 bases end in place.
 M0 is compiler-reserved: each block saves and restores it in the same statement.
 """
 import os
@@ -22,76 +24,116 @@ import os
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "approx_counter_amd", "csrc", "wm_tid_blocks.inc")
 AHEAD = 3  # LDS reads in flight ahead of the base being computed
-NE = AHEAD + 1  # rotating ~Eq registers
+NE = AHEAD + 3  # rotating ~Eq registers (base i's is read by rows 0-2 at steps i..i+2)
 
 
-def m0_setup(j, with_n):
+def m0_setup(j, with_n, eb0):
+    """SALU: M0 = ebase + 256 * (code of base j, or 4 for N).  With eb0 the
+    wave's table sits at LDS address 0 (one-wave workgroups) and the add goes."""
     lit = (2 << 16) | (2 * j)
     s = [f"s_bfe_u32 %[t], %[code], {lit:#x}"]
     if with_n:
         s += [f"s_bitcmp1_b32 %[nm], {j}", "s_cselect_b32 %[t], 4, %[t]"]
-    s += ["s_lshl_b32 %[t], %[t], 8", "s_add_u32 m0, %[t], %[eb]"]
+    if eb0:
+        s += ["s_lshl_b32 m0, %[t], 8"]
+    else:
+        s += ["s_lshl_b32 %[t], %[t], 8", "s_add_u32 m0, %[t], %[eb]"]
     return s
 
 
-def block(nb, with_n):
-    A = ["d0", "d1", "d2", "s0", "s1", "s2"]
-    B = ["n0", "n1", "n2", "u0", "u1", "u2"]
-    L = ["s_mov_b32 %[keep], m0"]
+def block(nb, with_n, eb0):
+    """Skewed (software-pipelined) schedule: step s runs row 0 of base s, row 1 of
+    base s-1 and row 2 of base s-2 -- three independent dependency chains per wave.
+    Row r of base i needs row r of base i-1 and row r-1 of bases i-1 and i, all
+    produced at earlier steps.  Values live in 4 rotating slots per (row, D/T);
+    slot 3 is the operand register, so blocks of a multiple of 4 bases end in place."""
+
+    def D(r, i):
+        return f"%[d{r}]" if i % 4 == 3 else f"%[D{r}{i % 4}]"
+
+    def T(r, i):
+        return f"%[s{r}]" if i % 4 == 3 else f"%[T{r}{i % 4}]"
+
+    def E(i):
+        return f"%[e{i % NE}]"
+
+    L = []
     for j in range(min(AHEAD, nb)):
-        L += m0_setup(j, with_n)
-        L += ["s_nop 0", f"ds_read_addtid_b32 %[e{j % NE}]"]
-    for j in range(nb):
-        X, Y = (A, B) if j % 2 == 0 else (B, A)
-        x = dict(zip(["d0", "d1", "d2", "s0", "s1", "s2"], X))
-        y = dict(zip(["d0", "d1", "d2", "s0", "s1", "s2"], Y))
-        e = f"%[e{j % NE}]"
-        issued = min(j + AHEAD, nb)
-        L.append(f"s_waitcnt lgkmcnt({issued - (j + 1)})")
-        ahead = j + AHEAD < nb
+        L += m0_setup(j, with_n, eb0)
+        L += ["s_nop 0", f"ds_read_addtid_b32 {E(j)}"]
+    for st in range(nb + 2):
+        rows = [(r, st - r) for r in range(3) if 0 <= st - r < nb]
+        if st < nb:
+            issued = min(st + AHEAD, nb)
+            L.append(f"s_waitcnt lgkmcnt({issued - (st + 1)})")
+        ahead = st < nb and st + AHEAD < nb
         if ahead:
-            L += m0_setup(j + AHEAD, with_n)
-        L.append(f"v_or_b32 %[{y['d0']}], %[{x['s0']}], {e}")  # one state after the M0 write
-        if ahead:
-            L.append(f"ds_read_addtid_b32 %[e{(j + AHEAD) % NE}]")
-        L += [
-            f"v_lshrrev_b32 %[{y['s0']}], %[P], %[{y['d0']}]",
-            f"v_bitop3_b32 %[x1], %[{x['s0']}], %[{x['d0']}], %[{y['s0']}] bitop3:0x80",
-            f"v_bitop3_b32 %[{y['d1']}], %[{x['s1']}], {e}, %[x1] bitop3:0xa8",
-            f"v_lshrrev_b32 %[{y['s1']}], %[P], %[{y['d1']}]",
-            f"v_bitop3_b32 %[x2], %[{x['s1']}], %[{x['d1']}], %[{y['s1']}] bitop3:0x80",
-            f"v_bitop3_b32 %[{y['d2']}], %[{x['s2']}], {e}, %[x2] bitop3:0xa8",
-            f"v_lshrrev_b32 %[{y['s2']}], %[P], %[{y['d2']}]",
-        ]
-        if j % 2 == 1:  # rows of this base and the previous one into the accumulators
-            for r in range(3):
-                L.append(f"v_bitop3_b32 %[a{r}], %[a{r}], %[{x['d%d' % r]}], %[{y['d%d' % r]}] bitop3:0x80")
-    if nb % 2 == 1:  # last base unpaired; state ends in B: accumulate it alone, copy back
+            L += m0_setup(st + AHEAD, with_n, eb0)
+        # phase A: row 0's new D; rows 1-2's x = s_{r-1} & d_{r-1} & t_{r-1}
+        for r, i in rows:
+            if r == 0:
+                L.append(f"v_or_b32 {D(0, i)}, {T(0, i - 1)}, {E(i)}")
+            else:
+                L.append(f"v_bitop3_b32 %[x{r}], {T(r - 1, i - 1)}, {D(r - 1, i - 1)}, {T(r - 1, i)} bitop3:0x80")
+            if r == 0 and ahead:  # one state after the M0 write
+                L.append(f"ds_read_addtid_b32 {E(st + AHEAD)}")
+        # phase B: row 0's shift; rows 1-2's new D = (s_r | ~Eq) & x
+        for r, i in rows:
+            if r == 0:
+                L.append(f"v_lshrrev_b32 {T(0, i)}, %[P], {D(0, i)}")
+            else:
+                L.append(f"v_bitop3_b32 {D(r, i)}, {T(r, i - 1)}, {E(i)}, %[x{r}] bitop3:0xa8")
+        # phase C: rows 1-2's shifts, then the hit accumulators (pairs of bases)
+        for r, i in rows:
+            if r > 0:
+                L.append(f"v_lshrrev_b32 {T(r, i)}, %[P], {D(r, i)}")
+        for r, i in rows:
+            if i % 2 == 1:
+                L.append(f"v_bitop3_b32 %[a{r}], %[a{r}], {D(r, i - 1)}, {D(r, i)} bitop3:0x80")
+            elif i == nb - 1:  # unpaired last base (odd nb)
+                L.append(f"v_and_b32 %[a{r}], %[a{r}], {D(r, i)}")
+    if (nb - 1) % 4 != 3:  # final state not in the operand slot
         for r in range(3):
-            L.append(f"v_and_b32 %[a{r}], %[a{r}], %[n{r}]")
-        for a, b in zip(A, B):
-            L.append(f"v_mov_b32 %[{a}], %[{b}]")
-    L.append("s_mov_b32 m0, %[keep]")
+            L.append(f"v_mov_b32 %[d{r}], {D(r, nb - 1)}")
+            L.append(f"v_mov_b32 %[s{r}], {T(r, nb - 1)}")
     return L
 
 
-def emit(nb, with_n):
-    name = f"tid_block{nb}{'n' if with_n else ''}"
-    body = "\n".join(f'        "{ln}\\n\\t"' for ln in block(nb, with_n))
-    nm_in = ', [nm] "s"(nm)' if with_n else ""
-    nm_arg = ", uint32_t nm" if with_n else ""
-    return f"""template <int P>
-__device__ __forceinline__ void {name}(TidNfa& s, uint32_t code{nm_arg}, uint32_t eb) {{
-    uint32_t n0, n1, n2, u0, u1, u2, x1, x2, e0, e1, e2, e3, t, keep;
-    asm volatile(
-{body}
-        : [d0] "+v"(s.d0), [d1] "+v"(s.d1), [d2] "+v"(s.d2), [s0] "+v"(s.s0), [s1] "+v"(s.s1),
-          [s2] "+v"(s.s2), [a0] "+v"(s.a0), [a1] "+v"(s.a1), [a2] "+v"(s.a2), [n0] "=&v"(n0),
-          [n1] "=&v"(n1), [n2] "=&v"(n2), [u0] "=&v"(u0), [u1] "=&v"(u1), [u2] "=&v"(u2),
-          [x1] "=&v"(x1), [x2] "=&v"(x2), [e0] "=&v"(e0), [e1] "=&v"(e1), [e2] "=&v"(e2),
-          [e3] "=&v"(e3), [t] "=&s"(t), [keep] "=&s"(keep)
-        : [code] "s"(code), [eb] "s"(eb), [P] "n"(P){nm_in}
-        : "memory", "scc");
+def body(nb, eb0):
+    """Whole statement text: N-free chunks take the fast path, chunks with an N
+    the N-aware one (same registers, so hipcc sees one statement)."""
+    L = ["s_mov_b32 %[keep], m0", "s_cmp_lg_u32 %[nm], 0", "s_cbranch_scc1 .Lnpath%="]
+    L += block(nb, False, eb0)
+    L += ["s_branch .Lend%=", ".Lnpath%=:"]
+    L += block(nb, True, eb0)
+    L += [".Lend%=:", "s_mov_b32 m0, %[keep]"]
+    return "\n".join(f'            "{ln}\\n\\t"' for ln in L)
+
+
+def emit(nb):
+    scratch = [f"D{r}{k}" for r in range(3) for k in range(3)] + [f"T{r}{k}" for r in range(3) for k in range(3)]
+    scratch += ["x1", "x2"] + [f"e{k}" for k in range(NE)]
+    decl = ", ".join(scratch)
+    outs = ", ".join(f'[{v}] "=&v"({v})' for v in scratch)
+    operands = f"""            : [d0] "+v"(s.d0), [d1] "+v"(s.d1), [d2] "+v"(s.d2), [s0] "+v"(s.s0), [s1] "+v"(s.s1),
+              [s2] "+v"(s.s2), [a0] "+v"(s.a0), [a1] "+v"(s.a1), [a2] "+v"(s.a2),
+              {outs},
+              [t] "=&s"(t), [keep] "=&s"(keep)
+            : [code] "s"(code), [nm] "s"(nm), [eb] "s"(eb), [P] "n"(P)
+            : "memory", "scc");"""
+    return f"""template <int P, bool EB0>
+__device__ __forceinline__ void tid_block{nb}(TidNfa& s, uint32_t code, uint32_t nm, uint32_t eb) {{
+    uint32_t {decl};
+    uint32_t t, keep;
+    if constexpr (EB0) {{
+        asm volatile(
+{body(nb, True)}
+{operands}
+    }} else {{
+        asm volatile(
+{body(nb, False)}
+{operands}
+    }}
 }}
 """
 
@@ -104,8 +146,7 @@ def main():
         "struct TidNfa {\n    uint32_t d0, d1, d2, s0, s1, s2, a0, a1, a2;\n};\n\n"
     ]
     for nb in (16, 8, 4, 2, 1):
-        for with_n in (False, True):
-            parts.append(emit(nb, with_n))
+        parts.append(emit(nb))
     with open(OUT, "w") as fh:
         fh.write("\n".join(parts))
     print("wrote", OUT)
