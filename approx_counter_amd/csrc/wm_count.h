@@ -6,14 +6,8 @@
 #define AC_MAX_SEGS 4    // segments fused into one launch (start + end ends, shards)
 #define AC_QUEUE_LINE 32  // u32 per queue counter: one 128-B line each (no false sharing between counters)
 #define AC_MAX_PACK 4    // candidates interleaved per 32-bit lane word (P = min(32/k, 4))
-#ifndef AC_WAVE_WORDS
-#define AC_WAVE_WORDS 1  // lane words (independent NFAs) per lane (2 measured slower: profiles/r01_kernel_log.md)
-#endif
-#ifndef AC_BLOCKS_PER_CU
-#define AC_BLOCKS_PER_CU 6  // resident 256-thread blocks per CU (= waves per SIMD), set by the LDS allocation
-#endif
-#ifndef AC_MIN_WAVES_PER_SIMD
-#define AC_MIN_WAVES_PER_SIMD 6  // occupancy the register budget is sized for (<= 80 VGPRs)
+#ifndef AC_WAVES_PER_SIMD
+#define AC_WAVES_PER_SIMD 8  // resident count-kernel waves per SIMD, set by the LDS allocation (<= 64 VGPRs)
 #endif
 
 namespace acamd {
@@ -52,7 +46,7 @@ struct LaunchArgs {
 };
 
 inline uint32_t pack_factor(uint32_t k) { return (32u / k) < AC_MAX_PACK ? (32u / k) : AC_MAX_PACK; }
-inline uint32_t cands_per_wave(uint32_t P) { return 64u * P * AC_WAVE_WORDS; }
+inline uint32_t cands_per_wave(uint32_t P) { return 64u * P; }
 
 // Waves of the count kernel for pattern pack P that fit on the device at once.
 hipError_t resident_waves(uint32_t P, int cu_count, uint32_t* waves);

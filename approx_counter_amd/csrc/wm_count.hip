@@ -18,29 +18,27 @@
 // A window hits level d iff the AND of D_d over its positions has the
 // pattern's last bit clear; the count adds the three levels.
 //
-// MI355X mapping (DESIGN.md §Kernel):
-//  * lane = 2 words x P candidates, window text wave-uniform.  P = floor(32/k) (<= 4)
+// MI355X mapping (DESIGN.md §4):
+//  * lane = P candidates, window text wave-uniform.  P = floor(32/k) (<= 4)
 //    patterns are INTERLEAVED in one 32-bit register: character i of pattern p
 //    sits at bit 31 - (i*P + p), so one logical right shift by P advances every
 //    pattern at once and the zero fill reaches every pattern's first character.
-//    Each lane runs AC_WAVE_WORDS = 2 independent words (two candidate groups)
-//    over the same text: two independent dependency chains per wave and one
-//    staging / LDS read per base for 2P candidates.
-//  * Issue cost drives the instruction choice (tools/ubench_valu.hip,
-//    profiles/r01_ubench_valu.txt): on gfx950 v_and/v_or/v_xor/v_add/
-//    v_lshrrev_b32 and v_bitop3_b32 issue in 2 cycles per wave64 with VGPR
-//    operands; shifts left, v_or3, v_and_or, v_lshl_or and ANY instruction
-//    reading an SGPR take 4.  So every 3-input boolean is one v_bitop3_b32 and
-//    the text masks reach the VALU as VGPRs: each wave expands its window into
-//    per-base masks H = -(bit 1), L = -(bit 0), N in LDS (one lane per 4
-//    bases, ~0.1 VALU op per base) and reads them back as wave-uniform
-//    broadcast ds_read_b128 (two bases per read).  The next window's code and
-//    N-mask words are loaded while the current window is computed.  A base then costs 2 ops of ~Eq
-//    ( (ph ^ H) | (pl ^ L) ) + 8 ops of NFA + 1.5 of hit accumulation (v_bitop3
-//    AND3 over two bases) = 11.5 full-rate VALU ops for P candidates.
-//  * N (any non-ACGT base) never matches: a ballot at staging flags the
-//    16-base chunks holding an N; those take a path that ORs the base's N
-//    mask (also staged in LDS) into ~Eq at no extra VALU cost.
+//  * ~Eq is a table lookup, as in the textbook algorithm: each wave keeps a
+//    5 x 64-word LDS table (lane's ~Eq for A, C, G, T, and all ones for N) and
+//    reads one word per lane per text base with ds_read_addtid_b32, the
+//    address coming from M0 = 256 * character, two SALU ops from the
+//    wave-uniform 2-bit text held in an SGPR.  No VALU op per base for ~Eq.
+//  * The NFA runs in generated inline-asm blocks (wm_tid_blocks.inc,
+//    tools/gen_tid_blocks.py): 8 full-rate VALU ops per base (v_or, v_lshrrev,
+//    v_bitop3 -- the forms that issue in 2 cycles per wave64 on gfx950,
+//    profiles/r01_ubench_valu.txt) + 1.5 of hit accumulation (AND3 over two
+//    bases) = 9.5 VALU ops per base for P candidates, scheduled skewed (row 0
+//    of base s, row 1 of base s-1, row 2 of base s-2 per step) so a wave has
+//    three independent dependency chains, with the LDS reads three bases ahead.
+//  * One wave per workgroup, so the table sits at LDS address 0 and M0 needs no
+//    per-wave add: per base 2 SALU + 1 LDS + 9.5 VALU.  The SALU is the
+//    CU-shared resource the first table-driven version ran out of (5 SALU per
+//    base: no faster than computing ~Eq with 2 VALU ops; profiles/r01_kernel_log.md).
 //  * Integer-only VALU work: no MFMA.  Counts are uint32 atomics
 //    (order-independent, bit-exact).
 #include <hip/hip_runtime.h>
@@ -51,10 +49,7 @@
 namespace acamd {
 namespace {
 
-#ifndef AC_WAVES_PER_BLOCK
-#define AC_WAVES_PER_BLOCK 4
-#endif
-constexpr int WAVES_PER_BLOCK = AC_WAVES_PER_BLOCK;
+constexpr int WAVES_PER_BLOCK = 1;  // one wave per workgroup: its ~Eq table at LDS address 0
 #ifdef AC_STAMPS
 // Diagnostic build only (tools/variants.sh ... -DAC_STAMPS): per-wave
 // s_memrealtime stamps (100 MHz) at entry, after the prologue, after the last
@@ -82,120 +77,7 @@ __device__ __forceinline__ void stamp_val(uint64_t wave, int i, uint64_t v) {
 __device__ __forceinline__ void stamp(uint64_t, int) {}
 __device__ __forceinline__ void stamp_val(uint64_t, int, uint64_t) {}
 #endif
-constexpr int W = AC_WAVE_WORDS;
-constexpr uint32_t SEG = 256;  // window bases staged in LDS per pass (4 per lane)
-
-// Per-wave LDS staging of one window segment (3 KB).
-struct Stage {
-    uint4 hl[SEG / 2 + 1];  // (H, L) of bases 2q and 2q+1; one pad pair for the read-ahead past the end
-    uint32_t n[SEG];        // N mask of each base (0 or ~0)
-};
-
-// v_bitop3_b32 truth tables over (s0, s1, s2) = (0xf0, 0xcc, 0xaa).
-constexpr int NEQ = 0xf6;     // a | (b ^ c)      ~Eq from (ph ^ H, pl, L)
-constexpr int XOR_OR = 0xbe;  // (a ^ b) | c      ph ^ H with the N mask folded in
-constexpr int AND3 = 0x80;    // a & b & c
-constexpr int OR_AND = 0xa8;  // (a | b) & c
-template <int TT>
-__device__ __forceinline__ uint32_t bop3(uint32_t a, uint32_t b, uint32_t c) {
-    return __builtin_amdgcn_bitop3_b32(a, b, c, TT);
-}
-
-struct Nfa {
-    uint32_t d0[W], d1[W], d2[W];  // complemented rows
-    uint32_t s0[W], s1[W], s2[W];  // rows >> P
-    uint32_t a0[W], a1[W], a2[W];  // AND of the rows over the window
-};
-
-// One text base (masks H, L, N) for both words: 11 full-rate VALU ops per
-// word, 8 of them NFA.  ACC (odd bases): also AND this base's rows and the
-// previous base's (still in s.d*) into the hit accumulators (3 more ops per
-// word per two bases).
-template <int P, bool HAS_N, bool ACC>
-__device__ __forceinline__ void step(Nfa& s, const uint32_t (&ph)[W], const uint32_t (&pl)[W], uint32_t H,
-                                     uint32_t L, uint32_t N) {
-#pragma unroll
-    for (int w = 0; w < W; ++w) {
-        const uint32_t xh = HAS_N ? bop3<XOR_OR>(ph[w], H, N) : (ph[w] ^ H);
-        const uint32_t ne = bop3<NEQ>(xh, pl[w], L);
-        const uint32_t d0n = s.s0[w] | ne;
-        const uint32_t t0 = d0n >> P;
-        const uint32_t d1n = bop3<OR_AND>(s.s1[w], ne, bop3<AND3>(s.s0[w], s.d0[w], t0));
-        const uint32_t t1 = d1n >> P;
-        const uint32_t d2n = bop3<OR_AND>(s.s2[w], ne, bop3<AND3>(s.s1[w], s.d1[w], t1));
-        const uint32_t t2 = d2n >> P;
-        if (ACC) {
-            s.a0[w] = bop3<AND3>(s.a0[w], s.d0[w], d0n);
-            s.a1[w] = bop3<AND3>(s.a1[w], s.d1[w], d1n);
-            s.a2[w] = bop3<AND3>(s.a2[w], s.d2[w], d2n);
-        }
-        s.d0[w] = d0n;
-        s.d1[w] = d1n;
-        s.d2[w] = d2n;
-        s.s0[w] = t0;
-        s.s1[w] = t1;
-        s.s2[w] = t2;
-    }
-}
-
-// NB (even) staged bases from pair index q; the next pair is read one pair ahead.
-template <int P, int NB, bool HAS_N>
-__device__ __forceinline__ void run(Nfa& s, const uint32_t (&ph)[W], const uint32_t (&pl)[W],
-                                    const Stage& st, uint32_t q) {
-    uint4 cur = st.hl[q];
-#pragma unroll
-    for (int j = 0; j < NB; j += 2) {
-        const uint4 nxt = st.hl[q + j / 2 + 1];  // base + immediate offset (the pad pair absorbs the last read)
-        uint32_t n0 = 0, n1 = 0;
-        if constexpr (HAS_N) {
-            n0 = st.n[2 * (q + j / 2)];
-            n1 = st.n[2 * (q + j / 2) + 1];
-        }
-        step<P, HAS_N, false>(s, ph, pl, cur.x, cur.y, n0);
-        step<P, HAS_N, true>(s, ph, pl, cur.z, cur.w, n1);
-        cur = nxt;
-        // Keep the one-pair-ahead read in this pair's block: without the fence
-        // hipcc hoists the whole chunk's reads (32 VGPRs) and occupancy drops.
-        __builtin_amdgcn_sched_barrier(0);
-    }
-}
-
-template <int P, int NB>
-__device__ __forceinline__ void run_any(Nfa& s, const uint32_t (&ph)[W], const uint32_t (&pl)[W],
-                                        const Stage& st, uint32_t q, bool has_n) {
-    if (!has_n) run<P, NB, false>(s, ph, pl, st, q);
-    else run<P, NB, true>(s, ph, pl, st, q);
-}
-
-// Lane `lane`'s share of staging window bases [sb, sb + SEG): bases sb + 4*lane .. +3.
-struct Fetch {
-    uint32_t code;  // the code word holding the lane's 4 bases (0 past the window)
-    uint32_t nmw;   // the N-mask word holding them
-};
-
-__device__ __forceinline__ Fetch fetch(const uint32_t* __restrict__ codes, const uint32_t* __restrict__ nmask,
-                                       uint32_t len, uint32_t sb, uint32_t lane) {
-    const uint32_t b = sb + 4u * lane;
-    Fetch f = {0u, 0u};
-    if (b < len) {
-        f.code = codes[b >> 4];
-        f.nmw = nmask[b >> 5];
-    }
-    return f;
-}
-
-// Writes the lane's 4 bases into the stage; returns the wave's ballot of
-// "my 4 bases hold an N" (bit l = bases 4l..4l+3 of the segment).
-__device__ __forceinline__ uint64_t stage_write(Stage& st, const Fetch& f, uint32_t lane) {
-    const uint32_t sh = 8u * (lane & 3u);  // 2 bits per base, 4 bases per lane, 16 per code word
-    const uint32_t c = f.code >> sh;
-    auto sx = [](uint32_t v, int bit) { return (uint32_t)(-(int32_t)((v >> bit) & 1u)); };
-    st.hl[2 * lane] = make_uint4(sx(c, 1), sx(c, 0), sx(c, 3), sx(c, 2));
-    st.hl[2 * lane + 1] = make_uint4(sx(c, 5), sx(c, 4), sx(c, 7), sx(c, 6));
-    const uint32_t nb = (f.nmw >> (4u * (lane & 7u))) & 0xfu;
-    *reinterpret_cast<uint4*>(&st.n[4 * lane]) = make_uint4(sx(nb, 0), sx(nb, 1), sx(nb, 2), sx(nb, 3));
-    return __ballot(nb != 0u);
-}
+constexpr uint32_t SEG = 256;  // window bases fetched per pass (16 code words, 8 N-mask words)
 
 // 32-bit outer unshuffle (Hacker's Delight 7-2): odd bits to the upper half,
 // even bits to the lower half, order kept.
@@ -238,7 +120,6 @@ __device__ __forceinline__ void build_masks(const uint64_t (&km)[P], uint32_t m,
     }
 }
 
-#ifdef AC_TID
 #include "wm_tid_blocks.inc"
 
 // Per-wave ~Eq table: word c*64 + lane = the lane's ~Eq mask for character c
@@ -262,8 +143,8 @@ __device__ __forceinline__ uint32_t tid_fetch(const uint32_t* __restrict__ codes
     return *p;
 }
 
-// With one-wave workgroups the wave's table is the block's only LDS object, at
-// address 0, and M0 needs no per-base add (tools/gen_tid_blocks.py, eb0).
+// The wave's table is its workgroup's only LDS object, at address 0, so M0
+// needs no per-base add (the eb0 form of tools/gen_tid_blocks.py).
 constexpr bool TID_EB0 = WAVES_PER_BLOCK == 1;
 
 // The remainder (< 16 bases) of a segment: blocks of 8, 4, 2, 1 bases.
@@ -286,26 +167,11 @@ __device__ __forceinline__ void tid_tail(TidNfa& s, uint32_t code, uint32_t nm, 
     }
     if (rem & 1u) tid_block1<P, TID_EB0>(s, code, nm & 0x1u, eb);
 }
-using StageT = TidTable;
-using FetchT = uint32_t;
-__device__ __forceinline__ FetchT fetchw(const uint32_t* __restrict__ codes, const uint32_t* __restrict__ nmask,
-                                         uint32_t len, uint32_t sb, uint32_t lane) {
-    return tid_fetch(codes, nmask, len, sb, lane);
-}
-#else
-using StageT = Stage;
-using FetchT = Fetch;
-__device__ __forceinline__ FetchT fetchw(const uint32_t* __restrict__ codes, const uint32_t* __restrict__ nmask,
-                                         uint32_t len, uint32_t sb, uint32_t lane) {
-    return fetch(codes, nmask, len, sb, lane);
-}
-#endif
 
 template <int P>
-__device__ __forceinline__ void count_body(const LaunchArgs& a, StageT& st) {
+__device__ __forceinline__ void count_body(const LaunchArgs& a, TidTable& st) {
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint64_t wave = (uint64_t)blockIdx.x * WAVES_PER_BLOCK + wib;
+    const uint64_t wave = blockIdx.x;  // one wave per workgroup
     if (wave >= a.total_waves) return;
     stamp(wave, 0);
 
@@ -322,27 +188,26 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, StageT& st) {
     const uint32_t g = ql % sg.groups, j = ql / sg.groups;
     const uint32_t m = a.m;
 
-    // Lane constants: character i of pattern p of word w at bit 31 - (i*P + p).
-    uint32_t ph[W], pl[W], cand[W][P];
+    // Lane constants: character i of pattern p at bit 31 - (i*P + p).
+    uint32_t ph, pl, cand[P];
     uint32_t first = 0;
 #pragma unroll
     for (int p = 0; p < P; ++p) first |= 1u << (31 - p);
-#pragma unroll
-    for (int w = 0; w < W; ++w) {
+    {
         uint64_t km[P];
 #pragma unroll
         for (int p = 0; p < P; ++p) {
-            cand[w][p] = g * (64u * P * W) + (uint32_t)(w * P + p) * 64u + lane;
-            km[p] = cand[w][p] < sg.n_kmers ? sg.kmers[cand[w][p]] : 0ull;
+            cand[p] = g * (64u * P) + (uint32_t)p * 64u + lane;
+            km[p] = cand[p] < sg.n_kmers ? sg.kmers[cand[p]] : 0ull;
         }
-        build_masks<P>(km, m, ph[w], pl[w]);
+        build_masks<P>(km, m, ph, pl);
     }
     // Initial rows (empty text): R1 has character 0 set, R2 characters 0 and 1.
     const uint32_t d1_init = ~first, d2_init = ~(first | (first >> P));
-#ifdef AC_TID
-    static_assert(W == 1, "the table-driven loop runs one lane word");
+    // ~Eq table: ~Eq_c = (ph ^ H_c) | (pl ^ L_c), H_c / L_c = all ones where
+    // character c's high / low code bit is set; N matches nothing.
 #pragma unroll
-    for (int c = 0; c < 4; ++c) st.e[c * 64 + lane] = ((c & 2) ? ~ph[0] : ph[0]) | ((c & 1) ? ~pl[0] : pl[0]);
+    for (int c = 0; c < 4; ++c) st.e[c * 64 + lane] = ((c & 2) ? ~ph : ph) | ((c & 1) ? ~pl : pl);
     st.e[4 * 64 + lane] = ~0u;
     const uint32_t eb = __builtin_amdgcn_readfirstlane(
         (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)(&st.e[0]));
@@ -350,13 +215,10 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, StageT& st) {
     // it were, the wave stops (no fault) and the counts come out short, which
     // the parity tests catch.
     if (TID_EB0 && eb != 0u) return;
-#endif
 
-    uint32_t cnt[W][P];
+    uint32_t cnt[P];
 #pragma unroll
-    for (int w = 0; w < W; ++w)
-#pragma unroll
-        for (int p = 0; p < P; ++p) cnt[w][p] = 0;
+    for (int p = 0; p < P; ++p) cnt[p] = 0;
 
     stamp(wave, 1);
 
@@ -433,23 +295,19 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, StageT& st) {
     auto valid = [&](uint64_t base, uint32_t len) { return !(base & 31u) && base + len <= sg.n_bases; };
     uint64_t nbase = 0;
     uint32_t nlen = 0;
-    FetchT nf{};
+    uint32_t nf = 0;
     if (item < n_items) {
         nbase = sg.start[w];
         nlen = sg.length[w];
-        if (valid(nbase, nlen)) nf = fetchw(sg.codes + (nbase >> 4), sg.nmask + (nbase >> 5), nlen, 0, lane);
+        if (valid(nbase, nlen)) nf = tid_fetch(sg.codes + (nbase >> 4), sg.nmask + (nbase >> 5), nlen, 0, lane);
     }
     while (item < n_items) {
         const uint64_t base = nbase;
         const uint32_t len = nlen;
-#ifdef AC_TID
         // Wait for this window's words here, before the next window's fetch is
         // issued: inside the chunk loop hipcc would otherwise wait for both.
-        FetchT f0 = nf;
+        uint32_t f0 = nf;
         asm volatile("" : "+v"(f0));
-#else
-        const FetchT f0 = nf;
-#endif
         // Within an item the next window is fetched while this one is counted.
         // During an item's last window the next item is claimed (one returning
         // atomic); it is read after the window, so a wave the arbiter starves
@@ -458,14 +316,13 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, StageT& st) {
         if (wn < item_end) {
             nbase = sg.start[wn];
             nlen = sg.length[wn];
-            if (valid(nbase, nlen)) nf = fetchw(sg.codes + (nbase >> 4), sg.nmask + (nbase >> 5), nlen, 0, lane);
+            if (valid(nbase, nlen)) nf = tid_fetch(sg.codes + (nbase >> 4), sg.nmask + (nbase >> 5), nlen, 0, lane);
         } else {
             pending = dequeue_issue();
         }
         if (valid(base, len)) {  // a malformed window is skipped: never read outside the image
         const uint32_t* __restrict__ codes = sg.codes + (base >> 4);
         const uint32_t* __restrict__ nmask = sg.nmask + (base >> 5);
-#ifdef AC_TID
         TidNfa s = {~0u, d1_init, d2_init, ~0u >> P, d1_init >> P, d2_init >> P, ~0u, d1_init, d2_init};
         auto segment = [&](uint32_t f, uint32_t sb) {
             const uint32_t nb = min(SEG, len - sb);
@@ -490,69 +347,8 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, StageT& st) {
 #pragma unroll
         for (int p = 0; p < P; ++p) {
             const uint32_t lb = 31u - ((m - 1u) * P + (uint32_t)p);
-            cnt[0][p] += 3u - ((s.a0 >> lb) & 1u) - ((s.a1 >> lb) & 1u) - ((s.a2 >> lb) & 1u);
+            cnt[p] += 3u - ((s.a0 >> lb) & 1u) - ((s.a1 >> lb) & 1u) - ((s.a2 >> lb) & 1u);
         }
-#else
-        Nfa s;
-#pragma unroll
-        for (int x = 0; x < W; ++x) {
-            s.d0[x] = ~0u;
-            s.d1[x] = d1_init;
-            s.d2[x] = d2_init;
-            s.s0[x] = ~0u >> P;
-            s.s1[x] = d1_init >> P;
-            s.s2[x] = d2_init >> P;
-            s.a0[x] = ~0u;
-            s.a1[x] = d1_init;
-            s.a2[x] = d2_init;  // for k <= 2 the empty alignment already reaches the last character
-        }
-        for (uint32_t sb = 0; sb < len; sb += SEG) {
-            const Fetch f = sb == 0 ? f0 : fetch(codes, nmask, len, sb, lane);
-            const uint64_t any_n = stage_write(st, f, lane);
-            const uint32_t nb = min(SEG, len - sb);
-            const uint32_t nfull = nb >> 4;
-            for (uint32_t ch = 0; ch < nfull; ++ch)
-                run_any<P, 16>(s, ph, pl, st, ch * 8u, ((any_n >> (4u * ch)) & 0xfu) != 0u);
-            const uint32_t rem = nb & 15u;
-            if (rem) {
-                uint32_t o = nfull * 16u;  // base offset in the segment
-                const uint32_t fl = (uint32_t)(any_n >> (o >> 2)) & 0xfu;  // 4-base groups o/4 .. o/4+3
-                uint32_t gi = 0;                                        // group index within fl
-                if (rem & 8u) {
-                    run_any<P, 8>(s, ph, pl, st, o / 2, (fl & 3u) != 0u);
-                    o += 8u;
-                    gi += 2u;
-                }
-                if (rem & 4u) {
-                    run_any<P, 4>(s, ph, pl, st, o / 2, ((fl >> gi) & 1u) != 0u);
-                    o += 4u;
-                    gi += 1u;
-                }
-                if (rem & 2u) {
-                    run_any<P, 2>(s, ph, pl, st, o / 2, ((fl >> gi) & 1u) != 0u);
-                    o += 2u;
-                }
-                if (rem & 1u) {
-                    const uint4 mm = st.hl[o / 2];
-                    step<P, true, false>(s, ph, pl, mm.x, mm.y, st.n[o]);
-#pragma unroll
-                    for (int x = 0; x < W; ++x) {
-                        s.a0[x] &= s.d0[x];
-                        s.a1[x] &= s.d1[x];
-                        s.a2[x] &= s.d2[x];
-                    }
-                }
-            }
-        }
-#pragma unroll
-        for (int x = 0; x < W; ++x) {
-#pragma unroll
-            for (int p = 0; p < P; ++p) {
-                const uint32_t lb = 31u - ((m - 1u) * P + (uint32_t)p);
-                cnt[x][p] += 3u - ((s.a0[x] >> lb) & 1u) - ((s.a1[x] >> lb) & 1u) - ((s.a2[x] >> lb) & 1u);
-            }
-        }
-#endif
         }  // valid window
         // advance the cursor; at an item boundary move to the prefetched item and request another
         if (++w >= item_end) {
@@ -563,7 +359,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, StageT& st) {
                 item_end = min(sg.n_windows, w + chunk);
                 nbase = sg.start[w];
                 nlen = sg.length[w];
-                if (valid(nbase, nlen)) nf = fetchw(sg.codes + (nbase >> 4), sg.nmask + (nbase >> 5), nlen, 0, lane);
+                if (valid(nbase, nlen)) nf = tid_fetch(sg.codes + (nbase >> 4), sg.nmask + (nbase >> 5), nlen, 0, lane);
             }
         }
     }
@@ -571,13 +367,11 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, StageT& st) {
     stamp(wave, 2);
     stamp_val(wave, 6, ((uint64_t)si << 32) | ((uint64_t)g << 16) | j);
 #pragma unroll
-    for (int x = 0; x < W; ++x)
-#pragma unroll
-        for (int p = 0; p < P; ++p)
+    for (int p = 0; p < P; ++p)
 #ifdef AC_TIMING_NO_ATOMICS  // timing-only build: results discarded (kept live by an impossible store)
-            if (cand[x][p] < sg.n_kmers && cnt[x][p] == 0xdeadbeefu) sg.counts[cand[x][p]] = 1u;
+        if (cand[p] < sg.n_kmers && cnt[p] == 0xdeadbeefu) sg.counts[cand[p]] = 1u;
 #else
-            if (cand[x][p] < sg.n_kmers && cnt[x][p]) atomicAdd(&sg.counts[cand[x][p]], cnt[x][p]);
+        if (cand[p] < sg.n_kmers && cnt[p]) atomicAdd(&sg.counts[cand[p]], cnt[p]);
 #endif
     stamp(wave, 3);
 }
@@ -585,12 +379,11 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, StageT& st) {
 }  // namespace
 
 template <int P>
-__global__ __launch_bounds__(64 * WAVES_PER_BLOCK, AC_MIN_WAVES_PER_SIMD) void wm2_count_kernel(LaunchArgs a) {
-    // The LDS allocation also caps residency at AC_BLOCKS_PER_CU blocks (6 waves
-    // per SIMD): measured faster than 8 (fewer waves starved by the oldest-first
-    // VALU arbitration; profiles/r01_kernel_log.md).
-    __shared__ StageT stage[(160 * 1024 / AC_BLOCKS_PER_CU) / sizeof(StageT)];
-    count_body<P>(a, stage[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)]);
+__global__ __launch_bounds__(64 * WAVES_PER_BLOCK, AC_WAVES_PER_SIMD) void wm2_count_kernel(LaunchArgs a) {
+    // The LDS allocation also caps residency at AC_WAVES_PER_SIMD waves per
+    // SIMD (8: faster than 6 or 10, profiles/r01_kernel_log.md).
+    __shared__ TidTable stage[(160 * 1024 / (4 * AC_WAVES_PER_SIMD)) / sizeof(TidTable)];
+    count_body<P>(a, stage[0]);
 }
 
 namespace {

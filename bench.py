@@ -17,8 +17,10 @@ count launch of step i+1 (two count buffers, async_op).  Rank 0 prints ONE JSON 
 Roofline: the count kernel is bound by integer VALU
 issue, not HBM and not MFMA.  `roofline.achieved` = algorithmic VALU lane-ops
 per launch / mean kernel duration (HIP events around each launch, on the
-launch stream, inside the timed loop); algorithmic work = 11.5 full-rate lane
-ops per text base per lane word of P candidates (P = 2 at k=16, 1 at k=22);
+launch stream, inside the timed loop); algorithmic work = 9.5 full-rate lane
+ops per text base per lane word of P candidates (P = 2 at k=16, 1 at k=22):
+the 8 ops of the Wu-Manber NFA for 3 rows + 1.5 of hit accumulation, with ~Eq
+a table lookup as in the textbook algorithm;
 `peak` = 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (MI355X_MICROARCH.md: SIMD-32,
 2-cycle wave64 VALU issue).  `traffic` = HBM bytes per launch from the
 committed rocprofv3 PMC passes (profiles/*_pmc_traffic.json) for the same
@@ -42,7 +44,7 @@ sys.path.insert(0, ROOT)
 METRIC = "approx-count kmer×base pairs/sec (k=16, lim=500, 10k×100bp ends)"
 VALU_PEAK_OPS = 256 * 4 * 32 * 2.4e9       # int32 lane-ops/s (2-cycle wave64 issue per SIMD-32)
 HBM_PEAK = 8.0e12                           # B/s (MI355X_MICROARCH.md, spec)
-OPS_PER_BASE_WORD = 11.5                    # 2 ~Eq + 8 NFA + 1.5 hit accumulation
+OPS_PER_BASE_WORD = 9.5                     # 8 NFA + 1.5 hit accumulation (~Eq: LDS table)
 SAMPLE_BYTES_PER_BASE = 0.375               # 2-bit code + 1-bit N mask, read once
 
 CONFIGS = {  # BASELINE.json configs (sn per rank for the bench)
