@@ -135,8 +135,9 @@ ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hi
     // windows, so the launch tail is about one window; up to 8 when they get
     // hundreds, for fewer atomics), each candidate group's items spread over
     // sub-queues of about 64 waves.  A segment gets sub-queues in proportion
-    // to its windows, so every sub-queue holds about the same work, and wave
-    // i serves sub-queue i mod n_queues.
+    // to its windows, so every sub-queue holds about the same work.  Workgroups
+    // of AC_WAVES_PER_BLOCK waves are dealt round-robin over blocks of that many
+    // consecutive sub-queues (one candidate group each).
     if (!ctx->resident[P]) AC_HIP(ctx, acamd::resident_waves(P, ctx->cu_count, &ctx->resident[P]));
     const uint64_t resident = ctx->resident[P];
     const uint32_t wpw = (uint32_t)std::max<uint64_t>(1, (items + resident - 1) / resident);
@@ -164,7 +165,10 @@ ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hi
         d.n_windows = s.sample.n_windows;
         d.groups = std::max<uint32_t>(1, (s.n_kmers + cpw - 1) / cpw);
         d.chunk = chunk;
-        d.subq = (uint32_t)std::max<uint64_t>(1, (s_base * s.sample.n_windows + max_nw / 2) / max_nw);
+        {  // a multiple of the workgroup size: a workgroup's waves take consecutive sub-queues of one group
+            const uint64_t sq = std::max<uint64_t>(1, (s_base * s.sample.n_windows + max_nw / 2) / max_nw);
+            d.subq = (uint32_t)((sq + AC_WAVES_PER_BLOCK - 1) / AC_WAVES_PER_BLOCK * AC_WAVES_PER_BLOCK);
+        }
         d.queue_begin = qbegin;
         if (s.n_kmers && s.sample.n_windows) {
             qbegin += d.groups * d.subq;

@@ -6,6 +6,9 @@
 #define AC_MAX_SEGS 4    // segments fused into one launch (start + end ends, shards)
 #define AC_QUEUE_LINE 32  // u32 per queue counter: one 128-B line each (no false sharing between counters)
 #define AC_MAX_PACK 4    // candidates interleaved per 32-bit lane word (P = min(32/k, 4))
+#ifndef AC_WAVES_PER_BLOCK
+#define AC_WAVES_PER_BLOCK 4  // waves per workgroup, all on one candidate group (shared ~Eq table, counts summed in LDS)
+#endif
 #ifndef AC_WAVES_PER_SIMD
 #define AC_WAVES_PER_SIMD 8  // resident count-kernel waves per SIMD, set by the LDS allocation (<= 64 VGPRs)
 #endif
@@ -25,7 +28,7 @@ struct SegDev {
     uint32_t groups;      // candidate groups of cands_per_wave(P) candidates
     uint32_t chunk;       // windows per work item of the dynamic queues
     uint32_t queue_begin; // index of this segment's first sub-queue (groups x subq of them)
-    uint32_t subq;        // sub-queues per candidate group (proportional to n_windows)
+    uint32_t subq;        // sub-queues per candidate group (proportional to n_windows; a multiple of AC_WAVES_PER_BLOCK)
 };
 
 struct LaunchArgs {
@@ -39,7 +42,8 @@ struct LaunchArgs {
     uint32_t qstride;
     uint32_t bank;
     uint32_t zero_count;
-    uint32_t n_queues;  // sub-queues over all segments; wave i serves sub-queue i % n_queues
+    uint32_t n_queues;  // sub-queues over all segments (a multiple of AC_WAVES_PER_BLOCK); wave w of
+                        // workgroup b serves sub-queue (b % (n_queues / AC_WAVES_PER_BLOCK)) * AC_WAVES_PER_BLOCK + w
     uint32_t n_segs;
     uint32_t m;  // k-mer length
     uint32_t P;  // candidates per lane word

@@ -49,7 +49,7 @@
 namespace acamd {
 namespace {
 
-constexpr int WAVES_PER_BLOCK = 1;  // one wave per workgroup: its ~Eq table at LDS address 0
+constexpr int WAVES_PER_BLOCK = AC_WAVES_PER_BLOCK;
 #ifdef AC_STAMPS
 // Diagnostic build only (tools/variants.sh ... -DAC_STAMPS): per-wave
 // s_memrealtime stamps (100 MHz) at entry, after the prologue, after the last
@@ -143,9 +143,16 @@ __device__ __forceinline__ uint32_t tid_fetch(const uint32_t* __restrict__ codes
     return *p;
 }
 
-// The wave's table is its workgroup's only LDS object, at address 0, so M0
-// needs no per-base add (the eb0 form of tools/gen_tid_blocks.py).
-constexpr bool TID_EB0 = WAVES_PER_BLOCK == 1;
+// The workgroup's waves serve one candidate group and share one table, the
+// first LDS object, at address 0, so M0 needs no per-base add (the eb0 form of
+// tools/gen_tid_blocks.py).
+constexpr bool TID_EB0 = true;
+
+// Workgroup LDS: the ~Eq table, then the count vector the waves sum into.
+struct BlockLds {
+    TidTable tab;
+    uint32_t cnt[AC_MAX_PACK * 64];
+};
 
 // The remainder (< 16 bases) of a segment: blocks of 8, 4, 2, 1 bases.
 template <int P>
@@ -169,23 +176,29 @@ __device__ __forceinline__ void tid_tail(TidNfa& s, uint32_t code, uint32_t nm, 
 }
 
 template <int P>
-__device__ __forceinline__ void count_body(const LaunchArgs& a, TidTable& st) {
+__device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
     const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t wave = blockIdx.x;  // one wave per workgroup
-    if (wave >= a.total_waves) return;
+    // Workgroup b serves block-queue b mod nqb (all its waves on one candidate
+    // group); its waves take the block-queue's AC_WAVES_PER_BLOCK sub-queues.
+    const uint32_t wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t wave = (uint64_t)blockIdx.x * WAVES_PER_BLOCK + wib;
     stamp(wave, 0);
+    const uint32_t nqb = a.n_queues / WAVES_PER_BLOCK;
+    const uint32_t blocks = (uint32_t)(a.total_waves / WAVES_PER_BLOCK);
 
-    // Wave -> sub-queue q = wave mod n_queues, so every sub-queue is served by
-    // waves of every dispatch age (see the work-queue comment below); q ->
-    // (segment, candidate group g, sub-queue j of that group).
-    const uint32_t q = (uint32_t)(wave % a.n_queues), rank = (uint32_t)(wave / a.n_queues);
+    // Workgroups are dealt round-robin over the block-queues, so every
+    // sub-queue is served by waves of every dispatch age (see the work-queue
+    // comment below); q -> (segment, candidate group g, sub-queue j of that group).
+    const uint32_t q = (blockIdx.x % nqb) * WAVES_PER_BLOCK + wib, rank = blockIdx.x / nqb;
     int si = 0;
 #pragma unroll
     for (int i = 1; i < AC_MAX_SEGS; ++i)
         if (i < (int)a.n_segs && q >= a.seg[i].queue_begin) si = i;
     const SegDev& sg = a.seg[si];
     const uint32_t ql = q - sg.queue_begin;
-    const uint32_t g = ql % sg.groups, j = ql / sg.groups;
+    // A group's sub-queues are contiguous (g * subq + j), so a workgroup's
+    // sub-queues lie in one group.
+    const uint32_t g = ql / sg.subq, j = ql % sg.subq;
     const uint32_t m = a.m;
 
     // Lane constants: character i of pattern p at bit 31 - (i*P + p).
@@ -206,15 +219,23 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, TidTable& st) {
     const uint32_t d1_init = ~first, d2_init = ~(first | (first >> P));
     // ~Eq table: ~Eq_c = (ph ^ H_c) | (pl ^ L_c), H_c / L_c = all ones where
     // character c's high / low code bit is set; N matches nothing.
+    // Every wave of the workgroup writes the same table (same candidates), so a
+    // wave's own writes precede its reads and no barrier is needed for it; the
+    // barrier below orders the zeroed count vector before any wave adds to it.
 #pragma unroll
-    for (int c = 0; c < 4; ++c) st.e[c * 64 + lane] = ((c & 2) ? ~ph : ph) | ((c & 1) ? ~pl : pl);
-    st.e[4 * 64 + lane] = ~0u;
+    for (int c = 0; c < 4; ++c) lds.tab.e[c * 64 + lane] = ((c & 2) ? ~ph : ph) | ((c & 1) ? ~pl : pl);
+    lds.tab.e[4 * 64 + lane] = ~0u;
+    if (wib == 0) {
+#pragma unroll
+        for (int p = 0; p < P; ++p) lds.cnt[p * 64 + lane] = 0u;
+    }
+    __syncthreads();
     const uint32_t eb = __builtin_amdgcn_readfirstlane(
-        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)(&st.e[0]));
-    // The eb0 blocks address the table from LDS 0.  Never expected otherwise; if
-    // it were, the wave stops (no fault) and the counts come out short, which
-    // the parity tests catch.
-    if (TID_EB0 && eb != 0u) return;
+        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)(&lds.tab.e[0]));
+    // The eb0 blocks address the table from LDS 0.  Never expected otherwise;
+    // if it were, the waves skip the work (no fault) and the counts come out
+    // short, which the parity tests catch.
+    const bool eb_ok = !TID_EB0 || eb == 0u;
 
     uint32_t cnt[P];
 #pragma unroll
@@ -247,11 +268,12 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, TidTable& st) {
     const uint32_t n_items = (sg.n_windows + chunk - 1u) / chunk;
     uint32_t jc = j;  // sub-queue currently served
     auto counter = [&](uint32_t jj) {
-        return a.queue + ((uint64_t)a.bank * a.qstride + sg.queue_begin + g + jj * sg.groups) * AC_QUEUE_LINE;
+        return a.queue + ((uint64_t)a.bank * a.qstride + sg.queue_begin + g * sg.subq + jj) * AC_QUEUE_LINE;
     };
     auto waves_in = [&](uint32_t jj) {  // waves dealt to sub-queue (g, jj): their first items are static
-        const uint32_t qq = sg.queue_begin + g + jj * sg.groups;
-        return (uint32_t)(a.total_waves / a.n_queues) + (qq < a.total_waves % a.n_queues ? 1u : 0u);
+        const uint32_t qq = sg.queue_begin + g * sg.subq + jj;
+        const uint32_t qb = qq / WAVES_PER_BLOCK;  // one wave of every workgroup dealt to block-queue qb
+        return blocks / nqb + (qb < blocks % nqb ? 1u : 0u);
     };
     auto n_in = [&](uint32_t jj) { return jj < n_items ? (n_items - jj + S - 1u) / S : 0u; };  // items of jj
     auto item_of = [&](uint32_t c) { return c < n_in(jc) ? jc + c * S : n_items; };
@@ -287,7 +309,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, TidTable& st) {
             if (c < n_in(jj)) return jj + c * S;
         }
     };
-    uint32_t item = j < n_items ? item_of(rank) : n_items;
+    uint32_t item = (j < n_items && eb_ok) ? item_of(rank) : n_items;
     uint32_t pending = 0;
     uint32_t w = item * chunk, item_end = min(sg.n_windows, w + chunk);
 
@@ -366,13 +388,25 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, TidTable& st) {
 
     stamp(wave, 2);
     stamp_val(wave, 6, ((uint64_t)si << 32) | ((uint64_t)g << 16) | j);
+    // The workgroup's waves sum their counts in LDS; one wave adds the sums to
+    // the global vector, so each counter takes 1/AC_WAVES_PER_BLOCK of the
+    // same-address atomics (they serialise at the L2: ~10 us of launch tail at
+    // cfg2 with one atomic per wave; profiles/r01_kernel_log.md).
 #pragma unroll
     for (int p = 0; p < P; ++p)
+        if (cnt[p]) __hip_atomic_fetch_add(&lds.cnt[p * 64 + lane], cnt[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __syncthreads();
+    if (wib == 0) {
+#pragma unroll
+        for (int p = 0; p < P; ++p) {
+            const uint32_t v = lds.cnt[p * 64 + lane];
 #ifdef AC_TIMING_NO_ATOMICS  // timing-only build: results discarded (kept live by an impossible store)
-        if (cand[p] < sg.n_kmers && cnt[p] == 0xdeadbeefu) sg.counts[cand[p]] = 1u;
+            if (cand[p] < sg.n_kmers && v == 0xdeadbeefu) sg.counts[cand[p]] = 1u;
 #else
-        if (cand[p] < sg.n_kmers && cnt[p]) atomicAdd(&sg.counts[cand[p]], cnt[p]);
+            if (cand[p] < sg.n_kmers && v) atomicAdd(&sg.counts[cand[p]], v);
 #endif
+        }
+    }
     stamp(wave, 3);
 }
 
@@ -382,8 +416,9 @@ template <int P>
 __global__ __launch_bounds__(64 * WAVES_PER_BLOCK, AC_WAVES_PER_SIMD) void wm2_count_kernel(LaunchArgs a) {
     // The LDS allocation also caps residency at AC_WAVES_PER_SIMD waves per
     // SIMD (8: faster than 6 or 10, profiles/r01_kernel_log.md).
-    __shared__ TidTable stage[(160 * 1024 / (4 * AC_WAVES_PER_SIMD)) / sizeof(TidTable)];
-    count_body<P>(a, stage[0]);
+    constexpr int kBlocksPerCu = 4 * AC_WAVES_PER_SIMD / WAVES_PER_BLOCK;
+    __shared__ BlockLds lds[(160 * 1024 / kBlocksPerCu) / sizeof(BlockLds)];
+    count_body<P>(a, lds[0]);
 }
 
 namespace {
