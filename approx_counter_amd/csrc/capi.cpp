@@ -37,6 +37,10 @@ struct ac_ctx {
     // counters of bank b used by the last launch on it (zeroed by the next launch)
     uint32_t* queue = nullptr;
     uint32_t qcap = 0, bank = 0, dirty[2] = {0, 0};
+    // count hand-off scratch: per-group sums and tickets (zero between launches)
+    uint32_t* acc = nullptr;
+    uint32_t* tickets = nullptr;
+    uint32_t acc_cap = 0, ticket_cap = 0;
     // resident waves of the count kernel per pattern pack P (0 = not queried yet)
     uint32_t resident[AC_MAX_PACK + 1] = {0, 0, 0, 0, 0};
     // last launch geometry
@@ -150,7 +154,7 @@ ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hi
         }
     const uint64_t s_base = std::max<uint64_t>(1, std::min<uint64_t>(32, resident / (64ull * std::max(1u, groups_live))));
     uint64_t wave = 0;
-    uint32_t groups_total = 0, qbegin = 0;
+    uint32_t groups_total = 0, qbegin = 0, acc_slots = 0;
     for (uint32_t i = 0; i < n; ++i) {
         const ac_segment& s = segs[i];
         acamd::SegDev& d = a.seg[i];
@@ -170,14 +174,52 @@ ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hi
             d.subq = (uint32_t)((sq + AC_WAVES_PER_BLOCK - 1) / AC_WAVES_PER_BLOCK * AC_WAVES_PER_BLOCK);
         }
         d.queue_begin = qbegin;
+        d.acc_begin = acc_slots;
+        d.ticket_begin = groups_total;
         if (s.n_kmers && s.sample.n_windows) {
             qbegin += d.groups * d.subq;
+            acc_slots += d.groups * cpw;
             groups_total += d.groups;
         } else {
             d.queue_begin = ~0u;  // never selected by the kernel's segment lookup
+            // no workgroup writes this segment's counts
+            if (zero && s.n_kmers) AC_HIP(ctx, hipMemsetAsync(s.counts, 0, sizeof(uint32_t) * s.n_kmers, stream));
         }
-        if (zero && s.n_kmers) AC_HIP(ctx, hipMemsetAsync(s.counts, 0, sizeof(uint32_t) * s.n_kmers, stream));
     }
+    // The group's last workgroup stores its counts (no memset), unless live
+    // segments share count slots (window shards of one candidate set): then
+    // zero them once and let every group add.
+    bool alias = false;
+    for (uint32_t i = 0; i < n && !alias; ++i)
+        for (uint32_t j = i + 1; j < n && !alias; ++j) {
+            const acamd::SegDev &x = a.seg[i], &y = a.seg[j];
+            if (x.queue_begin == ~0u || y.queue_begin == ~0u) continue;
+            alias = x.counts < y.counts + y.n_kmers && y.counts < x.counts + x.n_kmers;
+        }
+    a.add_counts = (!zero || alias) ? 1u : 0u;
+    if (zero && alias)
+        for (uint32_t i = 0; i < n; ++i)
+            if (a.seg[i].queue_begin != ~0u)
+                AC_HIP(ctx, hipMemsetAsync(a.seg[i].counts, 0, sizeof(uint32_t) * a.seg[i].n_kmers, stream));
+    if (acc_slots > ctx->acc_cap) {
+        if (ctx->acc) AC_HIP(ctx, hipFree(ctx->acc));
+        ctx->acc = nullptr;
+        ctx->acc_cap = 0;
+        AC_HIP(ctx, hipMalloc(&ctx->acc, sizeof(uint32_t) * acc_slots));
+        AC_HIP(ctx, hipMemsetAsync(ctx->acc, 0, sizeof(uint32_t) * acc_slots, stream));
+        ctx->acc_cap = acc_slots;
+    }
+    if (groups_total > ctx->ticket_cap) {
+        if (ctx->tickets) AC_HIP(ctx, hipFree(ctx->tickets));
+        ctx->tickets = nullptr;
+        ctx->ticket_cap = 0;
+        const size_t bytes = sizeof(uint32_t) * AC_QUEUE_LINE * (size_t)groups_total;
+        AC_HIP(ctx, hipMalloc(&ctx->tickets, bytes));
+        AC_HIP(ctx, hipMemsetAsync(ctx->tickets, 0, bytes, stream));
+        ctx->ticket_cap = groups_total;
+    }
+    a.acc = ctx->acc;
+    a.tickets = ctx->tickets;
     const uint32_t n_counters = qbegin;
     if (n_counters) wave = std::max<uint64_t>(resident, n_counters);
     if (n_counters > ctx->qcap) {
@@ -259,6 +301,8 @@ void ac_destroy(ac_ctx* ctx) {
     for (void* p : ctx->d_buf)
         if (p) (void)hipFree(p);
     if (ctx->queue) (void)hipFree(ctx->queue);
+    if (ctx->acc) (void)hipFree(ctx->acc);
+    if (ctx->tickets) (void)hipFree(ctx->tickets);
     for (void* p : ctx->s_buf)
         if (p) (void)hipFree(p);
     for (void* p : ctx->e_buf)

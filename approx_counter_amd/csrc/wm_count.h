@@ -29,6 +29,8 @@ struct SegDev {
     uint32_t chunk;       // windows per work item of the dynamic queues
     uint32_t queue_begin; // index of this segment's first sub-queue (groups x subq of them)
     uint32_t subq;        // sub-queues per candidate group (proportional to n_windows; a multiple of AC_WAVES_PER_BLOCK)
+    uint32_t acc_begin;   // this segment's first slot in LaunchArgs::acc (groups x cands_per_wave slots)
+    uint32_t ticket_begin;  // this segment's first group ticket in LaunchArgs::tickets
 };
 
 struct LaunchArgs {
@@ -44,6 +46,14 @@ struct LaunchArgs {
     uint32_t zero_count;
     uint32_t n_queues;  // sub-queues over all segments (a multiple of AC_WAVES_PER_BLOCK); wave w of
                         // workgroup b serves sub-queue (b % (n_queues / AC_WAVES_PER_BLOCK)) * AC_WAVES_PER_BLOCK + w
+    // Count hand-off: workgroups add their sums into `acc` and
+    // take a ticket of their candidate group; the group's last workgroup moves
+    // the group's sums to the segment's counts (stored, or added when
+    // `add_counts`) and zeroes its acc slots and ticket for the next launch, so
+    // a launch needs no memset of the counts.
+    uint32_t* acc;
+    uint32_t* tickets;  // one per AC_QUEUE_LINE u32
+    uint32_t add_counts;
     uint32_t n_segs;
     uint32_t m;  // k-mer length
     uint32_t P;  // candidates per lane word

@@ -389,22 +389,47 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
     stamp(wave, 2);
     stamp_val(wave, 6, ((uint64_t)si << 32) | ((uint64_t)g << 16) | j);
     // The workgroup's waves sum their counts in LDS; one wave adds the sums to
-    // the global vector, so each counter takes 1/AC_WAVES_PER_BLOCK of the
+    // the group's slots in `acc`, so each slot takes 1/AC_WAVES_PER_BLOCK of the
     // same-address atomics (they serialise at the L2: ~10 us of launch tail at
-    // cfg2 with one atomic per wave; profiles/r01_kernel_log.md).
+    // cfg2 with one atomic per wave; profiles/r01_kernel_log.md).  Then the
+    // group's last workgroup (ticket) moves the sums to the counts.
 #pragma unroll
     for (int p = 0; p < P; ++p)
         if (cnt[p]) __hip_atomic_fetch_add(&lds.cnt[p * 64 + lane], cnt[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     __syncthreads();
     if (wib == 0) {
+        uint32_t* acc = a.acc + sg.acc_begin + g * (64u * P);
 #pragma unroll
         for (int p = 0; p < P; ++p) {
             const uint32_t v = lds.cnt[p * 64 + lane];
 #ifdef AC_TIMING_NO_ATOMICS  // timing-only build: results discarded (kept live by an impossible store)
-            if (cand[p] < sg.n_kmers && v == 0xdeadbeefu) sg.counts[cand[p]] = 1u;
+            if (v == 0xdeadbeefu) acc[p * 64 + lane] = 1u;
 #else
-            if (cand[p] < sg.n_kmers && v) atomicAdd(&sg.counts[cand[p]], v);
+            if (v) __hip_atomic_fetch_add(&acc[p * 64 + lane], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #endif
+        }
+        // Workgroups serving group g: those dealt to its subq / WPB block-queues.
+        const uint32_t qb0 = (sg.queue_begin + g * sg.subq) / WAVES_PER_BLOCK, nq = sg.subq / WAVES_PER_BLOCK;
+        const uint32_t rem = blocks % nqb;
+        const uint32_t n_wg = nq * (blocks / nqb) + (rem > qb0 ? min(rem - qb0, nq) : 0u);
+        uint32_t* ticket = a.tickets + (uint64_t)(sg.ticket_begin + g) * AC_QUEUE_LINE;
+        uint32_t t = 0;
+        if (lane == 0) t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        t = __builtin_amdgcn_readfirstlane(t);
+        if (t == n_wg - 1u) {  // every other workgroup of the group has added its sums
+            __atomic_thread_fence(__ATOMIC_ACQUIRE);
+#pragma unroll
+            for (int p = 0; p < P; ++p) {
+                const uint32_t v = __hip_atomic_exchange(&acc[p * 64 + lane], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (cand[p] < sg.n_kmers) {
+                    if (a.add_counts) {
+                        if (v) atomicAdd(&sg.counts[cand[p]], v);
+                    } else {
+                        sg.counts[cand[p]] = v;
+                    }
+                }
+            }
+            if (lane == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     stamp(wave, 3);

@@ -171,3 +171,51 @@ def test_multi_gpu_context_shards_equal_one(shards):
     with ac.ApproxCounter(n_gpus=shards) as multi:
         assert np.array_equal(multi.count(13, kmers, ac.pack_windows(wins)), exp)
         assert np.array_equal(multi.count(13, kmers, ac.pack_windows(wins[:2])), oracle.count_myers(13, kmers, wins[:2]))
+
+
+def test_counts_stored_without_memset(counter):
+    """ac_error_count_device stores the counts from inside the launch (the group's
+    last workgroup): stale values in the buffer are overwritten, and the hand-off
+    scratch is back to zero for the next launch, across launches of varying shape."""
+    import torch
+
+    rng = np.random.default_rng(7)
+    for trial, (k, n_kmers, n_win) in enumerate([(16, 500, 900), (16, 37, 300), (22, 300, 500),
+                                                 (11, 1000, 200), (16, 500, 900), (5, 9, 50)]):
+        kmers, wins = cases.planted_case(4242 + trial, k, n_kmers, n_win, win_len=(60, 151), p_n=0.01)
+        seg = ac.DeviceSegment.upload(kmers, ac.pack_windows(wins))
+        seg.counts.copy_(torch.from_numpy(rng.integers(1, 1 << 30, seg.counts.numel(), dtype=np.int32)))
+        counter.count_device(k, [seg])
+        torch.cuda.synchronize()
+        assert np.array_equal(seg.counts_numpy(), oracle.count_myers(k, kmers, wins)), (trial, k)
+
+
+def test_accumulate_adds_to_existing(counter):
+    import torch
+
+    kmers, wins = cases.planted_case(31337, 16, 300, 400, win_len=(100, 101))
+    exp = oracle.count_myers(16, kmers, wins)
+    seg = ac.DeviceSegment.upload(kmers, ac.pack_windows(wins))
+    base = np.arange(seg.counts.numel(), dtype=np.int32) * 7
+    seg.counts.copy_(torch.from_numpy(base))
+    counter.count_device(16, [seg], accumulate=True)
+    counter.count_device(16, [seg], accumulate=True)
+    torch.cuda.synchronize()
+    assert np.array_equal(seg.counts_numpy(), base[: len(kmers)].astype(np.uint64) + 2 * exp)
+
+
+def test_fused_shards_sharing_counts(counter):
+    """Window shards of one candidate set fused in one non-accumulate launch, all
+    pointing at the same count vector: the launch sums them (zeroing once)."""
+    import torch
+
+    kmers, wins = cases.planted_case(2718, 16, 500, 1000, win_len=(90, 110), p_n=0.01)
+    exp = oracle.count_myers(16, kmers, wins)
+    bounds = np.linspace(0, len(wins), 5).astype(int)
+    segs = [ac.DeviceSegment.upload(kmers, ac.pack_windows(wins[bounds[i]:bounds[i + 1]])) for i in range(4)]
+    for s in segs[1:]:
+        s.counts = segs[0].counts
+    segs[0].counts.fill_(12345)
+    counter.count_device(16, segs)
+    torch.cuda.synchronize()
+    assert np.array_equal(segs[0].counts_numpy(), exp)
