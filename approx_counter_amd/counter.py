@@ -175,12 +175,20 @@ class ApproxCounter:
             n = int(n_out.value)
             return [(int(a), int(b)) for a, b in zip(km[:n], ct[:n])], int(n_dist.value), int(had_n.value)
 
+    @staticmethod
+    def segment_array(segments):
+        """The ac_segment array of DeviceSegment objects, built once and reusable with
+        count_device (saves the per-call ctypes marshalling in launch loops)."""
+        return (ACSegment * len(segments))(*[s.as_struct() for s in segments])
+
     def count_device(self, k: int, segments, stream=None, accumulate: bool = False) -> None:
-        """ac_error_count_device over DeviceSegment objects (asynchronous)."""
-        arr = (ACSegment * len(segments))(*[s.as_struct() for s in segments])
+        """ac_error_count_device over DeviceSegment objects, or an array from
+        segment_array (asynchronous)."""
+        arr = segments if isinstance(segments, ctypes.Array) else self.segment_array(segments)
         fn = self._L.ac_error_count_device_accumulate if accumulate else self._L.ac_error_count_device
-        st = fn(self._h, int(k), arr, len(segments), ctypes.c_void_p(stream or 0))
-        check(st, self._h)
+        st = fn(self._h, int(k), arr, len(arr), ctypes.c_void_p(stream or 0))
+        if st:
+            check(st, self._h)
 
     def last_launch(self):
         w, wpw, g = ctypes.c_uint64(), ctypes.c_uint32(), ctypes.c_uint32()

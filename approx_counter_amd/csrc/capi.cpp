@@ -196,6 +196,9 @@ ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hi
             if (x.queue_begin == ~0u || y.queue_begin == ~0u) continue;
             alias = x.counts < y.counts + y.n_kmers && y.counts < x.counts + x.n_kmers;
         }
+#ifdef AC_COUNTS_DIRECT  // A/B variant: memset + direct atomics
+    alias = true;
+#endif
     a.add_counts = (!zero || alias) ? 1u : 0u;
     if (zero && alias)
         for (uint32_t i = 0; i < n; ++i)

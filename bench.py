@@ -165,6 +165,7 @@ def main():
             ss.append(s2)
         seg_sets.append(ss)
     segs = seg_sets[0]
+    seg_arrays = [ac.ApproxCounter.segment_array(ss) for ss in seg_sets]
     bases = [sum(int(w.size) for w in wl[e]["windows"]) for e in ends]
     units = sum(n * b for n, b in zip(n_c, bases))
     stream = torch.cuda.current_stream(dev)
@@ -184,7 +185,7 @@ def main():
         if i is not None:
             evs[i][0].record(stream)
         # ac_error_count_device: the counts are stored by the launch itself (no memset)
-        counter.count_device(args.k, seg_sets[b], stream=sp)
+        counter.count_device(args.k, seg_arrays[b], stream=sp)
         if i is not None:
             evs[i][1].record(stream)
         if world > 1:
@@ -210,6 +211,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(i)
+    t_enq = time.perf_counter() - t0  # host enqueue time of the K steps (diagnostic)
     drain()
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -257,6 +259,7 @@ def main():
                        "parallelism": f"window shards x{world}, {'RCCL' if backend == 'nccl' else backend} "
                                       f"all-reduce of counts" if world > 1 else "1 GPU"},
             "kernel_ms": kern_ms,
+            "host_enqueue_ms_per_step": t_enq / args.steps * 1e3,
             "kernel_kmer_bp_per_s": units / (kern_ms * 1e-3),
             "launch": geo,
             "roofline": {"bound": "valu", "achieved": achieved / 1e12, "peak": VALU_PEAK_OPS / 1e12,
