@@ -201,47 +201,23 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
     const uint32_t g = ql / sg.subq, j = ql % sg.subq;
     const uint32_t m = a.m;
 
-    // Lane constants: character i of pattern p at bit 31 - (i*P + p).
-    uint32_t ph, pl, cand[P];
+    uint32_t cand[P];
+#pragma unroll
+    for (int p = 0; p < P; ++p) cand[p] = g * (64u * P) + (uint32_t)p * 64u + lane;
     uint32_t first = 0;
 #pragma unroll
     for (int p = 0; p < P; ++p) first |= 1u << (31 - p);
-    {
-        uint64_t km[P];
-#pragma unroll
-        for (int p = 0; p < P; ++p) {
-            cand[p] = g * (64u * P) + (uint32_t)p * 64u + lane;
-            km[p] = cand[p] < sg.n_kmers ? sg.kmers[cand[p]] : 0ull;
-        }
-        build_masks<P>(km, m, ph, pl);
-    }
     // Initial rows (empty text): R1 has character 0 set, R2 characters 0 and 1.
     const uint32_t d1_init = ~first, d2_init = ~(first | (first >> P));
-    // ~Eq table: ~Eq_c = (ph ^ H_c) | (pl ^ L_c), H_c / L_c = all ones where
-    // character c's high / low code bit is set; N matches nothing.
-    // Every wave of the workgroup writes the same table (same candidates), so a
-    // wave's own writes precede its reads and no barrier is needed for it; the
-    // barrier below orders the zeroed count vector before any wave adds to it.
+    uint32_t cnt[P];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) lds.tab.e[c * 64 + lane] = ((c & 2) ? ~ph : ph) | ((c & 1) ? ~pl : pl);
-    lds.tab.e[4 * 64 + lane] = ~0u;
-    if (wib == 0) {
-#pragma unroll
-        for (int p = 0; p < P; ++p) lds.cnt[p * 64 + lane] = 0u;
-    }
-    __syncthreads();
+    for (int p = 0; p < P; ++p) cnt[p] = 0;
     const uint32_t eb = __builtin_amdgcn_readfirstlane(
         (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)(&lds.tab.e[0]));
     // The eb0 blocks address the table from LDS 0.  Never expected otherwise;
     // if it were, the waves skip the work (no fault) and the counts come out
     // short, which the parity tests catch.
     const bool eb_ok = !TID_EB0 || eb == 0u;
-
-    uint32_t cnt[P];
-#pragma unroll
-    for (int p = 0; p < P; ++p) cnt[p] = 0;
-
-    stamp(wave, 1);
 
     // Counters of the other queue bank are zeroed for the next launch (strided
     // over the waves; nobody dequeues from that bank in this launch).
@@ -323,6 +299,29 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
         nlen = sg.length[w];
         if (valid(nbase, nlen)) nf = tid_fetch(sg.codes + (nbase >> 4), sg.nmask + (nbase >> 5), nlen, 0, lane);
     }
+
+    // ~Eq table, built by wave 0 of the workgroup (the waves share the
+    // candidates) while the first windows' loads are in flight: ~Eq_c =
+    // (ph ^ H_c) | (pl ^ L_c), H_c / L_c = all ones where character c's high /
+    // low code bit is set; N matches nothing.  Only wave 0 loads the k-mers
+    // (every wave of a group loading them at launch start queued for up to
+    // 12 us, tools/stamps.py).  The barrier waits for LDS only, not for the
+    // window prefetches.
+    if (wib == 0) {
+        uint64_t km[P];
+#pragma unroll
+        for (int p = 0; p < P; ++p) km[p] = cand[p] < sg.n_kmers ? sg.kmers[cand[p]] : 0ull;
+        uint32_t ph, pl;
+        build_masks<P>(km, a.m, ph, pl);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) lds.tab.e[c * 64 + lane] = ((c & 2) ? ~ph : ph) | ((c & 1) ? ~pl : pl);
+        lds.tab.e[4 * 64 + lane] = ~0u;
+#pragma unroll
+        for (int p = 0; p < P; ++p) lds.cnt[p * 64 + lane] = 0u;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    stamp(wave, 1);
+
     while (item < n_items) {
         const uint64_t base = nbase;
         const uint32_t len = nlen;
