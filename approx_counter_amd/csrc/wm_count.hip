@@ -120,7 +120,11 @@ __device__ __forceinline__ void build_masks(const uint64_t (&km)[P], uint32_t m,
     }
 }
 
+#ifdef AC_TID_BLOCKS_INC  // A/B builds (tools/variants.sh) of another generator setting
+#include AC_TID_BLOCKS_INC
+#else
 #include "wm_tid_blocks.inc"
+#endif
 
 // Per-wave ~Eq table: word c*64 + lane = the lane's ~Eq mask for character c
 // (A C G T, then N = all ones), read per base with ds_read_addtid_b32.

@@ -23,7 +23,10 @@ import os
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "approx_counter_amd", "csrc", "wm_tid_blocks.inc")
-AHEAD = 3  # LDS reads in flight ahead of the base being computed
+import sys
+
+AHEAD = 4  # LDS reads in flight ahead of the base being computed
+WAIT_PAIR = True  # one s_waitcnt per two bases (the SALU is the CU-shared resource)
 NE = AHEAD + 3  # rotating ~Eq registers (base i's is read by rows 0-2 at steps i..i+2)
 
 
@@ -65,7 +68,10 @@ def block(nb, with_n, eb0):
         rows = [(r, st - r) for r in range(3) if 0 <= st - r < nb]
         if st < nb:
             issued = min(st + AHEAD, nb)
-            L.append(f"s_waitcnt lgkmcnt({issued - (st + 1)})")
+            if not WAIT_PAIR:
+                L.append(f"s_waitcnt lgkmcnt({issued - (st + 1)})")
+            elif st % 2 == 0:  # bases st and st+1 (reads complete in order)
+                L.append(f"s_waitcnt lgkmcnt({max(0, issued - min(st + 2, nb))})")
         ahead = st < nb and st + AHEAD < nb
         if ahead:
             L += m0_setup(st + AHEAD, with_n, eb0)
@@ -139,6 +145,11 @@ __device__ __forceinline__ void tid_block{nb}(TidNfa& s, uint32_t code, uint32_t
 
 
 def main():
+    global AHEAD, NE, WAIT_PAIR, OUT
+    if "--v6" in sys.argv:  # A/B: one wait per base, 3 reads ahead (build/var only)
+        AHEAD, WAIT_PAIR = 3, False
+        NE = AHEAD + 3
+        OUT = os.path.join(ROOT, "build", "wm_tid_blocks_v6.inc")
     parts = [
         "// GENERATED by tools/gen_tid_blocks.py -- do not edit.  Inline-asm blocks of the\n"
         "// table-driven count loop (wm_count.hip, DESIGN.md §4).\n"
