@@ -126,8 +126,13 @@ ac_status ac_error_count(ac_ctx* ctx, uint32_t k, const uint64_t* kmers, uint32_
 /*
  * Device-resident form (same semantics), asynchronous on `hip_stream`
  * (a hipStream_t; NULL = the default stream).  All segments share k and run
- * in ONE kernel launch (both read ends of one run, 858-953).  Each segment's
- * counts are zeroed on the stream and then accumulated: uint32 counters.
+ * in ONE kernel launch (both read ends of one run, 858-953), uint32 counters.
+ * The launch itself stores each segment's counts (no memset dispatch): the
+ * last workgroup of every candidate group writes the group's sums.  Segments
+ * whose count vectors overlap (window shards of one candidate set) are zeroed
+ * on the stream first and summed.  The context's scratch (work queues, group
+ * sums) is stream-ordered: do not run two launches of one context on
+ * different streams at the same time.
  */
 ac_status ac_error_count_device(ac_ctx* ctx, uint32_t k, const ac_segment* segments,
                                 uint32_t n_segments, void* hip_stream);
