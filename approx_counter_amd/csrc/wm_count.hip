@@ -352,11 +352,28 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
         auto segment = [&](uint32_t f, uint32_t sb) {
             const uint32_t nb = min(SEG, len - sb);
             const uint32_t nfull = nb >> 4;
+#ifndef AC_BLOCK16_ONLY
+            // 32 bases per asm statement (half the per-block scalar overhead and
+            // pipeline fill), then at most one 16-base block.
+            uint32_t ch = 0;
+            for (; ch + 2u <= nfull; ch += 2u) {
+                const uint32_t code = __builtin_amdgcn_readlane(f, ch);
+                const uint32_t code2 = __builtin_amdgcn_readlane(f, ch + 1u);
+                const uint32_t nm = __builtin_amdgcn_readlane(f, 16u + (ch >> 1));
+                tid_block32<P, TID_EB0>(s, code, code2, nm, eb);
+            }
+            if (ch < nfull) {
+                const uint32_t code = __builtin_amdgcn_readlane(f, ch);
+                const uint32_t nm = (__builtin_amdgcn_readlane(f, 16u + (ch >> 1)) >> ((ch & 1u) * 16u)) & 0xffffu;
+                tid_block16<P, TID_EB0>(s, code, nm, eb);
+            }
+#else
             for (uint32_t ch = 0; ch < nfull; ++ch) {
                 const uint32_t code = __builtin_amdgcn_readlane(f, ch);
                 const uint32_t nm = (__builtin_amdgcn_readlane(f, 16u + (ch >> 1)) >> ((ch & 1u) * 16u)) & 0xffffu;
                 tid_block16<P, TID_EB0>(s, code, nm, eb);
             }
+#endif
             if (nb & 15u) {
                 const uint32_t code = __builtin_amdgcn_readlane(f, nfull);
                 const uint32_t nm = (__builtin_amdgcn_readlane(f, 16u + (nfull >> 1)) >> ((nfull & 1u) * 16u)) & 0xffffu;

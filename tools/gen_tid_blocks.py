@@ -4,10 +4,11 @@ the count kernel's table-driven inner loop ("~Eq from an LDS tabl
 
     python tools/gen_tid_blocks.py      # rewrites the .inc (committed; the build does not run this)
 
-One block runs NB text bases (NB = 16, 8, 4, 2, 1) of one window through the
+One block runs NB text bases (NB = 32, 16, 8, 4, 2, 1) of one window through the
 Wu-Manber NFA for P interleaved patterns per lane (see wm_count.hip).  The text
 is wave-uniform: base j's 2-bit code sits at bits 2j..2j+1 of the SGPR `code`
-(and, in the N-aware blocks, its N flag at bit j of the SGPR `nm`).  Per base:
+(bases 16-31 of a 32-base block in `code2`) and, in the N-aware path, its N flag
+at bit j of the SGPR `nm`.  Per base:
   SALU   c = code field (4 if N); M0 = ebase + 256*c
   LDS    ds_read_addtid_b32 e  -> e = lane's ~Eq mask for character c
          (a per-wave table of 5 x 64 words built once per wave: no VALU op per
@@ -33,8 +34,9 @@ NE = AHEAD + 3  # rotating ~Eq registers (base i's is read by rows 0-2 at steps 
 def m0_setup(j, with_n, eb0):
     """SALU: M0 = ebase + 256 * (code of base j, or 4 for N).  With eb0 the
     wave's table sits at LDS address 0 (one-wave workgroups) and the add goes."""
-    lit = (2 << 16) | (2 * j)
-    s = [f"s_bfe_u32 %[t], %[code], {lit:#x}"]
+    word, jj = ("%[code]", j) if j < 16 else ("%[code2]", j - 16)  # 32-base blocks take two code words
+    lit = (2 << 16) | (2 * jj)
+    s = [f"s_bfe_u32 %[t], {word}, {lit:#x}"]
     if with_n:
         s += [f"s_bitcmp1_b32 %[nm], {j}", "s_cselect_b32 %[t], 4, %[t]"]
     if eb0:
@@ -117,6 +119,8 @@ def body(nb, eb0):
 
 
 def emit(nb):
+    code2_in = ', [code2] "s"(code2)' if nb > 16 else ""
+    code2_arg = ", uint32_t code2" if nb > 16 else ""
     scratch = [f"D{r}{k}" for r in range(3) for k in range(3)] + [f"T{r}{k}" for r in range(3) for k in range(3)]
     scratch += ["x1", "x2"] + [f"e{k}" for k in range(NE)]
     decl = ", ".join(scratch)
@@ -125,10 +129,10 @@ def emit(nb):
               [s2] "+v"(s.s2), [a0] "+v"(s.a0), [a1] "+v"(s.a1), [a2] "+v"(s.a2),
               {outs},
               [t] "=&s"(t), [keep] "=&s"(keep)
-            : [code] "s"(code), [nm] "s"(nm), [eb] "s"(eb), [P] "n"(P)
+            : [code] "s"(code){code2_in}, [nm] "s"(nm), [eb] "s"(eb), [P] "n"(P)
             : "memory", "scc");"""
     return f"""template <int P, bool EB0>
-__device__ __forceinline__ void tid_block{nb}(TidNfa& s, uint32_t code, uint32_t nm, uint32_t eb) {{
+__device__ __forceinline__ void tid_block{nb}(TidNfa& s, uint32_t code{code2_arg}, uint32_t nm, uint32_t eb) {{
     uint32_t {decl};
     uint32_t t, keep;
     if constexpr (EB0) {{
@@ -156,7 +160,7 @@ def main():
         "// TidNfa: d* complemented NFA rows, s* = d* >> P, a* AND of the rows over the window.\n"
         "struct TidNfa {\n    uint32_t d0, d1, d2, s0, s1, s2, a0, a1, a2;\n};\n\n"
     ]
-    for nb in (16, 8, 4, 2, 1):
+    for nb in (32, 16, 8, 4, 2, 1):
         parts.append(emit(nb))
     with open(OUT, "w") as fh:
         fh.write("\n".join(parts))
