@@ -34,7 +34,7 @@ NE = AHEAD + 3  # rotating ~Eq registers (base i's is read by rows 0-2 at steps 
 def m0_setup(j, with_n, eb0):
     """SALU: M0 = ebase + 256 * (code of base j, or 4 for N).  With eb0 the
     wave's table sits at LDS address 0 (one-wave workgroups) and the add goes."""
-    word, jj = ("%[code]", j) if j < 16 else ("%[code2]", j - 16)  # 32-base blocks take two code words
+    word, jj = (("%[code]", "%[code2]", "%[code3]", "%[code4]")[j // 16], j % 16)  # one code word per 16 bases
     lit = (2 << 16) | (2 * jj)
     s = [f"s_bfe_u32 %[t], {word}, {lit:#x}"]
     if with_n:
@@ -119,8 +119,9 @@ def body(nb, eb0):
 
 
 def emit(nb):
-    code2_in = ', [code2] "s"(code2)' if nb > 16 else ""
-    code2_arg = ", uint32_t code2" if nb > 16 else ""
+    extra = [f"code{i}" for i in range(2, (nb + 15) // 16 + 1)]
+    code2_in = "".join(f', [{c}] "s"({c})' for c in extra)
+    code2_arg = "".join(f", uint32_t {c}" for c in extra)
     scratch = [f"D{r}{k}" for r in range(3) for k in range(3)] + [f"T{r}{k}" for r in range(3) for k in range(3)]
     scratch += ["x1", "x2"] + [f"e{k}" for k in range(NE)]
     decl = ", ".join(scratch)
@@ -160,7 +161,7 @@ def main():
         "// TidNfa: d* complemented NFA rows, s* = d* >> P, a* AND of the rows over the window.\n"
         "struct TidNfa {\n    uint32_t d0, d1, d2, s0, s1, s2, a0, a1, a2;\n};\n\n"
     ]
-    for nb in (32, 16, 8, 4, 2, 1):
+    for nb in (32, 16, 8, 4, 2, 1):  # 64-base blocks measured no faster (r01_kernel_log.md)
         parts.append(emit(nb))
     with open(OUT, "w") as fh:
         fh.write("\n".join(parts))
