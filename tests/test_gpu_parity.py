@@ -219,3 +219,11 @@ def test_fused_shards_sharing_counts(counter):
     counter.count_device(16, segs)
     torch.cuda.synchronize()
     assert np.array_equal(segs[0].counts_numpy(), exp)
+
+
+@pytest.mark.parametrize("k", [5, 11, 16, 22, 32])
+def test_long_ragged_windows(counter, k):
+    """Windows longer than one 256-base fetch segment (ragged lengths, N's, hits
+    planted anywhere incl. across the 256-base seams)."""
+    kmers, wins = cases.planted_case(777 + k, k, 150, 120, win_len=(200, 1500), p_n=0.005)
+    assert np.array_equal(gpu_counts(counter, k, kmers, wins), oracle.count_myers(k, kmers, wins)), k
