@@ -529,13 +529,16 @@ ac_status ac_exact_count_device(ac_ctx* ctx, uint32_t k, const ac_windows* dev, 
     std::vector<uint64_t> fb(forbidden, forbidden + n_forbidden);
     std::sort(fb.begin(), fb.end());
     fb.erase(std::unique(fb.begin(), fb.end()), fb.end());
-    if (ac_status s2 = grow(ctx, &ctx->e_buf[0], &ctx->e_cap[0], sizeof(acamd::ExactSlot) * slots)) return s2;
+    // k <= 16: compact 8-byte slots (key and count in one word, exact_count.h)
+    const bool compact = k <= acamd::EXACT_COMPACT_MAX_K;
+    const size_t slot_bytes = compact ? sizeof(unsigned long long) : sizeof(acamd::ExactSlot);
+    if (ac_status s2 = grow(ctx, &ctx->e_buf[0], &ctx->e_cap[0], slot_bytes * slots)) return s2;
     if (ac_status s2 = grow(ctx, &ctx->e_buf[1], &ctx->e_cap[1], (sizeof(uint64_t) + sizeof(uint32_t)) * list_cap))
         return s2;
     if (ac_status s2 = grow(ctx, &ctx->e_buf[2], &ctx->e_cap[2], small_bytes)) return s2;
     if (ac_status s2 = grow(ctx, &ctx->e_buf[3], &ctx->e_cap[3], sizeof(uint64_t) * std::max<size_t>(1, fb.size())))
         return s2;
-    AC_HIP(ctx, hipMemsetAsync(ctx->e_buf[0], 0, sizeof(acamd::ExactSlot) * slots, st));
+    AC_HIP(ctx, hipMemsetAsync(ctx->e_buf[0], 0, slot_bytes * slots, st));
     AC_HIP(ctx, hipMemsetAsync(ctx->e_buf[2], 0, small_bytes, st));
     if (!fb.empty())
         AC_HIP(ctx, hipMemcpyAsync(ctx->e_buf[3], fb.data(), sizeof(uint64_t) * fb.size(), hipMemcpyHostToDevice, st));
@@ -550,6 +553,8 @@ ac_status ac_exact_count_device(ac_ctx* ctx, uint32_t k, const ac_windows* dev, 
     a.n_windows = dev->n_windows;
     a.k = k;
     a.table = (acamd::ExactSlot*)ctx->e_buf[0];
+    a.ctable = (unsigned long long*)ctx->e_buf[0];
+    a.compact = compact ? 1u : 0u;
     a.slots = slots;
     a.mask = slots - 1;
     a.special = (uint32_t*)small;

@@ -11,11 +11,17 @@
 
 namespace acamd {
 
+// Wide slot (k > 16): 16 bytes, claimed with a CAS on the key, counted with an
+// add on cnt.
 struct alignas(16) ExactSlot {
     uint64_t key;  // k-mer + 1; 0 = empty
     uint32_t cnt;
     uint32_t pad;
 };
+// Compact slot (k <= 16): one u64 = (uint32)(k-mer + 1) << 32 | count.  A new
+// key is claimed AND counted by one CAS (most k-mers of a sample occur once);
+// a repeated key takes one 64-bit add on the same word.
+constexpr uint32_t EXACT_COMPACT_MAX_K = 16;
 
 struct ExactArgs {
     // window image (device)
@@ -26,11 +32,14 @@ struct ExactArgs {
     uint64_t n_bases;
     uint32_t n_windows;
     uint32_t k;
-    // hash table: `slots` (a power of two) 16-byte slots {k-mer + 1, count};
-    // stored key 0 = empty, so a zero memset clears it.  Slot index `slots`
-    // (past the table) stands for the all-T 32-mer (whose key + 1 wraps to 0),
-    // counted in special[0].
+    // hash table: `slots` (a power of two) slots, ExactSlot {k-mer + 1, count}
+    // or, when `compact`, u64 (k-mer + 1) << 32 | count; stored key 0 = empty,
+    // so a zero memset clears it.  Slot index `slots` (past the table) stands
+    // for the all-T k-mer whose stored key wraps to 0 (the 32-mer in the wide
+    // layout, the 16-mer in the compact one), counted in special[0].
     ExactSlot* table;
+    unsigned long long* ctable;
+    uint32_t compact;
     uint64_t slots;
     uint64_t mask;
     uint32_t* special;

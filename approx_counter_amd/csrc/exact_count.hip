@@ -10,7 +10,9 @@
 //     key (dna2int layout) counted in an open-addressing hash table in HBM.
 //     Each workgroup first aggregates its batch of windows in an LDS table
 //     (adapter k-mers occur in most windows, so hot keys are summed locally),
-//     then flushes the aggregated (key, count) pairs with global atomics.
+//     then flushes the aggregated (key, count) pairs with global atomics:
+//     for k <= 16 into 8-byte slots where one CAS both claims and counts a new
+//     key, otherwise into 16-byte slots (CAS on the key + add on the count).
 //  2. scan: every occupied slot passes the low-complexity filter (the float
 //     DUST score of approx_counter.cpp:247-267, computed exactly as the
 //     reference does) and the forbidden set (binary search); kept entries feed
@@ -70,8 +72,30 @@ __device__ __forceinline__ uint64_t to_dna2int(uint64_t le, uint32_t k) {
     return r >> (64u - 2u * k);
 }
 
-// One CAS claims or finds the slot, one add on the same 16-byte slot counts.
+// Wide layout: one CAS claims or finds the slot, one add on the same 16-byte
+// slot counts.  Compact layout (k <= 16): the CAS that claims a new slot also
+// stores its count, so a key seen once costs one atomic; a repeated key adds
+// to the low half of its 64-bit word (counts stay below 2^32).
 __device__ __forceinline__ void global_insert(const ExactArgs& a, uint64_t key, uint32_t c) {
+    if (a.compact) {
+        const uint32_t stored = (uint32_t)key + 1u;
+        if (!stored) {  // the all-T 16-mer
+            atomicAdd(&a.special[0], c);
+            return;
+        }
+        const unsigned long long tag = (unsigned long long)stored << 32;
+        uint64_t h = mix64(key) & a.mask;
+        for (;;) {
+            unsigned long long* sl = &a.ctable[h];
+            const unsigned long long cur = atomicCAS(sl, 0ull, tag | c);
+            if (cur == 0ull) return;
+            if ((uint32_t)(cur >> 32) == stored) {
+                atomicAdd(sl, (unsigned long long)c);
+                return;
+            }
+            h = (h + 1u) & a.mask;
+        }
+    }
     if (key == EMPTY) {  // the all-T 32-mer
         atomicAdd(&a.special[0], c);
         return;
@@ -190,25 +214,52 @@ __device__ __forceinline__ bool is_forbidden(const ExactArgs& a, uint64_t key) {
     return false;
 }
 
-// One 16-byte load of slot s.
-// Unconditional (clamped address) so a thread's loads issue back to back; for
-// s >= slots the value is ignored by kept_count.
-__device__ __forceinline__ uint4 load_slot(const ExactArgs& a, uint64_t s) {
-    return *reinterpret_cast<const uint4*>(&a.table[s < a.slots ? s : a.slots - 1u]);
-}
-
-// Kept (not low-complexity, not forbidden) entry count of a loaded slot, 0 if
-// none; slot index a.slots is the all-T 32-mer kept apart from the table.
-__device__ __forceinline__ uint32_t kept_count(const ExactArgs& a, uint64_t s, uint4 v, uint64_t& key) {
-    uint32_t c;
-    if (s == a.slots) {
-        key = EMPTY;
-        c = a.special[0];
-    } else {
+// Slot layouts.  load(): one load of slot s, unconditional (clamped address)
+// so a thread's loads issue back to back; for s >= slots the value is ignored
+// by kept_count.  decode(): count of a loaded slot (0 = empty) and its k-mer.
+// special: the all-T k-mer whose stored key wraps to 0, counted in special[0].
+template <bool Compact>
+struct Layout;
+template <>
+struct Layout<false> {
+    using V = uint4;
+    static constexpr uint32_t UNROLL = 4;  // four 16-byte loads in flight per thread
+    static constexpr uint64_t special = ~0ull;
+    __device__ static V load(const ExactArgs& a, uint64_t s) {
+        return *reinterpret_cast<const uint4*>(&a.table[s < a.slots ? s : a.slots - 1u]);
+    }
+    __device__ static uint32_t decode(V v, uint64_t& key) {
         const uint64_t stored = ((uint64_t)v.y << 32) | v.x;
         if (!stored) return 0;
         key = stored - 1ull;
-        c = v.z;
+        return v.z;
+    }
+};
+template <>
+struct Layout<true> {
+    using V = unsigned long long;
+    static constexpr uint32_t UNROLL = 8;  // eight 8-byte loads in flight per thread
+    static constexpr uint64_t special = 0xffffffffull;
+    __device__ static V load(const ExactArgs& a, uint64_t s) { return a.ctable[s < a.slots ? s : a.slots - 1u]; }
+    __device__ static uint32_t decode(V v, uint64_t& key) {
+        const uint32_t stored = (uint32_t)(v >> 32);
+        if (!stored) return 0;
+        key = stored - 1u;
+        return (uint32_t)v;
+    }
+};
+
+// Kept (not low-complexity, not forbidden) entry count of a loaded slot, 0 if
+// none; slot index a.slots is the all-T k-mer kept apart from the table.
+template <bool Compact>
+__device__ __forceinline__ uint32_t kept_count(const ExactArgs& a, uint64_t s, typename Layout<Compact>::V v,
+                                               uint64_t& key) {
+    uint32_t c;
+    if (s == a.slots) {
+        key = Layout<Compact>::special;
+        c = a.special[0];
+    } else {
+        c = Layout<Compact>::decode(v, key);
     }
     if (!c) return 0;
     if (complexity(key, a.k) >= a.lc_threshold) return 0;  // haveLowComplexity (214-234)
@@ -266,9 +317,10 @@ struct BlockAppender {
     __syncthreads();                                                                      \
     BlockAppender name{K, C, N, CAP, name##_k, name##_c, &name##_n, &name##_b};
 
-constexpr uint32_t SCAN_UNROLL = 4;  // slots per thread per trip: four 16-byte loads in flight
-
+template <bool Compact>
 __global__ __launch_bounds__(EXACT_THREADS) void exact_scan_kernel(ExactArgs a) {
+    using L = Layout<Compact>;
+    constexpr uint32_t SCAN_UNROLL = L::UNROLL;
     __shared__ uint32_t hist[EXACT_HIST_BINS];
     DECLARE_APPENDER(app, a.list_keys, a.list_cnts, a.n_list, a.list_cap)
     for (uint32_t i = threadIdx.x; i < EXACT_HIST_BINS; i += EXACT_THREADS) hist[i] = 0;
@@ -278,16 +330,16 @@ __global__ __launch_bounds__(EXACT_THREADS) void exact_scan_kernel(ExactArgs a) 
     const uint64_t stride = (uint64_t)gridDim.x * step;
     uint32_t ones = 0;  // kept entries seen once (the bulk): one LDS add per wave at the end
     for (uint64_t s0 = (uint64_t)blockIdx.x * step; s0 < n; s0 += stride) {  // block-uniform trips
-        uint4 v[SCAN_UNROLL];
+        typename L::V v[SCAN_UNROLL];
         uint64_t key[SCAN_UNROLL];
         uint32_t c[SCAN_UNROLL];
 #pragma unroll
-        for (uint32_t j = 0; j < SCAN_UNROLL; ++j) v[j] = load_slot(a, s0 + j * EXACT_THREADS + threadIdx.x);
+        for (uint32_t j = 0; j < SCAN_UNROLL; ++j) v[j] = L::load(a, s0 + j * EXACT_THREADS + threadIdx.x);
 #pragma unroll
         for (uint32_t j = 0; j < SCAN_UNROLL; ++j) {
             const uint64_t s = s0 + j * EXACT_THREADS + threadIdx.x;
             key[j] = 0;
-            c[j] = s < n ? kept_count(a, s, v[j], key[j]) : 0u;
+            c[j] = s < n ? kept_count<Compact>(a, s, v[j], key[j]) : 0u;
         }
 #pragma unroll
         for (uint32_t j = 0; j < SCAN_UNROLL; ++j) {
@@ -306,6 +358,7 @@ __global__ __launch_bounds__(EXACT_THREADS) void exact_scan_kernel(ExactArgs a) 
 }
 
 // Entries with count >= threshold from the whole table (threshold below EXACT_LIST_MIN).
+template <bool Compact>
 __global__ __launch_bounds__(EXACT_THREADS) void exact_gather_table_kernel(ExactArgs a) {
     DECLARE_APPENDER(app, a.out_keys, a.out_cnts, a.n_out, a.out_cap)
     const uint64_t n = a.slots + 1;
@@ -313,7 +366,7 @@ __global__ __launch_bounds__(EXACT_THREADS) void exact_gather_table_kernel(Exact
     for (uint64_t s0 = (uint64_t)blockIdx.x * EXACT_THREADS; s0 < n; s0 += stride) {
         const uint64_t s = s0 + threadIdx.x;
         uint64_t key = 0;
-        const uint32_t c = s < n ? kept_count(a, s, load_slot(a, s), key) : 0u;
+        const uint32_t c = s < n ? kept_count<Compact>(a, s, Layout<Compact>::load(a, s), key) : 0u;
         app.push(c && c >= a.threshold, key, c);
         app.sync_flush(false);
     }
@@ -349,7 +402,12 @@ static uint32_t scan_blocks(const ExactArgs& a, uint32_t per_thread) {
 }
 
 hipError_t launch_exact_scan(const ExactArgs& a, hipStream_t stream) {
-    hipLaunchKernelGGL(exact_scan_kernel, dim3(scan_blocks(a, SCAN_UNROLL)), dim3(EXACT_THREADS), 0, stream, a);
+    if (a.compact)
+        hipLaunchKernelGGL(exact_scan_kernel<true>, dim3(scan_blocks(a, Layout<true>::UNROLL)), dim3(EXACT_THREADS),
+                           0, stream, a);
+    else
+        hipLaunchKernelGGL(exact_scan_kernel<false>, dim3(scan_blocks(a, Layout<false>::UNROLL)),
+                           dim3(EXACT_THREADS), 0, stream, a);
     return hipGetLastError();
 }
 
@@ -358,8 +416,12 @@ hipError_t launch_exact_gather(const ExactArgs& a, bool from_list, uint64_t n_li
         if (!n_list) return hipSuccess;
         const uint32_t blocks = (uint32_t)std::min<uint64_t>(4096, (n_list + EXACT_THREADS - 1) / EXACT_THREADS);
         hipLaunchKernelGGL(exact_gather_list_kernel, dim3(blocks), dim3(EXACT_THREADS), 0, stream, a, n_list);
+    } else if (a.compact) {
+        hipLaunchKernelGGL(exact_gather_table_kernel<true>, dim3(scan_blocks(a, 1)), dim3(EXACT_THREADS), 0, stream,
+                           a);
     } else {
-        hipLaunchKernelGGL(exact_gather_table_kernel, dim3(scan_blocks(a, 1)), dim3(EXACT_THREADS), 0, stream, a);
+        hipLaunchKernelGGL(exact_gather_table_kernel<false>, dim3(scan_blocks(a, 1)), dim3(EXACT_THREADS), 0, stream,
+                           a);
     }
     return hipGetLastError();
 }

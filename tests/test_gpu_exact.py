@@ -68,6 +68,10 @@ def test_edge_windows(counter):
     check(counter, [], 16, 1.0)
     check(counter, ["", "ACG", "N" * 40], 16, 1.0)
     check(counter, ["T" * 80, "T" * 32 + "A", "NTTTT" + "T" * 40], 32, 1.0, limit=50)  # all-T 32-mer (table sentinel)
+    # all-T 16-mer: the compact layout's sentinel (its stored key wraps to 0); the
+    # threshold keeps the low-complexity run so the sentinel reaches the output
+    check(counter, ["T" * 40, "T" * 16 + "A", "ACGT" * 10 + "T" * 20], 16, 100.0, limit=50)
+    check(counter, ["T" * 40, "GT" * 30], 15, 100.0, limit=50)  # all-T 15-mer: an ordinary compact key
     check(counter, ["ACGT" * 300], 16, 1.0)  # a window longer than the LDS staging
 
 
