@@ -289,11 +289,12 @@ struct BlockAppender {
             lc[i] = c;
         }
     }
-    // Call from every thread of the block; flushes when `force` or nearly full.
-    __device__ void sync_flush(bool force) {
+    // Call from every thread of the block; flushes when `force` or when the
+    // next round of pushes (at most `max_push` entries) might not fit.
+    __device__ void sync_flush(bool force, uint32_t max_push = EXACT_THREADS) {
         __syncthreads();
         const uint32_t m = *ln;
-        if (!m || (!force && m + EXACT_THREADS <= APPEND_BUF)) return;  // block-uniform
+        if (!m || (!force && m + max_push <= APPEND_BUF)) return;  // block-uniform
         if (threadIdx.x == 0) *lbase = atomicAdd(n, (unsigned long long)m);
         __syncthreads();
         const uint64_t b = *lbase;
@@ -317,37 +318,74 @@ struct BlockAppender {
     __syncthreads();                                                                      \
     BlockAppender name{K, C, N, CAP, name##_k, name##_c, &name##_n, &name##_b};
 
+// The scan packs each trip's occupied slots densely per wave in LDS before
+// scoring them: most slots are empty (the table is sized for the image, load
+// <= 2/3, usually far less), and the DUST score of a lane-per-slot pass ran on
+// nearly every wave for a fifth of its lanes (VALU-bound, 283 us at 10^5
+// windows).  Per trip a block stages and pushes at most
+// EXACT_THREADS * UNROLL entries; the appender flushes before that could overflow.
+constexpr uint32_t SCAN_WAVES = EXACT_THREADS / 64;
+
 template <bool Compact>
 __global__ __launch_bounds__(EXACT_THREADS) void exact_scan_kernel(ExactArgs a) {
     using L = Layout<Compact>;
-    constexpr uint32_t SCAN_UNROLL = L::UNROLL;
+    constexpr uint32_t SCAN_UNROLL = 4;
+    constexpr uint32_t STAGE = 64 * SCAN_UNROLL;
+    static_assert(EXACT_THREADS * SCAN_UNROLL <= APPEND_BUF, "a trip must fit the appender");
     __shared__ uint32_t hist[EXACT_HIST_BINS];
+    __shared__ uint64_t st_key[SCAN_WAVES][STAGE];
+    __shared__ uint32_t st_cnt[SCAN_WAVES][STAGE];
     DECLARE_APPENDER(app, a.list_keys, a.list_cnts, a.n_list, a.list_cap)
     for (uint32_t i = threadIdx.x; i < EXACT_HIST_BINS; i += EXACT_THREADS) hist[i] = 0;
     __syncthreads();
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
     const uint64_t n = a.slots + 1;
     const uint64_t step = (uint64_t)EXACT_THREADS * SCAN_UNROLL;
     const uint64_t stride = (uint64_t)gridDim.x * step;
     uint32_t ones = 0;  // kept entries seen once (the bulk): one LDS add per wave at the end
     for (uint64_t s0 = (uint64_t)blockIdx.x * step; s0 < n; s0 += stride) {  // block-uniform trips
         typename L::V v[SCAN_UNROLL];
-        uint64_t key[SCAN_UNROLL];
-        uint32_t c[SCAN_UNROLL];
 #pragma unroll
         for (uint32_t j = 0; j < SCAN_UNROLL; ++j) v[j] = L::load(a, s0 + j * EXACT_THREADS + threadIdx.x);
+        uint32_t m = 0;  // entries staged by this wave (wave-uniform)
 #pragma unroll
         for (uint32_t j = 0; j < SCAN_UNROLL; ++j) {
             const uint64_t s = s0 + j * EXACT_THREADS + threadIdx.x;
-            key[j] = 0;
-            c[j] = s < n ? kept_count<Compact>(a, s, v[j], key[j]) : 0u;
+            uint64_t key = 0;
+            uint32_t c = 0;
+            if (s == a.slots) {
+                key = L::special;
+                c = a.special[0];
+            } else if (s < a.slots) {
+                c = L::decode(v[j], key);
+            }
+            const uint64_t occ = __ballot(c != 0u);
+            if (c) {
+                const uint32_t i = m + __builtin_amdgcn_mbcnt_hi((uint32_t)(occ >> 32),
+                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)occ, 0u));
+                st_key[wv][i] = key;
+                st_cnt[wv][i] = c;
+            }
+            m += (uint32_t)__popcll(occ);
         }
-#pragma unroll
-        for (uint32_t j = 0; j < SCAN_UNROLL; ++j) {
-            if (c[j] == 1u) ++ones;
-            else if (c[j]) atomicAdd(&hist[min(c[j], (uint32_t)EXACT_HIST_BINS - 1u)], 1u);
-            app.push(c[j] >= EXACT_LIST_MIN, key[j], c[j]);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (uint32_t i0 = 0; i0 < m; i0 += 64u) {  // wave-uniform
+            const uint32_t i = i0 + lane;
+            uint64_t key = 0;
+            uint32_t c = 0;
+            if (i < m) {
+                key = st_key[wv][i];
+                c = st_cnt[wv][i];
+                if (complexity(key, a.k) >= a.lc_threshold) c = 0;  // haveLowComplexity (214-234)
+                else if (is_forbidden(a, key)) c = 0;              // isForbiddenKmer (330-332)
+            }
+            if (c == 1u) ++ones;
+            else if (c) atomicAdd(&hist[min(c, (uint32_t)EXACT_HIST_BINS - 1u)], 1u);
+            app.push(c >= EXACT_LIST_MIN, key, c);
         }
-        app.sync_flush(false);
+        app.sync_flush(false, EXACT_THREADS * SCAN_UNROLL);
     }
     app.sync_flush(true);
     for (int off = 32; off; off >>= 1) ones += __shfl_xor(ones, off);

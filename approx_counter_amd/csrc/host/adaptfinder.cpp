@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <future>
 #include <iostream>
 #include <map>
 #include <random>
@@ -350,15 +351,23 @@ int main(int argc, char const** argv) {
     std::vector<std::string> ids;
     SeqSet seqs;
     WindowStore store;
+    // The GPU contexts (the reference builds its index inside errorCount; the
+    // device set is opened once).  Opening them (HIP runtime + device
+    // initialisation, ~75 ms) runs on a helper thread while the input is parsed;
+    // the first GPU stage waits for it and reports its failure, if any.
+    Devices dev;
+    std::future<void> dev_ready;
+    if (dump_sample.empty()) dev_ready = std::async(std::launch::async, [&dev, n_gpus] { open_devices(dev, n_gpus); });
+    auto devices = [&]() {
+        if (dev_ready.valid()) dev_ready.get();  // rethrows the helper's exception
+        open_devices(dev, n_gpus);
+    };
     if (v > 0) print("Parsing FASTA file", tab_level);
     if (host_exact) read_records(input_file, ids, seqs);
     else read_windows(input_file, sl, store);
     const uint64_t n_reads = host_exact ? seqs.size() : store.size();
     if (v > 0) print("Number of sequences found: " + std::to_string(n_reads) + ".", tab_level);
 
-    // The GPU contexts (the reference builds its index inside errorCount; the
-    // device set is opened once here).
-    Devices dev;
     std::mt19937 rng(seed_str.empty() ? std::random_device{}() : (uint32_t)std::strtoull(seed_str.c_str(), nullptr, 10));
 
     for (uint64_t run = 0; run < nb_of_runs; ++run) {
@@ -404,7 +413,7 @@ int main(int argc, char const** argv) {
                                         : get_most_frequent(std::move(count), limit, (uint32_t)k);
             } else {  // the same on GPU 0; the uploaded sample also serves the approximate count
                 try {
-                    open_devices(dev, n_gpus);
+                    devices();
                     const ac_windows hw = view(img);
                     if (ac_sample_upload(dev.ctx, &hw, &dsample) != AC_OK)
                         throw std::runtime_error(ac_last_error(dev.ctx));
@@ -434,7 +443,7 @@ int main(int argc, char const** argv) {
             if (mr_v > 0) print("Approximate k-mer count", tab_level);
             pair_vector error_counter;
             try {
-                open_devices(dev, n_gpus);
+                devices();
                 if (!host_exact && dev.shards == 1) {  // one GPU: count on the sample uploaded above
                     std::vector<uint64_t> km(first_n.size()), ct(first_n.size());
                     for (size_t i = 0; i < first_n.size(); ++i) km[i] = first_n[i].first;

@@ -6,7 +6,8 @@ approximate count).  Both must write identical files.
     python tools/cli_e2e.py [--reads 10000] [--lim 500] [--read-len 400]
 
 Prints one JSON line with the wall times and the stage timestamps of the
-default run (the CLI's own "[ms]" log lines)."""
+default run (the CLI's own "[ms]" log lines), plus the same parse + sampling
+with --dump-sample (no GPU stage) and a 100-read run (the fixed cost)."""
 import argparse
 import json
 import os
@@ -48,6 +49,22 @@ def main():
             out[tag + "_s"] = round(dt, 4)
             if tag == "default":
                 out["default_log"] = [ln.strip() for ln in r.stdout.splitlines() if ln.startswith("[")]
+        # the same parse + sampling without any GPU stage (--dump-sample), and the
+        # whole pipeline on 100 reads: the fixed cost (process, HIP runtime, device)
+        t = time.perf_counter()
+        r = subprocess.run(base + ["--dump-sample", os.path.join(d, "dump")], capture_output=True, text=True,
+                           timeout=600)
+        out["dump_sample_s"] = round(time.perf_counter() - t, 4)
+        if r.returncode != 0:
+            raise SystemExit(f"--dump-sample failed ({r.returncode}): {r.stderr[-2000:]}")
+        tiny = os.path.join(d, "tiny.fa")
+        write_fasta(tiny, reads[:100], width=80)
+        t = time.perf_counter()
+        r = subprocess.run([CLI, tiny, "-k", str(a.k), "-sl", str(a.sl), "-lim", str(a.lim), "--seed", "1", "-o",
+                            os.path.join(d, "tiny")], capture_output=True, text=True, timeout=600)
+        out["tiny_100_reads_s"] = round(time.perf_counter() - t, 4)
+        if r.returncode != 0:
+            raise SystemExit(f"tiny run failed ({r.returncode}): {r.stderr[-2000:]}")
         same = all(open(os.path.join(d, f"default{s}_0.{e}")).read() == open(os.path.join(d, f"host_exact{s}_0.{e}")).read()
                    for s in ("", "_exact") for e in ("start", "end"))
         out["identical_outputs"] = same
