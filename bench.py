@@ -73,6 +73,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-boundary", action="store_true",
                     help="skip the PCIe-inclusive host-buffer timing (keeps a rocprof trace to the timed launches)")
+    ap.add_argument("--inflight", type=int, default=1,
+                    help="batches in flight: independent counter contexts on their own HIP streams, "
+                         "steps dealt round-robin, so one batch's launch tail overlaps the next one's start")
     ap.add_argument("--verify", action="store_true", help="check counts against the oracle (slow)")
     ap.add_argument("--event-every", type=int, default=5,
                     help="bracket every N-th timed launch with HIP events (the kernel-duration sample); "
@@ -151,61 +154,74 @@ def main():
 
     wl, _ = workload.build(n_reads=args.sn, read_len=args.read_len, k=args.k, sl=args.sl,
                            lim=args.lim, seed=args.seed, shard=rank, n_shards=world)
-    counter = ac.ApproxCounter(local)
     ends = ("start", "end")
     n_c = [int(wl[e]["kmers"].size) for e in ends]
-    # Two count vectors: with N > 1 ranks the RCCL all-reduce of step i runs on
-    # the communicator's stream while step i+1 counts into the other buffer.
-    bufs = [torch.zeros(sum(n_c), dtype=torch.int32, device=dev) for _ in range(2)]
-    counts = bufs[0]
     packed = {e: ac.pack_windows(wl[e]["windows"]) for e in ends}
     base_segs = [ac.DeviceSegment.upload(wl[e]["kmers"], packed[e], device=dev) for e in ends]
-    seg_sets = []
-    for buf in bufs:
-        off, ss = 0, []
-        for seg, n in zip(base_segs, n_c):
-            s2 = copy.copy(seg)
-            s2.counts = buf[off:off + n]
-            off += n
-            ss.append(s2)
-        seg_sets.append(ss)
-    segs = seg_sets[0]
-    seg_arrays = [ac.ApproxCounter.segment_array(ss) for ss in seg_sets]
+    n_slots = max(1, args.inflight)
+    # One slot per batch in flight: its own counter context (device scratch, queue counters),
+    # its own stream and two count vectors.  With N > 1 ranks the RCCL all-reduce of a slot's
+    # step runs on the communicator's stream while that slot counts its next step into the
+    # other vector.
+    slots = []
+    for si in range(n_slots):
+        counter_s = ac.ApproxCounter(local)
+        st = torch.cuda.current_stream(dev) if si == 0 else torch.cuda.Stream(dev)
+        bufs = [torch.zeros(sum(n_c), dtype=torch.int32, device=dev) for _ in range(2)]
+        seg_sets = []
+        for buf in bufs:
+            off, ss = 0, []
+            for seg, n in zip(base_segs, n_c):
+                s2 = copy.copy(seg)
+                s2.counts = buf[off:off + n]
+                off += n
+                ss.append(s2)
+            seg_sets.append(ss)
+        slots.append(dict(counter=counter_s, stream=st, bufs=bufs, seg_sets=seg_sets,
+                          arrays=[ac.ApproxCounter.segment_array(ss) for ss in seg_sets],
+                          pending=[None, None], n=0))
+    counter = slots[0]["counter"]
+    segs = slots[0]["seg_sets"][0]
     bases = [sum(int(w.size) for w in wl[e]["windows"]) for e in ends]
     units = sum(n * b for n, b in zip(n_c, bases))
-    stream = torch.cuda.current_stream(dev)
-    sp = stream.cuda_stream
+    sp = slots[0]["stream"].cuda_stream
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
 
-    pending = [None, None]  # outstanding all-reduce per count buffer
     n_step = [0]
 
     def step(i=None):
-        b = n_step[0] % 2
+        sl = slots[n_step[0] % n_slots]
         n_step[0] += 1
-        buf = bufs[b]
-        if pending[b] is not None:  # the buffer's previous all-reduce must finish first
-            pending[b].wait()
-            pending[b] = None
+        b = sl["n"] % 2
+        sl["n"] += 1
+        buf = sl["bufs"][b]
+        st = sl["stream"]
+        if sl["pending"][b] is not None:  # the buffer's previous all-reduce must finish first
+            with torch.cuda.stream(st):
+                sl["pending"][b].wait()
+            sl["pending"][b] = None
         if i is not None:
-            evs[i][0].record(stream)
+            evs[i][0].record(st)
         # ac_error_count_device: the counts are stored by the launch itself (no memset)
-        counter.count_device(args.k, seg_arrays[b], stream=sp)
+        sl["counter"].count_device(args.k, sl["arrays"][b], stream=st.cuda_stream)
         if i is not None:
-            evs[i][1].record(stream)
+            evs[i][1].record(st)
         if world > 1:
             if backend == "nccl":
-                pending[b] = dist.all_reduce(buf, async_op=True)
+                with torch.cuda.stream(st):
+                    sl["pending"][b] = dist.all_reduce(buf, async_op=True)
             else:
+                st.synchronize()
                 host = buf.cpu()
                 dist.all_reduce(host)
                 buf.copy_(host)
 
     def drain():
-        for b in range(2):
-            if pending[b] is not None:
-                pending[b].wait()
-                pending[b] = None
+        for sl in slots:
+            for b in range(2):
+                if sl["pending"][b] is not None:
+                    sl["pending"][b].wait()
+                    sl["pending"][b] = None
 
     for _ in range(args.warmup):
         step()
@@ -262,6 +278,7 @@ def main():
             "data": "synthetic (seeded reads, SURVEY.md 8(d)); inputs resident in HBM",
             "config": {"workload": workload_name, "k": args.k, "sn_per_rank": args.sn, "sl": args.sl,
                        "lim": args.lim, "candidates": n_c, "kmer_bp_per_rank_step": units,
+                       "batches_in_flight": n_slots,
                        "parallelism": f"window shards x{world}, {'RCCL' if backend == 'nccl' else backend} "
                                       f"all-reduce of counts" if world > 1 else "1 GPU"},
             "kernel_ms": kern_ms,
@@ -297,7 +314,8 @@ def main():
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(wl, args.k, args.cpu_seconds)
         print(json.dumps(out), flush=True)
-    counter.close()
+    for sl in slots:
+        sl["counter"].close()
     if world > 1:
         dist.destroy_process_group()
 
