@@ -145,7 +145,12 @@ ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hi
     if (!ctx->resident[P]) AC_HIP(ctx, acamd::resident_waves(P, ctx->cu_count, &ctx->resident[P]));
     const uint64_t resident = ctx->resident[P];
     const uint32_t wpw = (uint32_t)std::max<uint64_t>(1, (items + resident - 1) / resident);
+#ifdef AC_FORCE_CHUNK  // A/B builds (tools/variants.sh): fixed item size
+    const uint32_t chunk = AC_FORCE_CHUNK;
+    (void)wpw;
+#else
     const uint32_t chunk = std::max<uint32_t>(1, std::min<uint32_t>(8, wpw / 64));
+#endif
     uint32_t groups_live = 0, max_nw = 1;
     for (uint32_t i = 0; i < n; ++i)
         if (segs[i].n_kmers && segs[i].sample.n_windows) {

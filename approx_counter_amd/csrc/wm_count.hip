@@ -126,6 +126,12 @@ __device__ __forceinline__ void build_masks(const uint64_t (&km)[P], uint32_t m,
 #include "wm_tid_blocks.inc"
 #endif
 
+// A wave-uniform 64-bit value kept in SGPRs.
+__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
+    return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
+           __builtin_amdgcn_readfirstlane((uint32_t)v);
+}
+
 // Per-wave ~Eq table: word c*64 + lane = the lane's ~Eq mask for character c
 // (A C G T, then N = all ones), read per base with ds_read_addtid_b32.
 struct TidTable {
@@ -256,7 +262,11 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
         return blocks / nqb + (qb < blocks % nqb ? 1u : 0u);
     };
     auto n_in = [&](uint32_t jj) { return jj < n_items ? (n_items - jj + S - 1u) / S : 0u; };  // items of jj
-    auto item_of = [&](uint32_t c) { return c < n_in(jc) ? jc + c * S : n_items; };
+    // Per-sub-queue constants of the served sub-queue, recomputed only when a
+    // steal changes it (their divisions are SALU sequences; with 1-window items
+    // they ran once per window).
+    uint32_t jc_waves = waves_in(jc), jc_items = n_in(jc);
+    auto item_of = [&](uint32_t c) { return c < jc_items ? jc + c * S : n_items; };
     auto dequeue_issue = [&]() -> uint32_t {  // lane 0 holds the result; read with readfirstlane
         uint32_t v = 0;
         if (lane == 0) v = __hip_atomic_fetch_add(counter(jc), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -285,8 +295,10 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
             if (found == S) return n_items;
             const uint32_t jj = (j + found) % S;
             jc = jj;
-            const uint32_t c = waves_in(jj) + __builtin_amdgcn_readfirstlane(dequeue_issue());
-            if (c < n_in(jj)) return jj + c * S;
+            jc_waves = waves_in(jj);
+            jc_items = n_in(jj);
+            const uint32_t c = jc_waves + __builtin_amdgcn_readfirstlane(dequeue_issue());
+            if (c < jc_items) return jj + c * S;
         }
     };
     uint32_t item = (j < n_items && eb_ok) ? item_of(rank) : n_items;
@@ -299,8 +311,8 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
     uint32_t nlen = 0;
     uint32_t nf = 0;
     if (item < n_items) {
-        nbase = sg.start[w];
-        nlen = sg.length[w];
+        nbase = uniform64(sg.start[w]);
+        nlen = __builtin_amdgcn_readfirstlane(sg.length[w]);
         if (valid(nbase, nlen)) nf = tid_fetch(sg.codes + (nbase >> 4), sg.nmask + (nbase >> 5), nlen, 0, lane);
     }
 
@@ -326,6 +338,10 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     stamp(wave, 1);
 
+    // Per window, the next window's three dependent global accesses (for an
+    // item's last window: claim -> descriptor -> first words; otherwise
+    // descriptor -> first words) are spread over the gaps between the window's
+    // first 32-base blocks, so none of them stalls the wave between windows.
     while (item < n_items) {
         const uint64_t base = nbase;
         const uint32_t len = nlen;
@@ -333,75 +349,87 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
         // issued: inside the chunk loop hipcc would otherwise wait for both.
         uint32_t f0 = nf;
         asm volatile("" : "+v"(f0));
-        // Within an item the next window is fetched while this one is counted.
-        // During an item's last window the next item is claimed (one returning
-        // atomic); it is read after the window, so a wave the arbiter starves
-        // never holds more than the item it is working on.
         const uint32_t wn = w + 1;
-        if (wn < item_end) {
-            nbase = sg.start[wn];
-            nlen = sg.length[wn];
-            if (valid(nbase, nlen)) nf = tid_fetch(sg.codes + (nbase >> 4), sg.nmask + (nbase >> 5), nlen, 0, lane);
+        const bool last = wn >= item_end;  // the item's last window: claim the next item
+        uint32_t nitem = n_items;
+        if (!last) {
+            nbase = uniform64(sg.start[wn]);
+            nlen = __builtin_amdgcn_readfirstlane(sg.length[wn]);
         } else {
             pending = dequeue_issue();
         }
-        if (valid(base, len)) {  // a malformed window is skipped: never read outside the image
+        const bool ok = valid(base, len);  // a malformed window is skipped: never read outside the image
+        const uint32_t nb0 = ok ? min(SEG, len) : 0u;
+        const uint32_t nfull0 = nb0 >> 4;
+        TidNfa s = {~0u, d1_init, d2_init, ~0u >> P, d1_init >> P, d2_init >> P, ~0u, d1_init, d2_init};
         const uint32_t* __restrict__ codes = sg.codes + (base >> 4);
         const uint32_t* __restrict__ nmask = sg.nmask + (base >> 5);
-        TidNfa s = {~0u, d1_init, d2_init, ~0u >> P, d1_init >> P, d2_init >> P, ~0u, d1_init, d2_init};
-        auto segment = [&](uint32_t f, uint32_t sb) {
-            const uint32_t nb = min(SEG, len - sb);
-            const uint32_t nfull = nb >> 4;
-#ifndef AC_BLOCK16_ONLY
-            // 32 bases per asm statement (half the per-block scalar overhead and
-            // pipeline fill), then at most one 16-base block.
-            uint32_t ch = 0;
-            for (; ch + 2u <= nfull; ch += 2u) {
-                const uint32_t code = __builtin_amdgcn_readlane(f, ch);
-                const uint32_t code2 = __builtin_amdgcn_readlane(f, ch + 1u);
-                const uint32_t nm = __builtin_amdgcn_readlane(f, 16u + (ch >> 1));
-                tid_block32<P, TID_EB0>(s, code, code2, nm, eb);
-            }
-            if (ch < nfull) {
-                const uint32_t code = __builtin_amdgcn_readlane(f, ch);
-                const uint32_t nm = (__builtin_amdgcn_readlane(f, 16u + (ch >> 1)) >> ((ch & 1u) * 16u)) & 0xffffu;
-                tid_block16<P, TID_EB0>(s, code, nm, eb);
-            }
-#else
-            for (uint32_t ch = 0; ch < nfull; ++ch) {
-                const uint32_t code = __builtin_amdgcn_readlane(f, ch);
-                const uint32_t nm = (__builtin_amdgcn_readlane(f, 16u + (ch >> 1)) >> ((ch & 1u) * 16u)) & 0xffffu;
-                tid_block16<P, TID_EB0>(s, code, nm, eb);
-            }
-#endif
-            if (nb & 15u) {
-                const uint32_t code = __builtin_amdgcn_readlane(f, nfull);
-                const uint32_t nm = (__builtin_amdgcn_readlane(f, 16u + (nfull >> 1)) >> ((nfull & 1u) * 16u)) & 0xffffu;
-                tid_tail<P>(s, code, nm, nb & 15u, eb);
-            }
+        auto block32 = [&](uint32_t f, uint32_t ch) __attribute__((always_inline)) {
+            const uint32_t code = __builtin_amdgcn_readlane(f, ch);
+            const uint32_t code2 = __builtin_amdgcn_readlane(f, ch + 1u);
+            const uint32_t nm = __builtin_amdgcn_readlane(f, 16u + (ch >> 1));
+            tid_block32<P, TID_EB0>(s, code, code2, nm, eb);
         };
-        segment(f0, 0u);
-        for (uint32_t sb = SEG; sb < len; sb += SEG) {  // windows longer than one segment
-            uint32_t f = tid_fetch(codes, nmask, len, sb, lane);
-            asm volatile("" : "+v"(f));
-            segment(f, sb);
+        // step 1 (after block 0): the claim's result -> the next item's descriptor,
+        // or the next window's first words
+        if (nfull0 >= 2u) block32(f0, 0u);
+        if (last) {
+            nitem = __builtin_amdgcn_readfirstlane(item_of(jc_waves + __builtin_amdgcn_readfirstlane(pending)));
+            if (nitem < n_items) {
+                nbase = uniform64(sg.start[nitem * chunk]);
+                nlen = __builtin_amdgcn_readfirstlane(sg.length[nitem * chunk]);
+            }
+        } else if (valid(nbase, nlen)) {
+            nf = tid_fetch(sg.codes + (nbase >> 4), sg.nmask + (nbase >> 5), nlen, 0, lane);
         }
+        // step 2 (after block 1): the next item's first words
+        if (nfull0 >= 4u) block32(f0, 2u);
+        if (last && nitem < n_items && valid(nbase, nlen))
+            nf = tid_fetch(sg.codes + (nbase >> 4), sg.nmask + (nbase >> 5), nlen, 0, lane);
+        if (ok) {
+            auto segment = [&](uint32_t f, uint32_t sb, uint32_t ch) __attribute__((always_inline)) {
+                const uint32_t nb = min(SEG, len - sb);
+                const uint32_t nfull = nb >> 4;
+                for (; ch + 2u <= nfull; ch += 2u) block32(f, ch);
+                if (ch < nfull) {
+                    const uint32_t code = __builtin_amdgcn_readlane(f, ch);
+                    const uint32_t nm = (__builtin_amdgcn_readlane(f, 16u + (ch >> 1)) >> ((ch & 1u) * 16u)) & 0xffffu;
+                    tid_block16<P, TID_EB0>(s, code, nm, eb);
+                }
+                if (nb & 15u) {
+                    const uint32_t code = __builtin_amdgcn_readlane(f, nfull);
+                    const uint32_t nm = (__builtin_amdgcn_readlane(f, 16u + (nfull >> 1)) >> ((nfull & 1u) * 16u)) & 0xffffu;
+                    tid_tail<P>(s, code, nm, nb & 15u, eb);
+                }
+            };
+            segment(f0, 0u, nfull0 >= 4u ? 4u : (nfull0 >= 2u ? 2u : 0u));
+            for (uint32_t sb = SEG; sb < len; sb += SEG) {  // windows longer than one segment
+                uint32_t f = tid_fetch(codes, nmask, len, sb, lane);
+                asm volatile("" : "+v"(f));
+                segment(f, sb, 0u);
+            }
 #pragma unroll
-        for (int p = 0; p < P; ++p) {
-            const uint32_t lb = 31u - ((m - 1u) * P + (uint32_t)p);
-            cnt[p] += 3u - ((s.a0 >> lb) & 1u) - ((s.a1 >> lb) & 1u) - ((s.a2 >> lb) & 1u);
+            for (int p = 0; p < P; ++p) {
+                const uint32_t lb = 31u - ((m - 1u) * P + (uint32_t)p);
+                cnt[p] += 3u - ((s.a0 >> lb) & 1u) - ((s.a1 >> lb) & 1u) - ((s.a2 >> lb) & 1u);
+            }
         }
-        }  // valid window
-        // advance the cursor; at an item boundary move to the prefetched item and request another
+        // advance the cursor; at an item boundary move to the claimed item
+        // (descriptor and first words already requested) or steal one
         if (++w >= item_end) {
-            item = item_of(waves_in(jc) + __builtin_amdgcn_readfirstlane(pending));
-            if (item >= n_items && S > 1) item = steal();
+            item = nitem;
+            if (item >= n_items && S > 1) {
+                item = __builtin_amdgcn_readfirstlane(steal());
+                if (item < n_items) {
+                    nbase = uniform64(sg.start[item * chunk]);
+                    nlen = __builtin_amdgcn_readfirstlane(sg.length[item * chunk]);
+                    if (valid(nbase, nlen))
+                        nf = tid_fetch(sg.codes + (nbase >> 4), sg.nmask + (nbase >> 5), nlen, 0, lane);
+                }
+            }
             if (item < n_items) {
                 w = item * chunk;
                 item_end = min(sg.n_windows, w + chunk);
-                nbase = sg.start[w];
-                nlen = sg.length[w];
-                if (valid(nbase, nlen)) nf = tid_fetch(sg.codes + (nbase >> 4), sg.nmask + (nbase >> 5), nlen, 0, lane);
             }
         }
     }
