@@ -82,6 +82,10 @@ def main():
     active = np.zeros((keys.size, grid.size))
     for i in range(n):
         active[inv[i]] += (grid >= us[i, 0]) & (grid < us[i, 3])
+    # waves past the prologue (counting) per SIMD during the launch ramp
+    for t in (2, 5, 10, 20, 30):
+        counting = ((us[:, 1] <= t) & (us[:, 2] > t)).sum() / keys.size
+        print(f"t={t:3d} us: counting waves per SIMD {counting:.2f}")
     print("mean resident waves per SIMD at 10%..90% of the kernel:",
           [round(float(active[:, int(f * 199)].mean()), 2) for f in (0.1, 0.3, 0.5, 0.7, 0.8, 0.9, 0.95)])
 
