@@ -240,7 +240,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
     // with a static split the first waves finish early and the last ones run
     // with few partners (profiles/r01_kernel_log.md).  Instead each candidate
     // group's items (`chunk` windows each) are spread over `subq` sub-queues
-    // (item j + c*subq belongs to sub-queue j), each a counter on its own
+    // (contiguous ranges, see `first_of` below), each a counter on its own
     // 128-B line; a wave's first item is assigned statically, further ones
     // are claimed one at a time (below).  Waves are dealt to sub-queues
     // round-robin, so every sub-queue serves a mix of old and young waves;
@@ -261,12 +261,27 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
         const uint32_t qb = qq / WAVES_PER_BLOCK;  // one wave of every workgroup dealt to block-queue qb
         return blocks / nqb + (qb < blocks % nqb ? 1u : 0u);
     };
-    auto n_in = [&](uint32_t jj) { return jj < n_items ? (n_items - jj + S - 1u) / S : 0u; };  // items of jj
+#ifndef AC_STRIDED_ITEMS
+    // Sub-queue jj holds the contiguous items [first(jj), first(jj) + n_in(jj)):
+    // a workgroup's sub-queues are consecutive and its XCD is fixed, so each
+    // XCD's L2 fetches a slice of the sample instead of all of it, and
+    // neighbouring windows (which share cache lines) are counted together.
+    const uint32_t q_items = n_items / S, r_items = n_items % S;
+    auto n_in = [&](uint32_t jj) { return q_items + (jj < r_items ? 1u : 0u); };
+    auto first_of = [&](uint32_t jj) { return jj * q_items + min(jj, r_items); };
+#else  // A/B: item jj + c*S in sub-queue jj
+    auto n_in = [&](uint32_t jj) { return jj < n_items ? (n_items - jj + S - 1u) / S : 0u; };
+#endif
     // Per-sub-queue constants of the served sub-queue, recomputed only when a
     // steal changes it (their divisions are SALU sequences; with 1-window items
     // they ran once per window).
     uint32_t jc_waves = waves_in(jc), jc_items = n_in(jc);
+#ifndef AC_STRIDED_ITEMS
+    uint32_t jc_first = first_of(jc);
+    auto item_of = [&](uint32_t c) { return c < jc_items ? jc_first + c : n_items; };
+#else
     auto item_of = [&](uint32_t c) { return c < jc_items ? jc + c * S : n_items; };
+#endif
     auto dequeue_issue = [&]() -> uint32_t {  // lane 0 holds the result; read with readfirstlane
         uint32_t v = 0;
         if (lane == 0) v = __hip_atomic_fetch_add(counter(jc), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -297,8 +312,11 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
             jc = jj;
             jc_waves = waves_in(jj);
             jc_items = n_in(jj);
+#ifndef AC_STRIDED_ITEMS
+            jc_first = first_of(jj);
+#endif
             const uint32_t c = jc_waves + __builtin_amdgcn_readfirstlane(dequeue_issue());
-            if (c < jc_items) return jj + c * S;
+            if (c < jc_items) return item_of(c);
         }
     };
     uint32_t item = (j < n_items && eb_ok) ? item_of(rank) : n_items;
