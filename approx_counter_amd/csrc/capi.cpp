@@ -96,6 +96,46 @@ ac_status grow(ac_ctx* ctx, void** buf, size_t* cap, size_t bytes) {
 
 ac_status ensure(ac_ctx* ctx, int slot, size_t bytes) { return grow(ctx, &ctx->d_buf[slot], &ctx->d_cap[slot], bytes); }
 
+// Host -> device copy of n host arrays through the context's pinned staging
+// block.  Array i lands at offset off(i) = sum of the earlier sizes rounded up
+// to 256 B, in the staging block and in the device block `dst` alike.  The
+// block is filled and sent in 1 MB pieces, each piece's DMA queued as soon as
+// it is filled, so the CPU fills the next piece while the previous one crosses
+// PCIe (pageable copies, one per array, each paid the driver's own staging
+// overhead; one DMA per array instead of per piece cost 70 us more at cfg2).
+// Asynchronous on ctx->stream; the block is reused by the next call, so callers
+// synchronise the stream before returning.  `extra` bytes after the arrays are
+// reserved (the counts' way back).
+size_t staged_bytes(int n, const size_t* sz) {
+    size_t total = 0;
+    for (int i = 0; i < n; ++i) total += (sz[i] + 255) / 256 * 256;
+    return total;
+}
+
+ac_status h2d_staged(ac_ctx* ctx, int n, const void* const* src, const size_t* sz, void* dst, size_t extra = 0) {
+    const size_t in_bytes = staged_bytes(n, sz), total = in_bytes + extra;
+    if (ctx->h_stage_cap < total) {
+        if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
+        ctx->h_stage = nullptr;
+        ctx->h_stage_cap = 0;
+        AC_HIP(ctx, hipHostMalloc(&ctx->h_stage, total, hipHostMallocDefault));
+        ctx->h_stage_cap = total;
+    }
+    constexpr size_t CHUNK = size_t(1) << 20;
+    char* h = (char*)ctx->h_stage;
+    for (size_t c0 = 0; c0 < in_bytes; c0 += CHUNK) {
+        const size_t c1 = std::min(in_bytes, c0 + CHUNK);
+        size_t off = 0;
+        for (int i = 0; i < n; ++i) {
+            const size_t lo = std::max(c0, off), hi = std::min(c1, off + sz[i]);
+            if (lo < hi) std::memcpy(h + lo, (const char*)src[i] + (lo - off), hi - lo);
+            off += (sz[i] + 255) / 256 * 256;
+        }
+        AC_HIP(ctx, hipMemcpyAsync((char*)dst + c0, h + c0, c1 - c0, hipMemcpyHostToDevice, ctx->stream));
+    }
+    return AC_OK;
+}
+
 // getComplexity (approx_counter.cpp:247-267) and CompareCount (275-305), for the
 // final ranking of the exact count's short list.
 float complexity(uint64_t kmer, uint32_t k) {
@@ -361,10 +401,8 @@ ac_status error_count_one(ac_ctx* ctx, uint32_t k, const uint64_t* kmers, uint32
             return fail(ctx, AC_ERR_INVALID, "window " + std::to_string(i) + " is misaligned or outside the image");
     }
     AC_HIP(ctx, hipSetDevice(ctx->device));
-    // One staging block: kmers | codes | nmask | start | length | counts, each
-    // 256-B aligned.  The inputs are copied into pinned memory and cross PCIe in
-    // 1 MB DMAs (five pageable copies each paid the driver's staging overhead);
-    // the counts come back into the same block.
+    // Device block: kmers | codes | nmask | start | length | counts, each
+    // 256-B aligned, filled through the pinned staging block (h2d_staged).
     const size_t sz[6] = {sizeof(uint64_t) * n_kmers, sizeof(uint32_t) * (s.n_bases / 16),
                           sizeof(uint32_t) * (s.n_bases / 32), sizeof(uint64_t) * s.n_windows,
                           sizeof(uint32_t) * s.n_windows, sizeof(uint32_t) * n_kmers};
@@ -372,29 +410,12 @@ ac_status error_count_one(ac_ctx* ctx, uint32_t k, const uint64_t* kmers, uint32
     size_t off[7];
     off[0] = 0;
     for (int i = 0; i < 6; ++i) off[i + 1] = (off[i] + sz[i] + 255) / 256 * 256;
-    const size_t in_bytes = off[5], total = off[6];
-    if (ctx->h_stage_cap < total) {
-        if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
-        ctx->h_stage = nullptr;
-        ctx->h_stage_cap = 0;
-        AC_HIP(ctx, hipHostMalloc(&ctx->h_stage, total, hipHostMallocDefault));
-        ctx->h_stage_cap = total;
-    }
-    if (ac_status rc = grow(ctx, &ctx->d_stage, &ctx->d_stage_cap, total)) return rc;
-    char* h = (char*)ctx->h_stage;
+    if (ac_status rc = grow(ctx, &ctx->d_stage, &ctx->d_stage_cap, off[6])) return rc;
     char* d = (char*)ctx->d_stage;
+    // the counts come back into the staging block, after the inputs
+    if (ac_status rc = h2d_staged(ctx, 5, src, sz, d, (sz[5] + 255) / 256 * 256)) return rc;
+    char* h = (char*)ctx->h_stage;
     hipStream_t st = ctx->stream;
-    // Pipelined: the CPU fills chunk c + 1 of the pinned block while chunk c
-    // crosses PCIe (a single memcpy-then-DMA cost their sum: +6 % at cfg3).
-    constexpr size_t CHUNK = size_t(1) << 20;
-    for (size_t c0 = 0; c0 < in_bytes; c0 += CHUNK) {
-        const size_t c1 = std::min(in_bytes, c0 + CHUNK);
-        for (int i = 0; i < 5; ++i) {
-            const size_t lo = std::max(c0, off[i]), hi = std::min(c1, off[i] + sz[i]);
-            if (lo < hi) std::memcpy(h + lo, (const char*)src[i] + (lo - off[i]), hi - lo);
-        }
-        AC_HIP(ctx, hipMemcpyAsync(d + c0, h + c0, c1 - c0, hipMemcpyHostToDevice, st));
-    }
     ac_segment seg;
     seg.kmers = (const uint64_t*)(d + off[0]);
     seg.n_kmers = n_kmers;
@@ -527,15 +548,21 @@ ac_status ac_sample_upload(ac_ctx* ctx, const ac_windows* host, ac_windows* dev)
     const size_t sz[4] = {sizeof(uint32_t) * (host->n_bases / 16), sizeof(uint32_t) * (host->n_bases / 32),
                           sizeof(uint64_t) * host->n_windows, sizeof(uint32_t) * host->n_windows};
     const void* src[4] = {host->codes, host->nmask, host->start, host->length};
-    for (int i = 0; i < 4; ++i) {
-        if (ac_status st = grow(ctx, &ctx->s_buf[i], &ctx->s_cap[i], sz[i])) return st;
-        if (sz[i]) AC_HIP(ctx, hipMemcpyAsync(ctx->s_buf[i], src[i], sz[i], hipMemcpyHostToDevice, ctx->stream));
-    }
+    // one device block (s_buf[0]) holding the four arrays at the staging offsets
+    if (ac_status st = grow(ctx, &ctx->s_buf[0], &ctx->s_cap[0], staged_bytes(4, sz))) return st;
+    if (ac_status st = h2d_staged(ctx, 4, src, sz, ctx->s_buf[0])) return st;
     AC_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    dev->codes = (const uint32_t*)ctx->s_buf[0];
-    dev->nmask = (const uint32_t*)ctx->s_buf[1];
-    dev->start = (const uint64_t*)ctx->s_buf[2];
-    dev->length = (const uint32_t*)ctx->s_buf[3];
+    const char* blk = (const char*)ctx->s_buf[0];
+    size_t off = 0;
+    const void* at[4];
+    for (int i = 0; i < 4; ++i) {
+        at[i] = blk + off;
+        off += (sz[i] + 255) / 256 * 256;
+    }
+    dev->codes = (const uint32_t*)at[0];
+    dev->nmask = (const uint32_t*)at[1];
+    dev->start = (const uint64_t*)at[2];
+    dev->length = (const uint32_t*)at[3];
     dev->n_windows = host->n_windows;
     dev->n_bases = host->n_bases;
     return AC_OK;
