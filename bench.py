@@ -76,6 +76,8 @@ def parse():
     ap.add_argument("--inflight", type=int, default=1,
                     help="batches in flight: independent counter contexts on their own HIP streams, "
                          "steps dealt round-robin, so one batch's launch tail overlaps the next one's start")
+    ap.add_argument("--no-inflight-probe", action="store_true",
+                    help="skip the informational two-batches-in-flight timing of a 1-GPU run")
     ap.add_argument("--verify", action="store_true", help="check counts against the oracle (slow)")
     ap.add_argument("--event-every", type=int, default=5,
                     help="bracket every N-th timed launch with HIP events (the kernel-duration sample); "
@@ -159,12 +161,15 @@ def main():
     packed = {e: ac.pack_windows(wl[e]["windows"]) for e in ends}
     base_segs = [ac.DeviceSegment.upload(wl[e]["kmers"], packed[e], device=dev) for e in ends]
     n_slots = max(1, args.inflight)
+    # rank 0 of a 1-GPU run also times two batches in flight (informational `inflight_2`)
+    extra_slot = world == 1 and n_slots == 1 and not args.no_inflight_probe
+    n_build = n_slots + (1 if extra_slot else 0)
     # One slot per batch in flight: its own counter context (device scratch, queue counters),
     # its own stream and two count vectors.  With N > 1 ranks the RCCL all-reduce of a slot's
     # step runs on the communicator's stream while that slot counts its next step into the
     # other vector.
     slots = []
-    for si in range(n_slots):
+    for si in range(n_build):
         counter_s = ac.ApproxCounter(local)
         st = torch.cuda.current_stream(dev) if si == 0 else torch.cuda.Stream(dev)
         bufs = [torch.zeros(sum(n_c), dtype=torch.int32, device=dev) for _ in range(2)]
@@ -189,8 +194,10 @@ def main():
 
     n_step = [0]
 
+    active = [n_slots]
+
     def step(i=None):
-        sl = slots[n_step[0] % n_slots]
+        sl = slots[n_step[0] % active[0]]
         n_step[0] += 1
         b = sl["n"] % 2
         sl["n"] += 1
@@ -311,6 +318,24 @@ def main():
             out["host_boundary"] = {"value": units / host_s, "unit": "kmer*bp/s", "ms_per_step": host_s * 1e3,
                                     "note": "ac_error_count with host buffers (PCIe-inclusive: H2D of the 2-bit "
                                             "sample + candidates, kernel, D2H of counts), both ends, synchronous"}
+        if extra_slot:
+            # Two batches in flight: the same steps dealt alternately to two counter contexts on
+            # two streams, so one launch's tail overlaps the next one's start.
+            # Reported beside `value` (which keeps one batch in flight and per-launch kernel
+            # times), never as it.
+            active[0] = 2
+            for _ in range(args.warmup):
+                step()
+            torch.cuda.synchronize(dev)
+            t2 = time.perf_counter()
+            for _ in range(args.steps):
+                step()
+            torch.cuda.synchronize(dev)
+            el2 = time.perf_counter() - t2
+            active[0] = n_slots
+            out["inflight_2"] = {"value": units * args.steps / el2, "unit": "kmer*bp/s",
+                                 "ms_per_step": el2 / args.steps * 1e3,
+                                 "note": "2 batches in flight (2 contexts, 2 streams), same steps and workload"}
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(wl, args.k, args.cpu_seconds)
         print(json.dumps(out), flush=True)
