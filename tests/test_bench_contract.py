@@ -1,0 +1,31 @@
+"""bench.py's driver contract, checked on CPU: the default workload is BASELINE.json's
+headline configuration (configs[1]) and the metric string is BASELINE.json's."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+
+def test_metric_is_baselines():
+    with open(os.path.join(ROOT, "BASELINE.json")) as f:
+        base = json.load(f)
+    assert bench.METRIC == base["metric"]
+
+
+def test_default_workload_is_cfg2(monkeypatch):
+    monkeypatch.setattr(sys, "argv", ["bench.py"])
+    a = bench.parse()
+    assert (a.gpus, a.k, a.sn, a.sl, a.lim) == (1, 16, 10_000, 100, 500)
+    assert a.inflight == 1  # the headline value keeps one batch in flight
+    assert a.steps > 0 and a.warmup >= 0
+
+
+def test_config_overrides(monkeypatch):
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--config", "cfg5", "--steps", "3", "--warmup", "1"])
+    a = bench.parse()
+    assert (a.k, a.sn, a.sl, a.lim, a.steps, a.warmup) == (22, 100_000, 150, 1000, 3, 1)
+    assert a.read_len >= 2 * a.sl  # every read long enough for both ends
