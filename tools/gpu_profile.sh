@@ -4,7 +4,7 @@
 # usage (on the box, from the repo root): tools/gpu_profile.sh TAG [bench args...]
 TAG=$1; shift
 D=$GRAFT_REPO_ROOT/gpurun_out/$TAG
-B="python3 $GRAFT_REPO_ROOT/bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-host-boundary $*"
+B="python3 $GRAFT_REPO_ROOT/bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-host-boundary --no-inflight-probe $*"
 P="cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3"
 exec tools/gpu_run.sh $TAG \
   "timeout -k 10 600 python -m pytest tests -m gpu -q -x" \
