@@ -126,10 +126,22 @@ __device__ __forceinline__ void build_masks(const uint64_t (&km)[P], uint32_t m,
 #include "wm_tid_blocks.inc"
 #endif
 
-// A wave-uniform 64-bit value kept in SGPRs.
-__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
-    return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
-           __builtin_amdgcn_readfirstlane((uint32_t)v);
+// Window descriptor (start, length) of window w with scalar loads: the arrays
+// do not change during a launch, so the constant address space is legal, and
+// both loads are in flight together (as vector loads hipcc waited for the
+// start before issuing the length: two round trips per window).
+typedef const __attribute__((address_space(4))) uint64_t* cu64p;
+typedef const __attribute__((address_space(4))) uint32_t* cu32p;
+__device__ __forceinline__ void load_desc(const uint64_t* start, const uint32_t* length, uint32_t w, uint64_t& base,
+                                          uint32_t& len) {
+#ifndef AC_VECTOR_DESC
+    base = ((cu64p)start)[w];
+    len = ((cu32p)length)[w];
+#else
+    base = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(start[w] >> 32)) << 32) |
+           __builtin_amdgcn_readfirstlane((uint32_t)start[w]);
+    len = __builtin_amdgcn_readfirstlane(length[w]);
+#endif
 }
 
 // Per-wave ~Eq table: word c*64 + lane = the lane's ~Eq mask for character c
@@ -329,8 +341,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
     uint32_t nlen = 0;
     uint32_t nf = 0;
     if (item < n_items) {
-        nbase = uniform64(sg.start[w]);
-        nlen = __builtin_amdgcn_readfirstlane(sg.length[w]);
+        load_desc(sg.start, sg.length, w, nbase, nlen);
         if (valid(nbase, nlen)) nf = tid_fetch(sg.codes + (nbase >> 4), sg.nmask + (nbase >> 5), nlen, 0, lane);
     }
 
@@ -371,8 +382,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
         const bool last = wn >= item_end;  // the item's last window: claim the next item
         uint32_t nitem = n_items;
         if (!last) {
-            nbase = uniform64(sg.start[wn]);
-            nlen = __builtin_amdgcn_readfirstlane(sg.length[wn]);
+            load_desc(sg.start, sg.length, wn, nbase, nlen);
         } else {
             pending = dequeue_issue();
         }
@@ -394,8 +404,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
         if (last) {
             nitem = __builtin_amdgcn_readfirstlane(item_of(jc_waves + __builtin_amdgcn_readfirstlane(pending)));
             if (nitem < n_items) {
-                nbase = uniform64(sg.start[nitem * chunk]);
-                nlen = __builtin_amdgcn_readfirstlane(sg.length[nitem * chunk]);
+                load_desc(sg.start, sg.length, nitem * chunk, nbase, nlen);
             }
         } else if (valid(nbase, nlen)) {
             nf = tid_fetch(sg.codes + (nbase >> 4), sg.nmask + (nbase >> 5), nlen, 0, lane);
@@ -439,8 +448,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
             if (item >= n_items && S > 1) {
                 item = __builtin_amdgcn_readfirstlane(steal());
                 if (item < n_items) {
-                    nbase = uniform64(sg.start[item * chunk]);
-                    nlen = __builtin_amdgcn_readfirstlane(sg.length[item * chunk]);
+                    load_desc(sg.start, sg.length, item * chunk, nbase, nlen);
                     if (valid(nbase, nlen))
                         nf = tid_fetch(sg.codes + (nbase >> 4), sg.nmask + (nbase >> 5), nlen, 0, lane);
                 }
