@@ -221,6 +221,24 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
     // A group's sub-queues are contiguous (g * subq + j), so a workgroup's
     // sub-queues lie in one group.
     const uint32_t g = ql / sg.subq, j = ql % sg.subq;
+    // The segment's arrays, pinned in SGPRs for the whole launch: read through the `sg` reference hipcc reloaded them from
+    // the kernel arguments in every window, each load waited for on the spot.
+    // (codes / nmask kept as global-address-space pointers: an opaque generic
+    // pointer would make the window fetches flat loads, which also count in
+    // lgkmcnt and so would be waited for by the NFA blocks' LDS waits)
+    typedef const __attribute__((address_space(1))) uint32_t* gu32p;
+    gu32p g_codes_g = (gu32p)sg.codes;
+    gu32p g_nmask_g = (gu32p)sg.nmask;
+    const uint64_t* g_start = sg.start;
+    const uint32_t* g_length = sg.length;
+    uint64_t g_nbases = sg.n_bases;
+    // (the claim counters stay addressed from the kernel argument: an opaque
+    // pointer would turn the claim into a flat atomic, which also counts in
+    // lgkmcnt and so would be waited for by the NFA blocks' LDS waits)
+    uint32_t* g_queue = a.queue + ((uint64_t)a.bank * a.qstride + sg.queue_begin + g * sg.subq) * AC_QUEUE_LINE;
+    asm volatile("" : "+s"(g_codes_g), "+s"(g_nmask_g), "+s"(g_start), "+s"(g_length), "+s"(g_nbases));
+    const uint32_t* g_codes = (const uint32_t*)g_codes_g;
+    const uint32_t* g_nmask = (const uint32_t*)g_nmask_g;
     const uint32_t m = a.m;
 
     uint32_t cand[P];
@@ -266,7 +284,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
     const uint32_t n_items = (sg.n_windows + chunk - 1u) / chunk;
     uint32_t jc = j;  // sub-queue currently served
     auto counter = [&](uint32_t jj) {
-        return a.queue + ((uint64_t)a.bank * a.qstride + sg.queue_begin + g * sg.subq + jj) * AC_QUEUE_LINE;
+        return g_queue + (uint64_t)jj * AC_QUEUE_LINE;
     };
     auto waves_in = [&](uint32_t jj) {  // waves dealt to sub-queue (g, jj): their first items are static
         const uint32_t qq = sg.queue_begin + g * sg.subq + jj;
@@ -336,13 +354,13 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
     uint32_t w = item * chunk, item_end = min(sg.n_windows, w + chunk);
 
     // Window pipeline: the next window's first segment is fetched while the current one is counted.
-    auto valid = [&](uint64_t base, uint32_t len) { return !(base & 31u) && base + len <= sg.n_bases; };
+    auto valid = [&](uint64_t base, uint32_t len) { return !(base & 31u) && base + len <= g_nbases; };
     uint64_t nbase = 0;
     uint32_t nlen = 0;
     uint32_t nf = 0;
     if (item < n_items) {
-        load_desc(sg.start, sg.length, w, nbase, nlen);
-        if (valid(nbase, nlen)) nf = tid_fetch(sg.codes + (nbase >> 4), sg.nmask + (nbase >> 5), nlen, 0, lane);
+        load_desc(g_start, g_length, w, nbase, nlen);
+        if (valid(nbase, nlen)) nf = tid_fetch(g_codes + (nbase >> 4), g_nmask + (nbase >> 5), nlen, 0, lane);
     }
 
     // ~Eq table, built by wave 0 of the workgroup (the waves share the
@@ -382,7 +400,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
         const bool last = wn >= item_end;  // the item's last window: claim the next item
         uint32_t nitem = n_items;
         if (!last) {
-            load_desc(sg.start, sg.length, wn, nbase, nlen);
+            load_desc(g_start, g_length, wn, nbase, nlen);
         } else {
             pending = dequeue_issue();
         }
@@ -390,8 +408,8 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
         const uint32_t nb0 = ok ? min(SEG, len) : 0u;
         const uint32_t nfull0 = nb0 >> 4;
         TidNfa s = {~0u, d1_init, d2_init, ~0u >> P, d1_init >> P, d2_init >> P, ~0u, d1_init, d2_init};
-        const uint32_t* __restrict__ codes = sg.codes + (base >> 4);
-        const uint32_t* __restrict__ nmask = sg.nmask + (base >> 5);
+        const uint32_t* __restrict__ codes = g_codes + (base >> 4);
+        const uint32_t* __restrict__ nmask = g_nmask + (base >> 5);
         auto block32 = [&](uint32_t f, uint32_t ch) __attribute__((always_inline)) {
             const uint32_t code = __builtin_amdgcn_readlane(f, ch);
             const uint32_t code2 = __builtin_amdgcn_readlane(f, ch + 1u);
@@ -404,15 +422,15 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
         if (last) {
             nitem = __builtin_amdgcn_readfirstlane(item_of(jc_waves + __builtin_amdgcn_readfirstlane(pending)));
             if (nitem < n_items) {
-                load_desc(sg.start, sg.length, nitem * chunk, nbase, nlen);
+                load_desc(g_start, g_length, nitem * chunk, nbase, nlen);
             }
         } else if (valid(nbase, nlen)) {
-            nf = tid_fetch(sg.codes + (nbase >> 4), sg.nmask + (nbase >> 5), nlen, 0, lane);
+            nf = tid_fetch(g_codes + (nbase >> 4), g_nmask + (nbase >> 5), nlen, 0, lane);
         }
         // step 2 (after block 1): the next item's first words
         if (nfull0 >= 4u) block32(f0, 2u);
         if (last && nitem < n_items && valid(nbase, nlen))
-            nf = tid_fetch(sg.codes + (nbase >> 4), sg.nmask + (nbase >> 5), nlen, 0, lane);
+            nf = tid_fetch(g_codes + (nbase >> 4), g_nmask + (nbase >> 5), nlen, 0, lane);
         if (ok) {
             auto segment = [&](uint32_t f, uint32_t sb, uint32_t ch) __attribute__((always_inline)) {
                 const uint32_t nb = min(SEG, len - sb);
@@ -448,9 +466,9 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
             if (item >= n_items && S > 1) {
                 item = __builtin_amdgcn_readfirstlane(steal());
                 if (item < n_items) {
-                    load_desc(sg.start, sg.length, item * chunk, nbase, nlen);
+                    load_desc(g_start, g_length, item * chunk, nbase, nlen);
                     if (valid(nbase, nlen))
-                        nf = tid_fetch(sg.codes + (nbase >> 4), sg.nmask + (nbase >> 5), nlen, 0, lane);
+                        nf = tid_fetch(g_codes + (nbase >> 4), g_nmask + (nbase >> 5), nlen, 0, lane);
                 }
             }
             if (item < n_items) {
