@@ -15,8 +15,8 @@ LIBDIR := $(PKG)/lib
 LIB := $(LIBDIR)/libapprox_counter_amd.so
 OBJDIR := build/obj
 
-DEV_SRC := $(CSRC)/wm_count.hip $(CSRC)/exact_count.hip $(CSRC)/capi.cpp
-HDRS := include/approx_counter_amd.h $(CSRC)/wm_count.h $(CSRC)/exact_count.h
+DEV_SRC := $(CSRC)/wm_count.hip $(CSRC)/exact_count.hip $(CSRC)/capi.cpp $(CSRC)/host_pack.cpp
+HDRS := include/approx_counter_amd.h $(CSRC)/wm_count.h $(CSRC)/exact_count.h $(CSRC)/host_pack.h
 
 CXX ?= g++
 HOST_CXXFLAGS ?= -O3 -std=c++17 -fPIC -Wall -Wextra
@@ -41,9 +41,14 @@ $(OBJDIR)/capi.o: $(CSRC)/capi.cpp $(HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -x hip -Iinclude -I$(CSRC) -c $< -o $@
 
-$(LIB): $(OBJDIR)/wm_count.o $(OBJDIR)/exact_count.o $(OBJDIR)/capi.o
+# host staging (worker pool + AVX2 packer): plain host C++, no device code
+$(OBJDIR)/host_pack.o: $(CSRC)/host_pack.cpp $(CSRC)/host_pack.h
+	@mkdir -p $(OBJDIR)
+	$(CXX) $(HOST_CXXFLAGS) -c $< -o $@
+
+$(LIB): $(OBJDIR)/wm_count.o $(OBJDIR)/exact_count.o $(OBJDIR)/capi.o $(OBJDIR)/host_pack.o
 	@mkdir -p $(LIBDIR)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -pthread
 
 $(HOSTLIB): $(HOST_SRC) $(HOSTDIR)/host_capi.cpp $(HOST_HDRS)
 	@mkdir -p $(LIBDIR)

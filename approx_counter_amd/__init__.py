@@ -5,9 +5,9 @@ The compute path is the HIP kernel behind the C ABI in
 include/approx_counter_amd.h; this package is the host-side mirror of the
 reference interface for that path (see counter.error_count).
 """
-from .counter import (ApproxCounter, DeviceSegment, PackedSample, error_count, pack_windows,
-                      to_dna5)
+from .counter import (ApproxCounter, DeviceSegment, Dna5Sample, Jobs, PackedSample, error_count,
+                      pack_windows, to_dna5)
 from ._lib import ApproxCounterError
 
-__all__ = ["ApproxCounter", "ApproxCounterError", "DeviceSegment", "PackedSample", "error_count",
-           "pack_windows", "to_dna5"]
+__all__ = ["ApproxCounter", "ApproxCounterError", "DeviceSegment", "Dna5Sample", "Jobs", "PackedSample",
+           "error_count", "pack_windows", "to_dna5"]

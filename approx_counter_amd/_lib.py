@@ -18,6 +18,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "approx_counter_am
 
 AC_OK, AC_ERR_INVALID, AC_ERR_DEVICE, AC_ERR_NOMEM, AC_ERR_INTERNAL = 0, 1, 2, 3, 4
 AC_MAX_SEGS = 4
+AC_MAX_JOBS = 4
 
 p32 = ctypes.POINTER(ctypes.c_uint32)
 p64 = ctypes.POINTER(ctypes.c_uint64)
@@ -32,6 +33,14 @@ class ACWindows(ctypes.Structure):
 class ACSegment(ctypes.Structure):
     _fields_ = [("kmers", p64), ("n_kmers", ctypes.c_uint32), ("sample", ACWindows),
                 ("counts", p32)]
+
+
+class ACDna5Windows(ctypes.Structure):
+    _fields_ = [("bases", p8), ("offset", p64), ("length", p32), ("n_windows", ctypes.c_uint32)]
+
+
+class ACJob(ctypes.Structure):
+    _fields_ = [("kmers", p64), ("n_kmers", ctypes.c_uint32), ("sample", ACDna5Windows), ("counts", p64)]
 
 
 class ApproxCounterError(RuntimeError):
@@ -95,6 +104,12 @@ def load():
     L.ac_count.argtypes = [vp, ctypes.c_uint32, p64, ctypes.c_uint32, p32, p32, p64,
                            ctypes.POINTER(ctypes.c_uint16), ctypes.c_uint32, p64]
     L.ac_count.restype = ctypes.c_int
+    L.ac_error_count_jobs.argtypes = [vp, ctypes.c_uint32, ctypes.POINTER(ACJob), ctypes.c_uint32]
+    L.ac_error_count_jobs.restype = ctypes.c_int
+    L.ac_error_count_jobs_submit.argtypes = [vp, ctypes.c_uint32, ctypes.POINTER(ACJob), ctypes.c_uint32, p32, vp]
+    L.ac_error_count_jobs_submit.restype = ctypes.c_int
+    L.ac_check.argtypes = [vp, vp]
+    L.ac_check.restype = ctypes.c_int
     _lib = L
     return L
 

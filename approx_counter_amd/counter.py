@@ -15,7 +15,7 @@ import ctypes
 import numpy as np
 
 from . import _lib
-from ._lib import ACSegment, ACWindows, check
+from ._lib import ACDna5Windows, ACJob, ACSegment, ACWindows, check
 
 _DNA5 = np.full(256, 4, dtype=np.uint8)
 for _c, _v in ((b"A", 0), (b"C", 1), (b"G", 2), (b"T", 3), (b"U", 3)):
@@ -93,6 +93,71 @@ def pack_windows(windows) -> PackedSample:
     return PackedSample(codes, nmask, out_start[: len(arrs)], out_len[: len(arrs)], n_bases)
 
 
+class Dna5Sample:
+    """A sample as errorCount receives it: a StringSet<Dna5String>
+    (approx_counter.cpp:38), i.e. Dna5 ordinal bytes concatenated, with each
+    window's offset and length (ac_dna5_windows)."""
+
+    def __init__(self, bases, offset, length):
+        self.bases = np.ascontiguousarray(bases, dtype=np.uint8)
+        self.offset = np.ascontiguousarray(offset, dtype=np.uint64)
+        self.length = np.ascontiguousarray(length, dtype=np.uint32)
+        if self.bases.size == 0:
+            self.bases = np.zeros(1, np.uint8)
+
+    @classmethod
+    def from_windows(cls, windows) -> "Dna5Sample":
+        """From a sequence of strings / Dna5 arrays, or a 2-D uint8 array of
+        equal-length windows (one per row)."""
+        if isinstance(windows, np.ndarray) and windows.ndim == 2:
+            n, wl = windows.shape
+            return cls(windows.reshape(-1), np.arange(n, dtype=np.uint64) * np.uint64(wl),
+                       np.full(n, wl, dtype=np.uint32))
+        arrs = [to_dna5(w) for w in windows]
+        length = np.array([a.size for a in arrs], dtype=np.uint32)
+        offset = np.zeros(len(arrs), dtype=np.uint64)
+        if len(arrs) > 1:
+            offset[1:] = np.cumsum(length[:-1], dtype=np.uint64)
+        bases = np.concatenate(arrs) if arrs and length.sum() else np.zeros(1, np.uint8)
+        return cls(bases, offset, length)
+
+    def subset(self, lo: int, hi: int) -> "Dna5Sample":
+        """Windows [lo, hi) (a shard), sharing the bases."""
+        return Dna5Sample(self.bases, self.offset[lo:hi], self.length[lo:hi])
+
+    @property
+    def n_windows(self) -> int:
+        return int(self.length.size)
+
+    @property
+    def total_bases(self) -> int:
+        return int(self.length.sum(dtype=np.uint64))
+
+    def as_struct(self) -> ACDna5Windows:
+        one = lambda a, t: _ptr(a if a.size else np.zeros(1, a.dtype), t)  # noqa: E731
+        return ACDna5Windows(_ptr(self.bases, ctypes.c_uint8), one(self.offset, ctypes.c_uint64),
+                             one(self.length, ctypes.c_uint32), self.n_windows)
+
+
+class Jobs:
+    """A reusable ac_job array (both read ends of one run, or shards): the
+    k-mer and count arrays are kept alive with it."""
+
+    def __init__(self, parts):
+        """`parts`: sequence of (kmers, Dna5Sample)."""
+        self.kmers = [np.ascontiguousarray(np.asarray(km, dtype=np.uint64)) for km, _ in parts]
+        self.samples = [smp for _, smp in parts]
+        self.counts = [np.zeros(max(k.size, 1), dtype=np.uint64) for k in self.kmers]
+        self.n_counts = sum(int(k.size) for k in self.kmers)
+        self.array = (ACJob * len(parts))(*[
+            ACJob(_ptr(km if km.size else np.zeros(1, np.uint64), ctypes.c_uint64), int(km.size), smp.as_struct(),
+                  _ptr(c, ctypes.c_uint64))
+            for km, smp, c in zip(self.kmers, self.samples, self.counts)])
+
+    def results(self):
+        return [c[: k.size] for c, k in zip(self.counts, self.kmers)]
+
+
 class ApproxCounter:
     """One device context (ac_create / ac_destroy), or with n_gpus a context
     whose host-buffer counts are sharded over that many devices (ac_create_multi)."""
@@ -151,6 +216,29 @@ class ApproxCounter:
                               int(ln.size), _ptr(counts, ctypes.c_uint64))
         check(st, self._h)
         return counts[: kmers.size]
+
+    def count_jobs(self, k: int, jobs) -> list:
+        """ac_error_count_jobs: the whole stage from Dna5 host buffers (pack, one DMA, one
+        fused launch, counts back), up to 4 jobs.  `jobs` is a Jobs object or a sequence of
+        (kmers, Dna5Sample / windows); returns the uint64 counts of every job."""
+        if not isinstance(jobs, Jobs):
+            jobs = Jobs([(km, w if isinstance(w, Dna5Sample) else Dna5Sample.from_windows(w)) for km, w in jobs])
+        st = self._L.ac_error_count_jobs(self._h, int(k), jobs.array, len(jobs.array))
+        check(st, self._h)
+        return jobs.results()
+
+    def submit_jobs(self, k: int, jobs: "Jobs", d_counts, stream=None) -> None:
+        """ac_error_count_jobs_submit: pack + send + launch; uint32 counts (jobs concatenated)
+        go to the device tensor `d_counts` on `stream` (asynchronous)."""
+        ptr = ctypes.cast(ctypes.c_void_p(d_counts.data_ptr()), ctypes.POINTER(ctypes.c_uint32))
+        st = self._L.ac_error_count_jobs_submit(self._h, int(k), jobs.array, len(jobs.array), ptr,
+                                                ctypes.c_void_p(stream or 0))
+        if st:
+            check(st, self._h)
+
+    def check(self, stream=None) -> None:
+        """ac_check: raise if a device launch since the last check skipped a malformed window."""
+        check(self._L.ac_check(self._h, ctypes.c_void_p(stream or 0)), self._h)
 
     def exact_count(self, k: int, sample: PackedSample, lc_threshold: float, forbidden=(), limit: int = 500,
                     solid: int = 0):
@@ -252,6 +340,6 @@ def error_count(sequences, exact_count, nb_thread: int = 4, k: int = 16, v: int 
     kmers = [int(km) for km, _ in exact_count]
     if not kmers:
         return {}
-    sample = pack_windows(sequences)
-    counts = _counter().count(k, kmers, sample)
+    # the sample as a StringSet<Dna5String>: packed, sent and counted by ac_error_count_jobs
+    counts = _counter().count_jobs(k, [(np.array(kmers, dtype=np.uint64), Dna5Sample.from_windows(sequences))])[0]
     return {km: int(c) for km, c in zip(kmers, counts)}

@@ -8,6 +8,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -16,7 +18,15 @@
 
 #include "approx_counter_amd.h"
 #include "exact_count.h"
+#include "host_pack.h"
 #include "wm_count.h"
+
+static_assert(AC_MAX_JOBS <= AC_MAX_SEGS, "every job of ac_error_count_jobs is one segment of one launch");
+
+// A synchronous jobs call is cut into up to this many parts (window ranges of
+// every job), each packed, sent and counted on its own stream, so a part's
+// packing and DMA overlap the previous part's kernel.
+#define AC_STAGE_MAX_PARTS 2
 
 struct ac_ctx {
     int device = 0;
@@ -39,14 +49,20 @@ struct ac_ctx {
     size_t s_cap[4] = {0, 0, 0, 0};
     void* e_buf[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     size_t e_cap[6] = {0, 0, 0, 0, 0, 0};
-    // work-queue counters: two banks of qcap u32; dirty[b] =
-    // counters of bank b used by the last launch on it (zeroed by the next launch)
-    uint32_t* queue = nullptr;
-    uint32_t qcap = 0, bank = 0, dirty[2] = {0, 0};
-    // count hand-off scratch: per-group sums and tickets (zero between launches)
-    uint32_t* acc = nullptr;
-    uint32_t* tickets = nullptr;
-    uint32_t acc_cap = 0, ticket_cap = 0;
+    // Count-kernel scratch, one set per stream a launch may run on at the same
+    // time as another (the parts of a jobs call, AC_STAGE_MAX_PARTS).
+    struct Scratch {
+        // work-queue counters: two banks of qcap u32; dirty[b] =
+        // counters of bank b used by the last launch on it (zeroed by the next launch)
+        uint32_t* queue = nullptr;
+        uint32_t qcap = 0, bank = 0, dirty[2] = {0, 0};
+        // count hand-off scratch: per-group sums and tickets (zero between launches)
+        uint32_t* acc = nullptr;
+        uint32_t* tickets = nullptr;
+        uint32_t acc_cap = 0, ticket_cap = 0;
+    } sc[AC_STAGE_MAX_PARTS];
+    // streams of parts 1.. of a jobs call (part 0 runs on `stream`)
+    hipStream_t part_stream[AC_STAGE_MAX_PARTS] = {};
     // resident waves of the count kernel per pattern pack P (0 = not queried yet)
     uint32_t resident[AC_MAX_PACK + 1] = {0, 0, 0, 0, 0};
     // last launch geometry
@@ -54,6 +70,23 @@ struct ac_ctx {
     uint32_t last_wpw = 0, last_groups = 0;
     // ac_create_multi: contexts of shards 1..n-1 (this context is shard 0)
     std::vector<ac_ctx*> peers;
+    // device error word of the asynchronous entry points (ac_check), and a
+    // pinned word to read it back through
+    uint32_t* d_err = nullptr;
+    uint32_t* h_err = nullptr;
+    // ac_error_count_jobs staging: two slots used alternately, so a submit
+    // packs into one while the previous launch still reads the other.  Each is
+    // a pinned host block, a device block (same layout) and an event recorded
+    // after the last stream work that reads either.
+    struct Slot {
+        void* h = nullptr;
+        void* d = nullptr;
+        void* hd = nullptr;  // device address of the pinned block (zero-copy stage)
+        size_t h_cap = 0, d_cap = 0;
+        hipEvent_t ev = nullptr;
+        bool pending = false;
+    } slot[2 * AC_STAGE_MAX_PARTS];
+    uint32_t next_slot = 0;
 };
 
 namespace {
@@ -157,8 +190,37 @@ ac_status check_sample(ac_ctx* ctx, const ac_windows* s) {
     return AC_OK;
 }
 
+// Every window inside the image and 32-aligned, written so that no sum can
+// wrap: a start near 2^64 must not pass as "start + length <= n_bases".
+inline bool window_ok(uint64_t start, uint32_t length, uint64_t n_bases) {
+    return start % 32 == 0 && length <= n_bases && start <= n_bases - length;
+}
+
+// Status for a device error word read back after a launch (wm_count.h).
+ac_status device_error(ac_ctx* ctx, uint32_t word) {
+    if (word & AC_DEVERR_SETUP)
+        return fail(ctx, AC_ERR_INTERNAL, "count kernel set-up fault (~Eq table not at LDS 0): its work was skipped");
+    if (word & AC_DEVERR_WINDOW)
+        return fail(ctx, AC_ERR_INVALID,
+                    "malformed window skipped on the device (misaligned start or past n_bases): counts are short");
+    return AC_OK;
+}
+
+ac_status check_layout(ac_ctx* ctx, const ac_windows& s) {
+    for (uint32_t i = 0; i < s.n_windows; ++i)
+        if (!window_ok(s.start[i], s.length[i], s.n_bases))
+            return fail(ctx, AC_ERR_INVALID, "window " + std::to_string(i) + " is misaligned or outside the image");
+    return AC_OK;
+}
+
+// One fused count launch over `n` device segments.  `err` = the device word
+// the kernel reports skipped windows in (the context's, for ac_check, when NULL).
+// `sc` = the scratch set (one per concurrently running stream); `wave_cap` (0
+// = none) limits the launch to that many waves, so another launch's waves can
+// be resident beside it.
 ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hipStream_t stream,
-                 bool zero) {
+                 bool zero, uint32_t* err = nullptr, int part = 0, uint64_t wave_cap = 0) {
+    ac_ctx::Scratch& sc = ctx->sc[part];
     if (ac_status st = check_k(ctx, k)) return st;
     if (n > AC_MAX_SEGS) return fail(ctx, AC_ERR_INVALID, "too many segments in one launch (max 4)");
     if (n && !segs) return fail(ctx, AC_ERR_INVALID, "segments is NULL");
@@ -189,7 +251,9 @@ ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hi
     // of AC_WAVES_PER_BLOCK waves are dealt round-robin over blocks of that many
     // consecutive sub-queues (one candidate group each).
     if (!ctx->resident[P]) AC_HIP(ctx, acamd::resident_waves(P, ctx->cu_count, &ctx->resident[P]));
-    const uint64_t resident = ctx->resident[P];
+    const uint64_t resident = wave_cap ? std::max<uint64_t>(AC_WAVES_PER_BLOCK, std::min<uint64_t>(wave_cap, ctx->resident[P]) /
+                                                                  AC_WAVES_PER_BLOCK * AC_WAVES_PER_BLOCK)
+                                       : ctx->resident[P];
     const uint32_t wpw = (uint32_t)std::max<uint64_t>(1, (items + resident - 1) / resident);
 #ifdef AC_FORCE_CHUNK  // A/B builds (tools/variants.sh): fixed item size
     const uint32_t chunk = AC_FORCE_CHUNK;
@@ -255,43 +319,44 @@ ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hi
         for (uint32_t i = 0; i < n; ++i)
             if (a.seg[i].queue_begin != ~0u)
                 AC_HIP(ctx, hipMemsetAsync(a.seg[i].counts, 0, sizeof(uint32_t) * a.seg[i].n_kmers, stream));
-    if (acc_slots > ctx->acc_cap) {
-        if (ctx->acc) AC_HIP(ctx, hipFree(ctx->acc));
-        ctx->acc = nullptr;
-        ctx->acc_cap = 0;
-        AC_HIP(ctx, hipMalloc(&ctx->acc, sizeof(uint32_t) * acc_slots));
-        AC_HIP(ctx, hipMemsetAsync(ctx->acc, 0, sizeof(uint32_t) * acc_slots, stream));
-        ctx->acc_cap = acc_slots;
+    if (acc_slots > sc.acc_cap) {
+        if (sc.acc) AC_HIP(ctx, hipFree(sc.acc));
+        sc.acc = nullptr;
+        sc.acc_cap = 0;
+        AC_HIP(ctx, hipMalloc(&sc.acc, sizeof(uint32_t) * acc_slots));
+        AC_HIP(ctx, hipMemsetAsync(sc.acc, 0, sizeof(uint32_t) * acc_slots, stream));
+        sc.acc_cap = acc_slots;
     }
-    if (groups_total > ctx->ticket_cap) {
-        if (ctx->tickets) AC_HIP(ctx, hipFree(ctx->tickets));
-        ctx->tickets = nullptr;
-        ctx->ticket_cap = 0;
+    if (groups_total > sc.ticket_cap) {
+        if (sc.tickets) AC_HIP(ctx, hipFree(sc.tickets));
+        sc.tickets = nullptr;
+        sc.ticket_cap = 0;
         const size_t bytes = sizeof(uint32_t) * AC_QUEUE_LINE * (size_t)groups_total;
-        AC_HIP(ctx, hipMalloc(&ctx->tickets, bytes));
-        AC_HIP(ctx, hipMemsetAsync(ctx->tickets, 0, bytes, stream));
-        ctx->ticket_cap = groups_total;
+        AC_HIP(ctx, hipMalloc(&sc.tickets, bytes));
+        AC_HIP(ctx, hipMemsetAsync(sc.tickets, 0, bytes, stream));
+        sc.ticket_cap = groups_total;
     }
-    a.acc = ctx->acc;
-    a.tickets = ctx->tickets;
+    a.acc = sc.acc;
+    a.tickets = sc.tickets;
+    a.err = err ? err : ctx->d_err;
     const uint32_t n_counters = qbegin;
     if (n_counters) wave = std::max<uint64_t>(resident, n_counters);
-    if (n_counters > ctx->qcap) {
-        if (ctx->queue) AC_HIP(ctx, hipFree(ctx->queue));
-        ctx->queue = nullptr;
-        ctx->qcap = 0;
+    if (n_counters > sc.qcap) {
+        if (sc.queue) AC_HIP(ctx, hipFree(sc.queue));
+        sc.queue = nullptr;
+        sc.qcap = 0;
         const uint32_t cap = std::max<uint32_t>(n_counters, 1024);
         const size_t bytes = sizeof(uint32_t) * AC_QUEUE_LINE * 2 * (size_t)cap;
-        AC_HIP(ctx, hipMalloc(&ctx->queue, bytes));
-        AC_HIP(ctx, hipMemsetAsync(ctx->queue, 0, bytes, stream));
-        ctx->qcap = cap;
-        ctx->bank = 0;
-        ctx->dirty[0] = ctx->dirty[1] = 0;
+        AC_HIP(ctx, hipMalloc(&sc.queue, bytes));
+        AC_HIP(ctx, hipMemsetAsync(sc.queue, 0, bytes, stream));
+        sc.qcap = cap;
+        sc.bank = 0;
+        sc.dirty[0] = sc.dirty[1] = 0;
     }
-    a.queue = ctx->queue;
-    a.qstride = ctx->qcap;
-    a.bank = ctx->bank;
-    a.zero_count = ctx->dirty[ctx->bank ^ 1u];
+    a.queue = sc.queue;
+    a.qstride = sc.qcap;
+    a.bank = sc.bank;
+    a.zero_count = sc.dirty[sc.bank ^ 1u];
     a.n_queues = std::max<uint32_t>(1, n_counters);
     // Live segments' queue_begin values are increasing; the kernel picks the
     // last live segment whose queue_begin <= its sub-queue.
@@ -301,9 +366,9 @@ ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hi
     ctx->last_groups = groups_total;
     AC_HIP(ctx, acamd::launch_wm2_count(a, stream));
     if (wave) {  // the launch dequeued from `bank` and zeroed the other one
-        ctx->dirty[ctx->bank] = n_counters;
-        ctx->dirty[ctx->bank ^ 1u] = 0;
-        ctx->bank ^= 1u;
+        sc.dirty[sc.bank] = n_counters;
+        sc.dirty[sc.bank ^ 1u] = 0;
+        sc.bank ^= 1u;
     }
     return AC_OK;
 }
@@ -344,6 +409,13 @@ ac_status ac_create(ac_ctx** out, int device) {
         return st;
     }
     ctx->cu_count = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    if ((e = hipMalloc(&ctx->d_err, sizeof(uint32_t))) != hipSuccess ||
+        (e = hipMemset(ctx->d_err, 0, sizeof(uint32_t))) != hipSuccess ||
+        (e = hipHostMalloc(&ctx->h_err, sizeof(uint32_t), hipHostMallocDefault)) != hipSuccess) {
+        ac_status st = hip_fail(nullptr, e, "device setup");
+        ac_destroy(ctx);
+        return st;
+    }
     *out = ctx;
     return AC_OK;
 }
@@ -356,13 +428,25 @@ void ac_destroy(ac_ctx* ctx) {
         if (p) (void)hipFree(p);
     if (ctx->d_stage) (void)hipFree(ctx->d_stage);
     if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
-    if (ctx->queue) (void)hipFree(ctx->queue);
-    if (ctx->acc) (void)hipFree(ctx->acc);
-    if (ctx->tickets) (void)hipFree(ctx->tickets);
+    for (auto& sc : ctx->sc) {
+        if (sc.queue) (void)hipFree(sc.queue);
+        if (sc.acc) (void)hipFree(sc.acc);
+        if (sc.tickets) (void)hipFree(sc.tickets);
+    }
+    for (hipStream_t ps : ctx->part_stream)
+        if (ps) (void)hipStreamDestroy(ps);
     for (void* p : ctx->s_buf)
         if (p) (void)hipFree(p);
     for (void* p : ctx->e_buf)
         if (p) (void)hipFree(p);
+    if (ctx->d_err) (void)hipFree(ctx->d_err);
+    if (ctx->h_err) (void)hipHostFree(ctx->h_err);
+    for (auto& sl : ctx->slot) {
+        if (sl.ev) (void)hipEventSynchronize(sl.ev);
+        if (sl.h) (void)hipHostFree(sl.h);
+        if (sl.d) (void)hipFree(sl.d);
+        if (sl.ev) (void)hipEventDestroy(sl.ev);
+    }
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -395,25 +479,23 @@ ac_status error_count_one(ac_ctx* ctx, uint32_t k, const uint64_t* kmers, uint32
     if (s.n_bases % 32) return fail(ctx, AC_ERR_INVALID, "sample n_bases must be a multiple of 32");
     if (s.n_windows && (!s.codes || !s.nmask || !s.start || !s.length))
         return fail(ctx, AC_ERR_INVALID, "sample has a NULL array");
-    // Host-side layout check: every window inside the image and 32-aligned.
-    for (uint32_t i = 0; i < s.n_windows; ++i) {
-        if (s.start[i] % 32 || s.start[i] + s.length[i] > s.n_bases)
-            return fail(ctx, AC_ERR_INVALID, "window " + std::to_string(i) + " is misaligned or outside the image");
-    }
+    if (ac_status st = check_layout(ctx, s)) return st;
     AC_HIP(ctx, hipSetDevice(ctx->device));
-    // Device block: kmers | codes | nmask | start | length | counts, each
-    // 256-B aligned, filled through the pinned staging block (h2d_staged).
-    const size_t sz[6] = {sizeof(uint64_t) * n_kmers, sizeof(uint32_t) * (s.n_bases / 16),
+    // Device block: kmers | codes | nmask | start | length | err | counts,
+    // each 256-B aligned, filled through the pinned staging block
+    // (h2d_staged; the device error word goes up as a zero with the inputs).
+    static const uint32_t zero_word = 0;
+    const size_t sz[7] = {sizeof(uint64_t) * n_kmers, sizeof(uint32_t) * (s.n_bases / 16),
                           sizeof(uint32_t) * (s.n_bases / 32), sizeof(uint64_t) * s.n_windows,
-                          sizeof(uint32_t) * s.n_windows, sizeof(uint32_t) * n_kmers};
-    const void* src[5] = {kmers, s.codes, s.nmask, s.start, s.length};
-    size_t off[7];
+                          sizeof(uint32_t) * s.n_windows, sizeof(uint32_t), sizeof(uint32_t) * n_kmers};
+    const void* src[6] = {kmers, s.codes, s.nmask, s.start, s.length, &zero_word};
+    size_t off[8];
     off[0] = 0;
-    for (int i = 0; i < 6; ++i) off[i + 1] = (off[i] + sz[i] + 255) / 256 * 256;
-    if (ac_status rc = grow(ctx, &ctx->d_stage, &ctx->d_stage_cap, off[6])) return rc;
+    for (int i = 0; i < 7; ++i) off[i + 1] = (off[i] + sz[i] + 255) / 256 * 256;
+    if (ac_status rc = grow(ctx, &ctx->d_stage, &ctx->d_stage_cap, off[7])) return rc;
     char* d = (char*)ctx->d_stage;
-    // the counts come back into the staging block, after the inputs
-    if (ac_status rc = h2d_staged(ctx, 5, src, sz, d, (sz[5] + 255) / 256 * 256)) return rc;
+    // the error word and the counts come back into the staging block
+    if (ac_status rc = h2d_staged(ctx, 6, src, sz, d, (sz[6] + 255) / 256 * 256)) return rc;
     char* h = (char*)ctx->h_stage;
     hipStream_t st = ctx->stream;
     ac_segment seg;
@@ -425,11 +507,12 @@ ac_status error_count_one(ac_ctx* ctx, uint32_t k, const uint64_t* kmers, uint32
     seg.sample.length = (const uint32_t*)(d + off[4]);
     seg.sample.n_windows = s.n_windows;
     seg.sample.n_bases = s.n_bases;
-    seg.counts = (uint32_t*)(d + off[5]);
-    if (ac_status rc = launch(ctx, k, &seg, 1, st, true)) return rc;
-    AC_HIP(ctx, hipMemcpyAsync(h + off[5], d + off[5], sz[5], hipMemcpyDeviceToHost, st));
+    seg.counts = (uint32_t*)(d + off[6]);
+    if (ac_status rc = launch(ctx, k, &seg, 1, st, true, (uint32_t*)(d + off[5]))) return rc;
+    AC_HIP(ctx, hipMemcpyAsync(h + off[5], d + off[5], off[6] - off[5] + sz[6], hipMemcpyDeviceToHost, st));
     AC_HIP(ctx, hipStreamSynchronize(st));
-    const uint32_t* hc = (const uint32_t*)(h + off[5]);
+    if (ac_status rc = device_error(ctx, *(const uint32_t*)(h + off[5]))) return rc;
+    const uint32_t* hc = (const uint32_t*)(h + off[6]);
     for (uint32_t i = 0; i < n_kmers; ++i) counts[i] = hc[i];
     return AC_OK;
 }
@@ -446,9 +529,7 @@ ac_status ac_error_count(ac_ctx* ctx, uint32_t k, const uint64_t* kmers, uint32_
     if (!kmers || !counts || !sample) return fail(ctx, AC_ERR_INVALID, "NULL argument");
     if (ac_status st = check_sample(ctx, sample)) return st;
     const ac_windows& s = *sample;
-    for (uint32_t i = 0; i < s.n_windows; ++i)
-        if (s.start[i] % 32 || s.start[i] + s.length[i] > s.n_bases)
-            return fail(ctx, AC_ERR_INVALID, "window " + std::to_string(i) + " is misaligned or outside the image");
+    if (ac_status st = check_layout(ctx, s)) return st;
     // Shards: contiguous window ranges balanced by bases; shard g is a slice of
     // the image (codes/nmask from its first window's start), starts rebased.
     const size_t G = ctx->peers.size() + 1;
@@ -470,11 +551,16 @@ ac_status ac_error_count(ac_ctx* ctx, uint32_t k, const uint64_t* kmers, uint32_
         ac_ctx* c = g == 0 ? ctx : ctx->peers[g - 1];
         const uint32_t lo = cut[g], hi = cut[g + 1];
         if (hi == lo) return;
-        const uint64_t b0 = s.start[lo];
-        uint64_t b1 = b0;
-        for (uint32_t i = lo; i < hi; ++i) b1 = std::max<uint64_t>(b1, s.start[i] + s.length[i]);
-        b1 = (b1 + 31) / 32 * 32;
-        if (b1 == b0) return;  // only empty windows: no occurrences
+        // The shard's slice of the image spans its lowest start to its highest
+        // end: windows may come in any order and overlap (window_ok above
+        // guarantees start + length <= n_bases, so nothing here wraps).
+        uint64_t b0 = s.start[lo], b1 = 0;
+        for (uint32_t i = lo; i < hi; ++i) {
+            b0 = std::min<uint64_t>(b0, s.start[i]);
+            b1 = std::max<uint64_t>(b1, s.start[i] + s.length[i]);
+        }
+        b1 = std::max<uint64_t>(b0 + 32, (b1 + 31) / 32 * 32);  // empty windows still count (k = 2: d = 2)
+        if (b1 > s.n_bases) b1 = s.n_bases;  // b0 + 32 <= n_bases: b0 is a 32-aligned start < n_bases or 0
         std::vector<uint64_t> st(hi - lo);
         for (uint32_t i = lo; i < hi; ++i) st[i - lo] = s.start[i] - b0;
         const ac_windows w{s.codes + b0 / 16, s.nmask + b0 / 32, st.data(), s.length + lo, hi - lo, b1 - b0};
@@ -540,10 +626,7 @@ ac_status ac_count(ac_ctx* ctx, uint32_t k, const uint64_t* kmers, uint32_t n_km
 ac_status ac_sample_upload(ac_ctx* ctx, const ac_windows* host, ac_windows* dev) {
     if (!ctx || !dev) return fail(ctx, AC_ERR_INVALID, "ctx or dev is NULL");
     if (ac_status st = check_sample(ctx, host)) return st;
-    // layout check on the host copy: every window inside the image, 32-aligned
-    for (uint32_t i = 0; i < host->n_windows; ++i)
-        if (host->start[i] % 32 || host->start[i] + host->length[i] > host->n_bases)
-            return fail(ctx, AC_ERR_INVALID, "window " + std::to_string(i) + " is misaligned or outside the image");
+    if (ac_status st = check_layout(ctx, *host)) return st;  // on the host copy
     AC_HIP(ctx, hipSetDevice(ctx->device));
     const size_t sz[4] = {sizeof(uint32_t) * (host->n_bases / 16), sizeof(uint32_t) * (host->n_bases / 32),
                           sizeof(uint64_t) * host->n_windows, sizeof(uint32_t) * host->n_windows};
@@ -585,7 +668,8 @@ ac_status ac_exact_count_device(ac_ctx* ctx, uint32_t k, const ac_windows* dev, 
     while (slots < dev->n_bases + dev->n_bases / 2) slots <<= 1;
     // Kept entries seen >= EXACT_LIST_MIN (2) times: at most n_bases / 2 (+ the all-T 32-mer).
     const uint64_t list_cap = dev->n_bases / 2 + 2;
-    // small block: special[0..1] u32, had_n u64 @16, n_out u64 @24, n_list u64 @32, hist[EXACT_HIST_BINS] u32 @64
+    // small block: special[0..1] u32, had_n u64 @16, n_out u64 @24, n_list u64 @32, err u32 @40,
+    // hist[EXACT_HIST_BINS] u32 @64
     const size_t small_bytes = 64 + sizeof(uint32_t) * EXACT_HIST_BINS;
     std::vector<uint64_t> fb(forbidden, forbidden + n_forbidden);
     std::sort(fb.begin(), fb.end());
@@ -622,6 +706,7 @@ ac_status ac_exact_count_device(ac_ctx* ctx, uint32_t k, const ac_windows* dev, 
     a.had_n = (unsigned long long*)(small + 16);
     a.n_out = (unsigned long long*)(small + 24);
     a.n_list = (unsigned long long*)(small + 32);
+    a.err = (uint32_t*)(small + 40);
     a.hist = (uint32_t*)(small + 64);
     a.list_keys = (uint64_t*)ctx->e_buf[1];
     a.list_cnts = (uint32_t*)((char*)ctx->e_buf[1] + sizeof(uint64_t) * list_cap);
@@ -634,6 +719,7 @@ ac_status ac_exact_count_device(ac_ctx* ctx, uint32_t k, const ac_windows* dev, 
     std::vector<char> h_small(small_bytes);
     AC_HIP(ctx, hipMemcpyAsync(h_small.data(), small, small_bytes, hipMemcpyDeviceToHost, st));
     AC_HIP(ctx, hipStreamSynchronize(st));
+    if (ac_status rc = device_error(ctx, *(const uint32_t*)(h_small.data() + 40))) return rc;
     const uint32_t* hist = (const uint32_t*)(h_small.data() + 64);
     uint64_t kept = 0;
     for (int i = 0; i < EXACT_HIST_BINS; ++i) kept += hist[i];
@@ -735,7 +821,7 @@ ac_status ac_error_count_sample(ac_ctx* ctx, uint32_t k, const uint64_t* kmers, 
     if (ac_status rc = launch(ctx, k, &seg, 1, st, true)) return rc;
     ctx->h_counts.resize(n_kmers);
     AC_HIP(ctx, hipMemcpyAsync(ctx->h_counts.data(), ctx->d_buf[5], sizeof(uint32_t) * n_kmers, hipMemcpyDeviceToHost, st));
-    AC_HIP(ctx, hipStreamSynchronize(st));
+    if (ac_status rc = ac_check(ctx, st)) return rc;  // synchronises the stream
     for (uint32_t i = 0; i < n_kmers; ++i) counts[i] = ctx->h_counts[i];
     return AC_OK;
 }
@@ -761,23 +847,426 @@ ac_status ac_pack_windows(const uint8_t* dna5, const uint64_t* seq_start, const 
     if (!codes || !nmask) return fail(nullptr, AC_ERR_INVALID, "NULL image");
     if (n_bases % 32 || n_bases < ac_image_bases(seq_len, n))
         return fail(nullptr, AC_ERR_INVALID, "image too small (use ac_image_bases)");
-    std::memset(codes, 0, sizeof(uint32_t) * (n_bases / 16));
-    std::memset(nmask, 0, sizeof(uint32_t) * (n_bases / 32));
-    uint64_t pos = 0;
-    for (uint32_t i = 0; i < n; ++i) {
-        const uint8_t* src = dna5 + seq_start[i];
-        const uint32_t len = seq_len[i];
-        start[i] = pos;
-        length[i] = len;
-        for (uint32_t j = 0; j < len; ++j) {
-            const uint64_t b = pos + j;
-            const uint8_t v = src[j];
-            if (v < 4) codes[b >> 4] |= (uint32_t)v << (2 * (b & 15));
-            else nmask[b >> 5] |= 1u << (b & 31);
+    // The same packer as the jobs stage (host_pack.cpp); it writes every
+    // 32-base block the windows occupy, the rest of the image is zeroed here.
+    uint64_t used = 0;
+    for (uint32_t i = 0; i < n; ++i) used += acamd::image_span(seq_len[i]);
+    acamd::pack_dna5_range(dna5, seq_start, seq_len, 0, n, 0, codes, nmask, start, length);
+    std::memset(codes + used / 16, 0, sizeof(uint32_t) * ((n_bases - used) / 16));
+    std::memset(nmask + used / 32, 0, sizeof(uint32_t) * ((n_bases - used) / 32));
+    return AC_OK;
+}
+
+ac_status ac_check(ac_ctx* ctx, void* hip_stream) {
+    if (!ctx) return fail(nullptr, AC_ERR_INVALID, "ctx is NULL");
+    AC_HIP(ctx, hipSetDevice(ctx->device));
+    hipStream_t st = (hipStream_t)hip_stream;
+    AC_HIP(ctx, hipMemcpyAsync(ctx->h_err, ctx->d_err, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    AC_HIP(ctx, hipStreamSynchronize(st));
+    const uint32_t word = *ctx->h_err;
+    if (!word) return AC_OK;
+    AC_HIP(ctx, hipMemsetAsync(ctx->d_err, 0, sizeof(uint32_t), st));
+    AC_HIP(ctx, hipStreamSynchronize(st));
+    return device_error(ctx, word);
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// ac_error_count_jobs: the whole errorCount stage from Dna5 host buffers.
+namespace {
+
+inline size_t align256(size_t x) { return (x + 255) / 256 * 256; }
+
+// AC_STAGE_TRACE=1: per-phase host timings of the jobs stage, summed over the
+// calls and printed to stderr at exit (a measurement aid; no effect otherwise).
+struct StageTrace {
+    bool on = std::getenv("AC_STAGE_TRACE") != nullptr;
+    double sum[8] = {};
+    uint64_t calls = 0;
+    void skip_warmup() {  // the first calls allocate: leave them out of the means
+        if (calls == 5) {
+            for (double& x : sum) x = 0.0;
         }
-        pos += ((uint64_t)len + 31) / 32 * 32;
+    }
+    ~StageTrace() {
+        if (!on || !calls) return;
+        static const char* names[8] = {"span", "layout", "pack", "h2d_enq", "launch_enq", "d2h_enq", "sync", "widen"};
+        const double n = calls > 5 ? double(calls - 5) : double(calls);
+        std::fprintf(stderr, "[ac stage trace] %llu calls (first 5 left out), mean us:", (unsigned long long)calls);
+        for (int i = 0; i < 8; ++i) std::fprintf(stderr, " %s %.1f", names[i], sum[i] / n);
+        std::fprintf(stderr, "\n");
+    }
+};
+StageTrace g_trace;
+inline double now_us() {
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// Where one device's part of a jobs call lives in its staging slot (the same
+// offsets in the pinned host block and the device block).  Inputs first
+// (sent by one DMA), then the device error word and the uint32 counts (the
+// way back: one DMA from off_err to the end).
+struct JobPlan {
+    uint32_t n = 0;
+    uint32_t lo[AC_MAX_JOBS] = {}, hi[AC_MAX_JOBS] = {};  // window range of each job on this device
+    uint64_t n_bases[AC_MAX_JOBS] = {};
+    size_t off_kmers[AC_MAX_JOBS] = {}, off_codes[AC_MAX_JOBS] = {}, off_nmask[AC_MAX_JOBS] = {};
+    size_t off_start[AC_MAX_JOBS] = {}, off_len[AC_MAX_JOBS] = {}, off_counts[AC_MAX_JOBS] = {};
+    size_t off_err = 0, total = 0;
+    int slot = 0;
+};
+
+// AC_STAGE_PARTS (1 or 2, default 1) and AC_STAGE_SPLIT (first part's share of
+// the bases, default 0.5): experiment switches of the synchronous stage.
+int stage_parts() {
+    static const int v = [] {
+        const char* e = std::getenv("AC_STAGE_PARTS");
+        const int n = e ? std::atoi(e) : 1;  // 2 measured slower (DMA and zero-copy alike)
+        return std::max(1, std::min(AC_STAGE_MAX_PARTS, n));
+    }();
+    return v;
+}
+// Zero-copy stage (default; AC_STAGE_ZEROCOPY=0 = DMA in and out): the count
+// kernel reads the packed inputs straight from the pinned host block and
+// writes the counts back into it.  Each window is fetched one window ahead of
+// its use (~8 us of slack at 8 waves/SIMD), which hides the PCIe latency, and
+// the contiguous item ranges of the work queues make each XCD read a slice of
+// the sample; it saves the DMA (1.2 MB, ~27 us at cfg2), the ~9 us
+// DMA-to-kernel dependency and the D2H blit.
+// AC_STAGE_HOSTALLOC=coherent|noncoherent: the pinned block's flags (A/B).
+bool stage_zerocopy() {
+    static const bool v = [] {
+        const char* e = std::getenv("AC_STAGE_ZEROCOPY");
+        return !e || std::atoi(e) != 0;
+    }();
+    return v;
+}
+unsigned stage_host_flags() {
+    static const unsigned v = [] {
+        const char* e = std::getenv("AC_STAGE_HOSTALLOC");
+        if (e && std::string(e) == "coherent") return (unsigned)hipHostMallocCoherent;
+        if (e && std::string(e) == "noncoherent") return (unsigned)hipHostMallocNonCoherent;
+        return (unsigned)hipHostMallocDefault;
+    }();
+    return v;
+}
+
+double stage_split() {
+    static const double v = [] {
+        const char* e = std::getenv("AC_STAGE_SPLIT");
+        const double f = e ? std::atof(e) : 0.5;
+        return std::max(0.05, std::min(0.95, f));
+    }();
+    return v;
+}
+
+ac_status check_jobs(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint32_t n_jobs) {
+    if (!ctx) return fail(nullptr, AC_ERR_INVALID, "ctx is NULL");
+    if (ac_status st = check_k(ctx, k)) return st;
+    if (n_jobs > AC_MAX_JOBS) return fail(ctx, AC_ERR_INVALID, "too many jobs in one call (max 4)");
+    if (n_jobs && !jobs) return fail(ctx, AC_ERR_INVALID, "jobs is NULL");
+    for (uint32_t j = 0; j < n_jobs; ++j) {
+        const ac_job& b = jobs[j];
+        if (b.n_kmers && !b.kmers) return fail(ctx, AC_ERR_INVALID, "job kmers is NULL");
+        if (b.sample.n_windows && (!b.sample.bases || !b.sample.offset || !b.sample.length))
+            return fail(ctx, AC_ERR_INVALID, "job sample has a NULL array");
     }
     return AC_OK;
+}
+
+// Packs the jobs' window ranges p.lo/p.hi into a staging slot of ctx (the
+// host worker pool writes the 2-bit codes, N bitmap and window descriptors
+// straight into pinned memory), sends the inputs with one DMA on `stream`
+// and launches the fused count kernel, whose counts go to d_counts (job j at
+// d_counts + sum of the earlier n_kmers) or, when NULL, to the slot's counts
+// area.  Records the slot's event after the launch.
+ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan& p, hipStream_t stream,
+                           uint32_t* d_counts, int part = 0, uint32_t wave_div = 0) {
+    using acamd::image_span;
+    acamd::WorkPool& pool = acamd::host_pool();
+    // Tasks: contiguous window ranges, about 4 per pool thread.
+    struct Task {
+        uint32_t job, w0, w1;
+        uint64_t bases;  // image bases the range occupies, then its first image base
+    };
+    uint64_t total_w = 0;
+    for (uint32_t j = 0; j < p.n; ++j)
+        if (jobs[j].n_kmers) total_w += p.hi[j] - p.lo[j];
+    const uint64_t per = std::max<uint64_t>(256, std::min<uint64_t>(65536, total_w / (4ull * pool.size()) + 1));
+    std::vector<Task> tasks;
+    for (uint32_t j = 0; j < p.n; ++j) {
+        if (!jobs[j].n_kmers) continue;  // nothing to count: its windows are not needed
+        for (uint64_t w = p.lo[j]; w < p.hi[j]; w += per)
+            tasks.push_back({j, (uint32_t)w, (uint32_t)std::min<uint64_t>(p.hi[j], w + per), 0});
+    }
+    const std::function<void(uint32_t)> span_of = [&](uint32_t t) {
+        Task& x = tasks[t];
+        const uint32_t* len = jobs[x.job].sample.length;
+        uint64_t b = 0;
+        for (uint32_t w = x.w0; w < x.w1; ++w) b += image_span(len[w]);
+        x.bases = b;
+    };
+    double tt = g_trace.on ? now_us() : 0.0;
+    auto mark = [&](int i) {
+        if (!g_trace.on) return;
+        const double t = now_us();
+        g_trace.sum[i] += t - tt;
+        tt = t;
+    };
+    if (total_w <= (1u << 18)) {  // a serial pass is cheaper than a pool round trip up to ~256k windows
+        for (uint32_t t = 0; t < (uint32_t)tasks.size(); ++t) span_of(t);
+    } else {
+        pool.run((uint32_t)tasks.size(), span_of);
+    }
+    mark(0);
+    // Image of each job: its tasks' ranges back to back; at least one 32-base block.
+    uint64_t acc[AC_MAX_JOBS] = {};
+    for (Task& x : tasks) {
+        const uint64_t b = x.bases;
+        x.bases = acc[x.job];
+        acc[x.job] += b;
+    }
+    size_t off = 0;
+    for (uint32_t j = 0; j < p.n; ++j) {
+        const uint32_t nw = jobs[j].n_kmers ? p.hi[j] - p.lo[j] : 0;
+        p.n_bases[j] = std::max<uint64_t>(32, acc[j]);
+        p.off_kmers[j] = off;
+        off = align256(off + sizeof(uint64_t) * jobs[j].n_kmers);
+        p.off_codes[j] = off;
+        off = align256(off + sizeof(uint32_t) * (p.n_bases[j] / 16));
+        p.off_nmask[j] = off;
+        off = align256(off + sizeof(uint32_t) * (p.n_bases[j] / 32));
+        p.off_start[j] = off;
+        off = align256(off + sizeof(uint64_t) * nw);
+        p.off_len[j] = off;
+        off = align256(off + sizeof(uint32_t) * nw);
+    }
+    p.off_err = off;
+    off = align256(off + sizeof(uint32_t));
+    for (uint32_t j = 0; j < p.n; ++j) {
+        p.off_counts[j] = off;
+        off = align256(off + sizeof(uint32_t) * jobs[j].n_kmers);
+    }
+    p.total = off;
+    // The slot: wait until the launch that last read it has finished, grow it.
+    p.slot = (int)ctx->next_slot;
+    ctx->next_slot = (ctx->next_slot + 1u) % (2u * AC_STAGE_MAX_PARTS);
+    ac_ctx::Slot& sl = ctx->slot[p.slot];
+    if (sl.pending) {
+        AC_HIP(ctx, hipEventSynchronize(sl.ev));
+        sl.pending = false;
+    }
+    if (!sl.ev) AC_HIP(ctx, hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming));
+    const bool zc = stage_zerocopy();
+    if (sl.h_cap < p.total) {
+        if (sl.h) (void)hipHostFree(sl.h);
+        sl.h = nullptr;
+        sl.hd = nullptr;
+        sl.h_cap = 0;
+        const size_t cap = p.total + p.total / 4;
+        AC_HIP(ctx, hipHostMalloc(&sl.h, cap, stage_host_flags()));
+        sl.h_cap = cap;
+        AC_HIP(ctx, hipHostGetDevicePointer(&sl.hd, sl.h, 0));
+    }
+    if (!zc)
+        if (ac_status st = grow(ctx, &sl.d, &sl.d_cap, p.total)) return st;
+    char* h = (char*)sl.h;
+    for (uint32_t j = 0; j < p.n; ++j) {
+        if (jobs[j].n_kmers) std::memcpy(h + p.off_kmers[j], jobs[j].kmers, sizeof(uint64_t) * jobs[j].n_kmers);
+        if (acc[j] == 0) {  // no window bases: the one 32-base block is zero
+            std::memset(h + p.off_codes[j], 0, 2 * sizeof(uint32_t));
+            std::memset(h + p.off_nmask[j], 0, sizeof(uint32_t));
+        }
+    }
+    *(uint32_t*)(h + p.off_err) = 0u;
+    mark(1);
+    const std::function<void(uint32_t)> pack = [&](uint32_t t) {
+        const Task& x = tasks[t];
+        const ac_dna5_windows& w = jobs[x.job].sample;
+        const uint32_t j = x.job, r = x.w0 - p.lo[j];
+        acamd::pack_dna5_range(w.bases, w.offset, w.length, x.w0, x.w1, x.bases, (uint32_t*)(h + p.off_codes[j]),
+                               (uint32_t*)(h + p.off_nmask[j]), (uint64_t*)(h + p.off_start[j]) + r,
+                               (uint32_t*)(h + p.off_len[j]) + r);
+    };
+    pool.run((uint32_t)tasks.size(), pack);
+    mark(2);
+    char* d = zc ? (char*)sl.hd : (char*)sl.d;
+    if (!zc) AC_HIP(ctx, hipMemcpyAsync(d, h, p.off_err + sizeof(uint32_t), hipMemcpyHostToDevice, stream));
+    mark(3);
+    ac_segment segs[AC_MAX_JOBS];
+    uint64_t cbase = 0;
+    for (uint32_t j = 0; j < p.n; ++j) {
+        ac_segment& g = segs[j];
+        const uint32_t nw = jobs[j].n_kmers ? p.hi[j] - p.lo[j] : 0;
+        g.kmers = (const uint64_t*)(d + p.off_kmers[j]);
+        g.n_kmers = jobs[j].n_kmers;
+        g.sample = ac_windows{(const uint32_t*)(d + p.off_codes[j]), (const uint32_t*)(d + p.off_nmask[j]),
+                              (const uint64_t*)(d + p.off_start[j]), (const uint32_t*)(d + p.off_len[j]), nw,
+                              p.n_bases[j]};
+        g.counts = d_counts ? d_counts + cbase : (uint32_t*)(d + p.off_counts[j]);
+        cbase += jobs[j].n_kmers;
+    }
+    // the synchronous path reads the error word back with the counts; a
+    // submit reports through the context's word (ac_check)
+    uint64_t cap = 0;
+    if (wave_div > 1) {
+        const uint32_t P = acamd::pack_factor(k);
+        if (!ctx->resident[P]) AC_HIP(ctx, acamd::resident_waves(P, ctx->cu_count, &ctx->resident[P]));
+        cap = ctx->resident[P] / wave_div;
+    }
+    if (ac_status st = launch(ctx, k, segs, p.n, stream, true, d_counts ? nullptr : (uint32_t*)(d + p.off_err), part,
+                              cap))
+        return st;
+    mark(4);
+    if (!d_counts && !zc)  // the way back: error word + counts
+        AC_HIP(ctx, hipMemcpyAsync(h + p.off_err, d + p.off_err, p.total - p.off_err, hipMemcpyDeviceToHost, stream));
+    mark(5);
+    AC_HIP(ctx, hipEventRecord(sl.ev, stream));
+    sl.pending = true;
+    return AC_OK;
+}
+
+// Shard g of G of job windows [0, n): contiguous, balanced by bases (the rule
+// of ac_error_count's multi-device split and approx_counter_amd/shard.py).
+void shard_range(const uint32_t* length, uint32_t n, size_t G, size_t g, uint32_t* lo, uint32_t* hi) {
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < n; ++i) total += length[i];
+    std::vector<uint32_t> cut(G + 1, n);
+    cut[0] = 0;
+    uint64_t acc = 0;
+    size_t c = 1;
+    for (uint32_t i = 0; i < n && c < G; ++i) {
+        acc += length[i];
+        while (c < G && acc * G >= total * c) cut[c++] = i + 1;
+    }
+    *lo = cut[g];
+    *hi = cut[g + 1];
+}
+
+// The two parts of a single-device call: windows [0, cut) and [cut, n), the
+// first holding `frac` of the bases.
+uint32_t part_cut(const uint32_t* length, uint32_t n, double frac) {
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < n; ++i) total += length[i];
+    const double want = frac * (double)total;
+    uint64_t acc = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        if ((double)acc >= want) return i;
+        acc += length[i];
+    }
+    return n;
+}
+
+
+}  // namespace
+
+extern "C" {
+
+ac_status ac_error_count_jobs(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint32_t n_jobs) {
+    if (ac_status st = check_jobs(ctx, k, jobs, n_jobs)) return st;
+    for (uint32_t j = 0; j < n_jobs; ++j)
+        if (jobs[j].n_kmers && !jobs[j].counts) return fail(ctx, AC_ERR_INVALID, "job counts is NULL");
+    if (n_jobs == 0) return AC_OK;
+    // Units of work: on an ac_create_multi context one per device (shard g of
+    // every job's windows on context g); on one device up to AC_STAGE_MAX_PARTS
+    // parts on their own streams, the first launched with half the resident
+    // waves so the second part's waves run beside it as soon as its DMA lands.
+    struct Unit {
+        ac_ctx* c;
+        int part;
+        hipStream_t stream;
+        uint32_t wave_div;
+        JobPlan plan;
+    };
+    std::vector<Unit> units;
+    uint64_t total_w = 0;
+    for (uint32_t j = 0; j < n_jobs; ++j) total_w += jobs[j].sample.n_windows;
+    if (!ctx->peers.empty()) {
+        const size_t G = ctx->peers.size() + 1;
+        for (size_t g = 0; g < G; ++g) {
+            Unit u{g == 0 ? ctx : ctx->peers[g - 1], 0, nullptr, 0, JobPlan()};
+            u.stream = u.c->stream;
+            u.plan.n = n_jobs;
+            for (uint32_t j = 0; j < n_jobs; ++j)
+                shard_range(jobs[j].sample.length, jobs[j].sample.n_windows, G, g, &u.plan.lo[j], &u.plan.hi[j]);
+            units.push_back(u);
+        }
+    } else {
+        const int parts = total_w >= 2048 ? stage_parts() : 1;  // small calls: one launch
+        for (int q = 0; q < parts; ++q) {
+            if (q > 0 && !ctx->part_stream[q])
+                AC_HIP(ctx, hipStreamCreateWithFlags(&ctx->part_stream[q], hipStreamNonBlocking));
+            Unit u{ctx, q, q == 0 ? ctx->stream : ctx->part_stream[q], (parts > 1 && q == 0) ? 2u : 0u, JobPlan()};
+            u.plan.n = n_jobs;
+            for (uint32_t j = 0; j < n_jobs; ++j) {
+                const uint32_t n = jobs[j].sample.n_windows;
+                const uint32_t cut = parts > 1 ? part_cut(jobs[j].sample.length, n, stage_split()) : n;
+                u.plan.lo[j] = q == 0 ? 0 : cut;
+                u.plan.hi[j] = q == 0 ? cut : n;
+            }
+            units.push_back(u);
+        }
+    }
+    // Units are staged one after another on the host pool; a unit's DMA and
+    // kernel run while the next one is packed.
+    for (size_t g = 0; g < units.size(); ++g) {
+        Unit& u = units[g];
+        AC_HIP(u.c, hipSetDevice(u.c->device));
+        if (ac_status st = stage_and_launch(u.c, k, jobs, u.plan, u.stream, nullptr, u.part, u.wave_div))
+            return u.c != ctx ? fail(ctx, st, "shard " + std::to_string(g) + ": " + u.c->err) : st;
+    }
+    for (uint32_t j = 0; j < n_jobs; ++j)
+        for (uint32_t i = 0; i < jobs[j].n_kmers; ++i) jobs[j].counts[i] = 0;
+    ac_status first_err = AC_OK;
+    double t_sync = g_trace.on ? now_us() : 0.0;
+    for (size_t g = 0; g < units.size(); ++g) {
+        Unit& u = units[g];
+        AC_HIP(u.c, hipSetDevice(u.c->device));
+        AC_HIP(u.c, hipStreamSynchronize(u.stream));
+        if (g_trace.on && g + 1 == units.size()) {
+            const double t = now_us();
+            g_trace.sum[6] += t - t_sync;
+            t_sync = t;
+        }
+        ac_ctx::Slot& sl = u.c->slot[u.plan.slot];
+        sl.pending = false;
+        const char* h = (const char*)sl.h;
+        if (ac_status st = device_error(u.c, *(const uint32_t*)(h + u.plan.off_err))) {
+            if (first_err == AC_OK)
+                first_err = u.c != ctx ? fail(ctx, st, "shard " + std::to_string(g) + ": " + u.c->err) : st;
+            continue;
+        }
+        for (uint32_t j = 0; j < n_jobs; ++j) {
+            const uint32_t* hc = (const uint32_t*)(h + u.plan.off_counts[j]);
+            for (uint32_t i = 0; i < jobs[j].n_kmers; ++i) jobs[j].counts[i] += hc[i];
+        }
+    }
+    if (g_trace.on) {
+        g_trace.sum[7] += now_us() - t_sync;
+        ++g_trace.calls;
+        g_trace.skip_warmup();
+    }
+    return first_err;
+}
+
+ac_status ac_error_count_jobs_submit(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint32_t n_jobs,
+                                     uint32_t* d_counts, void* hip_stream) {
+    if (ac_status st = check_jobs(ctx, k, jobs, n_jobs)) return st;
+    if (!ctx->peers.empty())
+        return fail(ctx, AC_ERR_INVALID, "ac_error_count_jobs_submit needs a single-device context");
+    uint64_t n_counts = 0;
+    for (uint32_t j = 0; j < n_jobs; ++j) n_counts += jobs[j].n_kmers;
+    if (n_counts && !d_counts) return fail(ctx, AC_ERR_INVALID, "d_counts is NULL");
+    if (n_jobs == 0) return AC_OK;
+    AC_HIP(ctx, hipSetDevice(ctx->device));
+    JobPlan p;
+    p.n = n_jobs;
+    for (uint32_t j = 0; j < n_jobs; ++j) {
+        p.lo[j] = 0;
+        p.hi[j] = jobs[j].sample.n_windows;
+    }
+    return stage_and_launch(ctx, k, jobs, p, (hipStream_t)hip_stream, d_counts);
 }
 
 #ifdef AC_STAMPS

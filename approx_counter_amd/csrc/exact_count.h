@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "wm_count.h"  // AC_DEVERR_*
+
 #ifndef EXACT_WINDOWS_PER_BLOCK
 #define EXACT_WINDOWS_PER_BLOCK 16  // windows aggregated per workgroup in LDS
 #endif
@@ -44,6 +46,7 @@ struct ExactArgs {
     uint64_t mask;
     uint32_t* special;
     unsigned long long* had_n;
+    uint32_t* err;  // AC_DEVERR_* bits (wm_count.h), read back by the host
     // filters
     float lc_threshold;
     const uint64_t* forbidden;  // sorted

@@ -131,7 +131,9 @@ __global__ __launch_bounds__(EXACT_THREADS) void exact_insert_kernel(ExactArgs a
             wpos[i] = acc;
             const uint64_t st = a.start[w0 + i];
             const uint32_t len = a.length[w0 + i];
-            const bool ok = !(st & 31u) && st + len <= a.n_bases;  // malformed windows hold no k-mers
+            // malformed windows hold no k-mers; the host hears of them (ExactArgs::err)
+            const bool ok = !(st & 31u) && len <= a.n_bases && st <= a.n_bases - len;
+            if (!ok) atomicOr(a.err, AC_DEVERR_WINDOW);
             acc += (ok && len >= a.k) ? len - a.k + 1u : 0u;
         }
         wpos[nw] = acc;

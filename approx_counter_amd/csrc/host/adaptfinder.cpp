@@ -244,13 +244,15 @@ void open_devices(Devices& dev, uint64_t n_gpus) {
 pair_vector exact_count_gpu(ac_ctx* ctx, const ac_windows& dsample, uint32_t k, float lc, const kmer_set& forbidden,
                             uint64_t limit, uint64_t solid, uint64_t* n_distinct, uint64_t* had_n) {
     std::vector<uint64_t> fb(forbidden.begin(), forbidden.end());
-    uint64_t cap = std::max<uint64_t>(1, solid ? 4096 : limit);
+    // Start small: a huge -lim (used to mean "keep all") must not allocate
+    // `limit` entries up front; the call reports the size it needs.
+    uint64_t cap = std::max<uint64_t>(1, solid ? 4096 : std::min<uint64_t>(limit, 4096));
     for (;;) {
         std::vector<uint64_t> km(cap), ct(cap);
         uint64_t n_out = 0;
         const ac_status st = ac_exact_count_device(ctx, k, &dsample, lc, fb.data(), (uint32_t)fb.size(), limit, solid,
                                                    km.data(), ct.data(), cap, &n_out, n_distinct, had_n);
-        if (st == AC_ERR_INVALID && n_out > cap) {  // solid mode: more solid k-mers than room
+        if (st == AC_ERR_INVALID && n_out > cap) {  // more kept k-mers than room
             cap = n_out;
             continue;
         }

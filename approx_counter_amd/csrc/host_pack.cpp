@@ -1,0 +1,236 @@
+// host_pack.cpp -- worker pool and Dna5 packer of the host-buffer stage (host_pack.h).
+#include "host_pack.h"
+
+#include <immintrin.h>
+#include <sched.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+
+namespace acamd {
+
+namespace {
+
+inline void cpu_relax() { _mm_pause(); }
+
+int64_t now_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
+}  // namespace
+
+WorkPool::WorkPool(unsigned n_threads) {
+    const char* s = std::getenv("AC_HOST_SPIN_US");
+    spin_ns_ = (s ? std::atoll(s) : 2000) * 1000;  // 2 ms: consecutive calls find the workers spinning
+    for (unsigned i = 1; i < std::max(1u, n_threads); ++i) threads_.emplace_back([this] { worker(); });
+}
+
+WorkPool::~WorkPool() {
+    {
+        std::lock_guard<std::mutex> lk(m_);
+        stop_.store(true);
+    }
+    cv_.notify_all();
+    for (auto& t : threads_) t.join();
+}
+
+void WorkPool::drain() {
+    const uint32_t n = n_tasks_;
+    for (;;) {
+        const uint32_t i = next_.fetch_add(1, std::memory_order_relaxed);
+        if (i >= n) break;
+        (*fn_)(i);
+        done_.fetch_add(1, std::memory_order_release);
+    }
+}
+
+void WorkPool::worker() {
+    uint64_t seen = 0;
+    for (;;) {
+        // Wait for the next job: spin for spin_ns_, then sleep.  gen_ changes
+        // under m_, so a sleeper cannot miss it.
+        const int64_t t0 = now_ns();
+        uint32_t polls = 0;
+        while (gen_.load(std::memory_order_acquire) == seen && !stop_.load(std::memory_order_relaxed)) {
+            cpu_relax();
+            if ((++polls & 255u) == 0 && now_ns() - t0 > spin_ns_) {
+                std::unique_lock<std::mutex> lk(m_);
+                cv_.wait(lk, [&] { return gen_.load(std::memory_order_relaxed) != seen || stop_.load(); });
+            }
+        }
+        if (stop_.load()) return;
+        seen = gen_.load(std::memory_order_acquire);
+        drain();
+        // run() returns only once every worker has left drain() for this job,
+        // so no worker can still be reading fn_ / n_tasks_ when the next job
+        // replaces them.
+        acked_.fetch_add(1, std::memory_order_release);
+    }
+}
+
+void WorkPool::run(uint32_t n, const std::function<void(uint32_t)>& fn) {
+    std::lock_guard<std::mutex> lk(run_m_);
+    if (threads_.empty() || n <= 1) {
+        for (uint32_t i = 0; i < n; ++i) fn(i);
+        return;
+    }
+    fn_ = &fn;
+    n_tasks_ = n;
+    next_.store(0, std::memory_order_relaxed);
+    done_.store(0, std::memory_order_relaxed);
+    acked_.store(0, std::memory_order_relaxed);
+    {
+        std::lock_guard<std::mutex> l2(m_);
+        gen_.fetch_add(1, std::memory_order_release);
+    }
+    cv_.notify_all();
+    drain();
+    while (done_.load(std::memory_order_acquire) < n) cpu_relax();
+    const uint32_t nw = (uint32_t)threads_.size();
+    uint32_t polls = 0;
+    while (acked_.load(std::memory_order_acquire) < nw) {
+        cpu_relax();
+        if ((++polls & 1023u) == 0) std::this_thread::yield();  // a worker that was asleep is still waking
+    }
+}
+
+WorkPool& host_pool() {
+    static WorkPool pool([] {
+        unsigned n = 0;
+        if (const char* s = std::getenv("AC_HOST_THREADS")) n = (unsigned)std::max(1, std::atoi(s));
+        if (!n) {
+            cpu_set_t set;
+            unsigned cpus = std::thread::hardware_concurrency();
+            if (sched_getaffinity(0, sizeof set, &set) == 0) cpus = (unsigned)CPU_COUNT(&set);
+            n = std::max(1u, std::min(16u, cpus));
+        }
+        return n;
+    }());
+    return pool;
+}
+
+namespace {
+
+// 32 Dna5 bases -> two code words (16 bases each, base b at bits 2*(b%16)) and
+// one N-mask word (bit b set iff base b > 3).
+__attribute__((target("avx2"))) inline void pack32_avx2(const uint8_t* src, uint32_t* code2, uint32_t* nm) {
+    const __m256i v = _mm256_loadu_si256((const __m256i*)src);
+    const __m256i three = _mm256_set1_epi8(3);
+    const uint32_t acgt = (uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(_mm256_min_epu8(v, three), v));
+    *nm = ~acgt;
+    const __m256i c = _mm256_and_si256(v, three);
+    // pairs: c0 + 4*c1 (16-bit), then quads: p0 + 16*p1 (32-bit) = one byte of 4 bases
+    __m256i t = _mm256_maddubs_epi16(c, _mm256_set1_epi16(0x0401));
+    t = _mm256_madd_epi16(t, _mm256_set1_epi32(0x00100001));
+    t = _mm256_shuffle_epi8(t, _mm256_setr_epi8(0, 4, 8, 12, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, 0, 4, 8,
+                                                12, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1));
+    code2[0] = (uint32_t)_mm256_extract_epi32(t, 0);
+    code2[1] = (uint32_t)_mm256_extract_epi32(t, 4);
+}
+
+inline void pack32_scalar(const uint8_t* src, uint32_t* code2, uint32_t* nm) {
+    uint32_t c0 = 0, c1 = 0, n = 0;
+    for (int b = 0; b < 16; ++b) {
+        c0 |= (uint32_t)(src[b] & 3u) << (2 * b);
+        c1 |= (uint32_t)(src[16 + b] & 3u) << (2 * b);
+    }
+    for (int b = 0; b < 32; ++b) n |= (uint32_t)(src[b] > 3u) << b;
+    code2[0] = c0;
+    code2[1] = c1;
+    *nm = n;
+}
+
+// AVX-512BW: 64 bases per step, the tail through a byte-masked load (no
+// access past the window, so no over-read of the caller's buffer).  Codes: the
+// 2-bit values multiply-added into one byte per 4 bases, vpmovdb narrows 16
+// such dwords to the 16 bytes of four code words; N: one compare to a k-mask.
+__attribute__((target("avx512f,avx512bw,avx512vl"))) void pack_range_avx512(
+    const uint8_t* bases, const uint64_t* offset, const uint32_t* length, uint32_t w0, uint32_t w1, uint64_t first,
+    uint32_t* codes, uint32_t* nmask, uint64_t* start_out, uint32_t* len_out) {
+    const __m512i three = _mm512_set1_epi8(3);
+    const __m512i pair = _mm512_set1_epi16(0x0401);
+    const __m512i quad = _mm512_set1_epi32(0x00100001);
+    uint64_t pos = first;
+    for (uint32_t w = w0; w < w1; ++w) {
+        const uint8_t* src = bases + offset[w];
+        const uint32_t len = length[w];
+        start_out[w - w0] = pos;
+        len_out[w - w0] = len;
+        const uint64_t span = image_span(len);
+        uint8_t* cw = (uint8_t*)(codes + pos / 16);
+        uint8_t* nw = (uint8_t*)(nmask + pos / 32);
+        for (uint32_t b = 0; b < span; b += 64) {
+            const uint32_t left = len > b ? len - b : 0u;
+            const __mmask64 m = left >= 64 ? ~0ull : ((1ull << left) - 1ull);
+            const __m512i v = _mm512_maskz_loadu_epi8(m, src + b);
+            const uint64_t isn = _mm512_mask_cmpgt_epu8_mask(m, v, three);
+            __m512i t = _mm512_maddubs_epi16(_mm512_and_si512(v, three), pair);
+            t = _mm512_madd_epi16(t, quad);
+            const __m128i c = _mm512_cvtepi32_epi8(t);
+            if (span - b >= 64) {
+                _mm_storeu_si128((__m128i*)(cw + b / 4), c);
+                std::memcpy(nw + b / 8, &isn, 8);
+            } else {  // the last 32 bases of the span: half the words (the next window's follow)
+                _mm_storel_epi64((__m128i*)(cw + b / 4), c);
+                const uint32_t lo = (uint32_t)isn;
+                std::memcpy(nw + b / 8, &lo, 4);
+            }
+        }
+        pos += span;
+    }
+}
+
+template <bool AVX2>
+void pack_range_impl(const uint8_t* bases, const uint64_t* offset, const uint32_t* length, uint32_t w0, uint32_t w1,
+                     uint64_t first, uint32_t* codes, uint32_t* nmask, uint64_t* start_out, uint32_t* len_out) {
+    uint64_t pos = first;
+    alignas(32) uint8_t tail[32];
+    for (uint32_t w = w0; w < w1; ++w) {
+        const uint8_t* src = bases + offset[w];
+        const uint32_t len = length[w];
+        start_out[w - w0] = pos;
+        len_out[w - w0] = len;
+        uint32_t* cw = codes + pos / 16;
+        uint32_t* nw = nmask + pos / 32;
+        const uint32_t full = len / 32;
+        for (uint32_t b = 0; b < full; ++b) {
+            if (AVX2) pack32_avx2(src + 32 * b, cw + 2 * b, nw + b);
+            else pack32_scalar(src + 32 * b, cw + 2 * b, nw + b);
+        }
+        if (const uint32_t r = len % 32) {  // the last block: padding bases are code 0 (A), not N
+            std::memset(tail, 0, sizeof tail);
+            std::memcpy(tail, src + 32 * full, r);
+            if (AVX2) pack32_avx2(tail, cw + 2 * full, nw + full);
+            else pack32_scalar(tail, cw + 2 * full, nw + full);
+        }
+        pos += image_span(len);
+    }
+}
+
+bool have_avx2() {
+    static const bool v = __builtin_cpu_supports("avx2");
+    return v;
+}
+
+bool have_avx512() {
+    static const bool v = __builtin_cpu_supports("avx512bw") && __builtin_cpu_supports("avx512vl") &&
+                          std::getenv("AC_NO_AVX512") == nullptr;
+    return v;
+}
+
+}  // namespace
+
+void pack_dna5_range(const uint8_t* bases, const uint64_t* offset, const uint32_t* length, uint32_t w0, uint32_t w1,
+                     uint64_t first, uint32_t* codes, uint32_t* nmask, uint64_t* start_out, uint32_t* len_out) {
+    if (have_avx512())
+        pack_range_avx512(bases, offset, length, w0, w1, first, codes, nmask, start_out, len_out);
+    else if (have_avx2())
+        pack_range_impl<true>(bases, offset, length, w0, w1, first, codes, nmask, start_out, len_out);
+    else
+        pack_range_impl<false>(bases, offset, length, w0, w1, first, codes, nmask, start_out, len_out);
+}
+
+}  // namespace acamd

@@ -1,0 +1,70 @@
+// host_pack.h -- host side of the host-buffer entry points: a persistent worker
+// pool and the Dna5 -> window-image packer (include/approx_counter_amd.h,
+// ac_error_count_jobs).  The reference hands errorCount its sample as a
+// StringSet<Dna5String>, one byte per base (approx_counter.cpp:38, 531); the
+// GPU reads 2-bit codes + an N bitmap, so the packing is part of the stage.
+#pragma once
+#include <stdint.h>
+
+#include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+namespace acamd {
+
+// A fixed set of worker threads that run the tasks [0, n) of one job
+// together with the calling thread.  Workers spin for a short while after a
+// job (back-to-back calls find them awake: a futex wake costs tens of us,
+// the whole cfg2 stage ~150 us) and then sleep on a condition variable.
+class WorkPool {
+public:
+    explicit WorkPool(unsigned n_threads);  // total participants, caller included
+    ~WorkPool();
+    WorkPool(const WorkPool&) = delete;
+    WorkPool& operator=(const WorkPool&) = delete;
+
+    unsigned size() const { return (unsigned)threads_.size() + 1; }
+    // fn(i) for every i in [0, n); returns when all have run.  One run() at a
+    // time (serialised by a mutex); fn must not call run() itself.
+    void run(uint32_t n, const std::function<void(uint32_t)>& fn);
+
+private:
+    void worker();
+    void drain();
+
+    std::vector<std::thread> threads_;
+    std::mutex run_m_;
+    std::mutex m_;
+    std::condition_variable cv_;
+    std::atomic<uint64_t> gen_{0};
+    std::atomic<uint32_t> next_{0};
+    std::atomic<uint32_t> done_{0};
+    std::atomic<uint32_t> acked_{0};
+    std::atomic<bool> stop_{false};
+    const std::function<void(uint32_t)>* fn_ = nullptr;
+    uint32_t n_tasks_ = 0;
+    int64_t spin_ns_ = 0;
+};
+
+// The process-wide pool of the host-buffer entry points.  Size: the
+// AC_HOST_THREADS environment variable, else min(16, CPUs this process may
+// run on); AC_HOST_THREADS=1 packs on the calling thread alone.
+WorkPool& host_pool();
+
+// Image bases a window of `len` bases occupies (windows start on 32-base
+// boundaries, include/approx_counter_amd.h).
+inline uint64_t image_span(uint32_t len) { return ((uint64_t)len + 31u) / 32u * 32u; }
+
+// Packs windows [w0, w1) of a Dna5 window set into a window image whose window
+// w0 starts at image base `first`: writes the 2-bit codes and the N bitmap of
+// every 32-base block the windows occupy (padding bases as code 0, not N), and
+// the image start / length of each window into start_out[w - w0] /
+// len_out[w - w0].  `codes` / `nmask` are the image's word arrays (indexed by
+// absolute image base).  Dna5 ordinals: 0..3 = A C G T, anything else = N.
+void pack_dna5_range(const uint8_t* bases, const uint64_t* offset, const uint32_t* length, uint32_t w0, uint32_t w1,
+                     uint64_t first, uint32_t* codes, uint32_t* nmask, uint64_t* start_out, uint32_t* len_out);
+
+}  // namespace acamd

@@ -13,6 +13,12 @@
 #define AC_WAVES_PER_SIMD 8  // resident count-kernel waves per SIMD, set by the LDS allocation (<= 64 VGPRs)
 #endif
 
+// Device error word bits (ac_check, include/approx_counter_amd.h): a window
+// that is misaligned or reaches past the image was skipped; the kernel found
+// its set-up broken (the ~Eq table not at LDS address 0) and skipped its work.
+#define AC_DEVERR_WINDOW 1u
+#define AC_DEVERR_SETUP 2u
+
 namespace acamd {
 
 struct SegDev {
@@ -53,6 +59,7 @@ struct LaunchArgs {
     // a launch needs no memset of the counts.
     uint32_t* acc;
     uint32_t* tickets;  // one per AC_QUEUE_LINE u32
+    uint32_t* err;      // AC_DEVERR_* bits, or-ed in by the kernel
     uint32_t add_counts;
     uint32_t n_segs;
     uint32_t m;  // k-mer length

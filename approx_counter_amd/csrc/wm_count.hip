@@ -255,9 +255,10 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
     const uint32_t eb = __builtin_amdgcn_readfirstlane(
         (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)(&lds.tab.e[0]));
     // The eb0 blocks address the table from LDS 0.  Never expected otherwise;
-    // if it were, the waves skip the work (no fault) and the counts come out
-    // short, which the parity tests catch.
+    // if it were, the waves skip the work (no fault) and report it in the
+    // device error word (ac_check) instead of returning short counts silently.
     const bool eb_ok = !TID_EB0 || eb == 0u;
+    if (!eb_ok && lane == 0) atomicOr(a.err, AC_DEVERR_SETUP);
 
     // Counters of the other queue bank are zeroed for the next launch (strided
     // over the waves; nobody dequeues from that bank in this launch).
@@ -354,13 +355,16 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
     uint32_t w = item * chunk, item_end = min(sg.n_windows, w + chunk);
 
     // Window pipeline: the next window's first segment is fetched while the current one is counted.
-    auto valid = [&](uint64_t base, uint32_t len) { return !(base & 31u) && base + len <= g_nbases; };
+    // (written so that no sum wraps: a start near 2^64 must not pass)
+    auto valid = [&](uint64_t base, uint32_t len) { return !(base & 31u) && len <= g_nbases && base <= g_nbases - len; };
+    // an empty window reads no word (its start may be the image's end)
+    auto fetchable = [&](uint64_t base, uint32_t len) { return len != 0u && valid(base, len); };
     uint64_t nbase = 0;
     uint32_t nlen = 0;
     uint32_t nf = 0;
     if (item < n_items) {
         load_desc(g_start, g_length, w, nbase, nlen);
-        if (valid(nbase, nlen)) nf = tid_fetch(g_codes + (nbase >> 4), g_nmask + (nbase >> 5), nlen, 0, lane);
+        if (fetchable(nbase, nlen)) nf = tid_fetch(g_codes + (nbase >> 4), g_nmask + (nbase >> 5), nlen, 0, lane);
     }
 
     // ~Eq table, built by wave 0 of the workgroup (the waves share the
@@ -405,6 +409,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
             pending = dequeue_issue();
         }
         const bool ok = valid(base, len);  // a malformed window is skipped: never read outside the image
+        if (!ok && lane == 0) atomicOr(a.err, AC_DEVERR_WINDOW);
         const uint32_t nb0 = ok ? min(SEG, len) : 0u;
         const uint32_t nfull0 = nb0 >> 4;
         TidNfa s = {~0u, d1_init, d2_init, ~0u >> P, d1_init >> P, d2_init >> P, ~0u, d1_init, d2_init};
@@ -424,12 +429,12 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
             if (nitem < n_items) {
                 load_desc(g_start, g_length, nitem * chunk, nbase, nlen);
             }
-        } else if (valid(nbase, nlen)) {
+        } else if (fetchable(nbase, nlen)) {
             nf = tid_fetch(g_codes + (nbase >> 4), g_nmask + (nbase >> 5), nlen, 0, lane);
         }
         // step 2 (after block 1): the next item's first words
         if (nfull0 >= 4u) block32(f0, 2u);
-        if (last && nitem < n_items && valid(nbase, nlen))
+        if (last && nitem < n_items && fetchable(nbase, nlen))
             nf = tid_fetch(g_codes + (nbase >> 4), g_nmask + (nbase >> 5), nlen, 0, lane);
         if (ok) {
             auto segment = [&](uint32_t f, uint32_t sb, uint32_t ch) __attribute__((always_inline)) {
@@ -467,7 +472,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
                 item = __builtin_amdgcn_readfirstlane(steal());
                 if (item < n_items) {
                     load_desc(g_start, g_length, item * chunk, nbase, nlen);
-                    if (valid(nbase, nlen))
+                    if (fetchable(nbase, nlen))
                         nf = tid_fetch(g_codes + (nbase >> 4), g_nmask + (nbase >> 5), nlen, 0, lane);
                 }
             }

@@ -2,35 +2,44 @@
 """Benchmark of the approximate-count stage (errorCount, approx_counter.cpp:531-601).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4|cfg5]
+                    [--scaling weak|strong]
 
-A step is one pass of the hot path over one batch: both read ends of one run
-(start + end windows, approx_counter.cpp:858) counted against their own
-top-`lim` candidates in ONE fused kernel launch, which also stores the count
-vector (no separate zeroing dispatch), inputs already resident in HBM.  Default workload = BASELINE.json
-configs[1] (k=16, sn=10,000, sl=100, lim=500), the configuration the metric is
-quoted on, on seeded synthetic reads.  With N > 1 ranks (one
-process per GPU, torchrun) every rank counts its own sn reads against the same
-candidates and the per-candidate count vector is summed with one RCCL
-all-reduce per step (weak scaling); the all-reduce of step i overlaps the
-count launch of step i+1 (two count buffers, async_op).  Rank 0 prints ONE JSON line.
+A step is one pass of the stage BASELINE.md defines over one batch: both read
+ends of one run (start + end windows, approx_counter.cpp:858), each against its
+own top-`lim` candidates, from HOST buffers to HOST counts -- the sample as a
+StringSet<Dna5String> (one byte per base, what errorCount receives), packed to
+2-bit codes + N bitmap by the library's host worker pool into pinned memory, one
+DMA, ONE fused kernel launch over both ends, (N > 1: one RCCL all-reduce of the
+count vector), counts back.  That is `value`.  Default workload = BASELINE.json
+configs[1] (k=16, sn=10,000, sl=100, lim=500), on seeded synthetic reads
+(SURVEY.md §8(d)).
 
-Roofline: the count kernel is bound by integer VALU
-issue, not HBM and not MFMA.  `roofline.achieved` = algorithmic VALU lane-ops
-per launch / mean kernel duration (HIP events around every 5th timed launch,
-on the launch stream, inside the timed loop: an event is a queue packet of its
-own and bracketing every launch adds ~3 us between launches); algorithmic work = 9.5 full-rate lane
-ops per text base per lane word of P candidates (P = 2 at k=16, 1 at k=22):
-the 8 ops of the Wu-Manber NFA for 3 rows + 1.5 of hit accumulation, with ~Eq
-a table lookup as in the textbook algorithm;
-`peak` = 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (MI355X_MICROARCH.md: SIMD-32,
-2-cycle wave64 VALU issue).  `traffic` = HBM bytes per launch from the
-committed rocprofv3 PMC passes (profiles/*_pmc_traffic.json) for the same
-workload, FETCH_SIZE doubled per the gfx950 correction, or null.
+Multi-GPU (one process per GPU, torchrun): `--scaling weak` (default except
+cfg4) gives every rank its own sn reads against the same candidates;
+`--scaling strong` (cfg4's default, BASELINE "sn=1M sharded over 8 GPUs") builds
+ONE sample and gives rank r its contiguous shard (balanced by bases,
+approx_counter_amd/shard.py).  Either way each step ends with one RCCL
+all-reduce (sum) of the per-candidate count vector and its copy to the host.
+
+Also reported (never as `value`): `kernel_ms` / `kernel_kmer_bp_per_s`, the
+count kernel alone on device-resident inputs (HIP events around every 5th
+launch, on the launch stream), the basis of `roofline`; `pipelined`, the same
+host-buffer steps issued back to back with ac_error_count_jobs_submit (a step's
+packing overlaps the previous step's kernel: runs of -mr are independent).
+
+Roofline: the count kernel is bound by integer VALU issue, not
+HBM and not MFMA.  `roofline.frac` = algorithmic lane-ops / kernel time / peak,
+with 9.5 lane-ops per text base per lane word of P = floor(32/k) candidates
+(the Wu-Manber NFA's 8 + 1.5 of hit accumulation; ~Eq a table lookup);
+`frac_survey_basis` is the same time on SURVEY.md §8(d)'s 20 ops per kmer*bp;
+`sq_insts_valu` is the measured wave-instruction count of a committed PMC pass
+(profiles/*_pmc_traffic.json), next to the 9.5/P model.  `peak` = 256 CU x 4
+SIMD x 32 lanes x 2.4 GHz.  `traffic` = HBM bytes per launch from the same PMC
+files (FETCH_SIZE doubled per the gfx950 correction), or null.
 """
 from __future__ import annotations
 
 import argparse
-import copy
 import glob
 import json
 import os
@@ -46,13 +55,16 @@ METRIC = "approx-count kmer×base pairs/sec (k=16, lim=500, 10k×100bp ends)"
 VALU_PEAK_OPS = 256 * 4 * 32 * 2.4e9       # int32 lane-ops/s (2-cycle wave64 issue per SIMD-32)
 HBM_PEAK = 8.0e12                           # B/s (MI355X_MICROARCH.md, spec)
 OPS_PER_BASE_WORD = 9.5                     # 8 NFA + 1.5 hit accumulation (~Eq: LDS table)
+SURVEY_OPS_PER_UNIT = 20.0                  # one Myers column, 20 int32 ops per kmer*bp
 SAMPLE_BYTES_PER_BASE = 0.375               # 2-bit code + 1-bit N mask, read once
+DATA_NOTE = ("synthetic (seeded reads, SURVEY.md 8(d)); host Dna5 buffers in, host counts out; "
+             "bit-exact vs model M1 (oracle/), parity with SeqAn unpinned (SURVEY.md 0)")
 
-CONFIGS = {  # BASELINE.json configs (sn per rank for the bench)
-    "cfg2": dict(k=16, sn=10_000, sl=100, lim=500),
-    "cfg3": dict(k=16, sn=100_000, sl=100, lim=2000),
-    "cfg4": dict(k=16, sn=1_000_000, sl=100, lim=500),
-    "cfg5": dict(k=22, sn=100_000, sl=150, lim=1000),
+CONFIGS = {  # BASELINE.json configs
+    "cfg2": dict(k=16, sn=10_000, sl=100, lim=500, scaling="weak"),
+    "cfg3": dict(k=16, sn=100_000, sl=100, lim=2000, scaling="weak"),
+    "cfg4": dict(k=16, sn=1_000_000, sl=100, lim=500, scaling="strong"),
+    "cfg5": dict(k=22, sn=100_000, sl=150, lim=1000, scaling="weak"),
 }
 
 
@@ -62,27 +74,24 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
+    ap.add_argument("--scaling", choices=("weak", "strong"),
+                    help="N > 1: weak = every rank its own sn reads; strong = one sample sharded over the ranks")
     ap.add_argument("--k", type=int)
     ap.add_argument("--sn", type=int)
     ap.add_argument("--sl", type=int)
     ap.add_argument("--lim", type=int)
     ap.add_argument("--read-len", type=int, default=400)
     ap.add_argument("--seed", type=int, default=1)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0,
-                    help="target duration of the bounded CPU-baseline sample")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="total duration of the bounded CPU-baseline samples")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-host-boundary", action="store_true",
-                    help="skip the PCIe-inclusive host-buffer timing (keeps a rocprof trace to the timed launches)")
-    ap.add_argument("--inflight", type=int, default=1,
-                    help="batches in flight: independent counter contexts on their own HIP streams, "
-                         "steps dealt round-robin, so one batch's launch tail overlaps the next one's start")
-    ap.add_argument("--no-inflight-probe", action="store_true",
-                    help="skip the informational two-batches-in-flight timing of a 1-GPU run")
-    ap.add_argument("--verify", action="store_true", help="check counts against the oracle (slow)")
+    ap.add_argument("--no-kernel-leg", action="store_true",
+                    help="skip the device-resident kernel timing (and with it the roofline)")
+    ap.add_argument("--no-pipelined", action="store_true", help="skip the informational pipelined leg")
+    ap.add_argument("--verify", action="store_true", help="check the stage's counts against the oracle (slow)")
     ap.add_argument("--event-every", type=int, default=5,
-                    help="bracket every N-th timed launch with HIP events (the kernel-duration sample); "
-                         "each event is a queue packet of its own, ~3 us between launches when every "
-                         "launch is bracketed")
+                    help="bracket every N-th kernel-leg launch with HIP events (each event is a queue "
+                         "packet of its own: ~3 us between launches when every launch is bracketed)")
     a = ap.parse_args()
     for key, v in CONFIGS[a.config].items():
         if getattr(a, key) is None:
@@ -91,34 +100,68 @@ def parse():
     return a
 
 
+def cpu_share():
+    """(CPUs this process may run on = nproc, CPU quota of its cgroup or None)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(period)
+    except (OSError, ValueError):
+        pass
+    return n, quota
+
+
 def cpu_baseline(wl, k, seconds):
-    """The oracle's OpenMP Myers restatement (the 'port' CPU path) timed on this
-    host's cores over the same workload (both ends), repeated to fill ~`seconds`."""
+    """The oracle's OpenMP Myers restatement (kind "port": the reference's SeqAn
+    FM-index path cannot be built here) on this host's cores:
+    all `nproc` CPUs (the headline), the cgroup's CPU quota, and one thread on a
+    bounded subset of the candidates."""
     import oracle
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    units_rep = sum(wl[e]["kmers"].size * sum(int(w.size) for w in wl[e]["windows"]) for e in ("start", "end"))
+    nproc, quota = cpu_share()
+    ends = ("start", "end")
+    bases = {e: sum(int(w.size) for w in wl[e]["windows"]) for e in ends}
 
-    def one():
-        for e in ("start", "end"):
-            oracle.count_myers(k, wl[e]["kmers"], wl[e]["windows"], threads)
+    def leg(threads, frac_cands, budget):
+        sub = {e: wl[e]["kmers"][: max(1, int(round(wl[e]["kmers"].size * frac_cands)))] for e in ends}
+        units = sum(sub[e].size * bases[e] for e in ends)
+        t = time.perf_counter()
+        for e in ends:
+            oracle.count_myers(k, sub[e], wl[e]["windows"], threads)
+        dt1 = max(time.perf_counter() - t, 1e-6)
+        reps = max(1, int(budget / dt1))
+        t = time.perf_counter()
+        for _ in range(reps):
+            for e in ends:
+                oracle.count_myers(k, sub[e], wl[e]["windows"], threads)
+        dt = time.perf_counter() - t
+        return units * reps / dt, units, reps, dt
 
-    t = time.perf_counter()
-    one()
-    dt1 = max(time.perf_counter() - t, 1e-6)
-    reps = max(1, int(seconds / dt1))
-    t = time.perf_counter()
-    for _ in range(reps):
-        one()
-    dt = time.perf_counter() - t
-    return {"value": units_rep * reps / dt, "unit": "kmer*bp/s", "cores": threads, "kind": "port",
-            "sample": f"the full workload (both ends, {units_rep:.4g} kmer*bp) x {reps} repetitions = {dt:.1f} s; "
-                      f"oracle/ac_oracle.c Myers bit-vector, OpenMP over candidates (the reference's SeqAn "
-                      f"FM-index path cannot be built here: SURVEY.md 8(c))"}
+    v, units, reps, dt = leg(nproc, 1.0, seconds * 0.5)
+    out = {"value": v, "unit": "kmer*bp/s", "cores": nproc, "kind": "port",
+           "sample": f"the full workload (both ends, {units:.4g} kmer*bp) x {reps} = {dt:.1f} s on {nproc} OpenMP "
+                     f"threads (nproc; cgroup CPU quota {quota if quota else 'none'}); oracle/ac_oracle.c Myers "
+                     f"bit-vector, OpenMP over candidates (restated CPU path: SeqAn is absent, SURVEY.md 8(c))"}
+    if quota and int(quota) < nproc:
+        q = max(1, int(quota))
+        vq, units, reps, dt = leg(q, 1.0, seconds * 0.25)
+        out["quota_threads"] = {"value": vq, "threads": q,
+                                "sample": f"full workload x {reps} = {dt:.1f} s on {q} threads (the cgroup quota)"}
+    v1, units, reps, dt = leg(1, 0.05, seconds * 0.25)
+    out["one_thread"] = {"value": v1, "threads": 1,
+                         "sample": f"5% of the candidates of both ends over all windows ({units:.4g} kmer*bp) x {reps} "
+                                   f"= {dt:.1f} s"}
+    return out
 
 
-def load_traffic(workload: str):
-    """HBM bytes per launch of the count kernel from committed PMC summaries."""
+def load_pmc(workload: str):
+    """PMC summary (HBM bytes, VALU instructions per launch) of the count kernel
+    for this workload from the committed profiles/*_pmc_traffic.json files."""
     best = None
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json"))):
         try:
@@ -126,8 +169,42 @@ def load_traffic(workload: str):
         except (OSError, ValueError):
             continue
         if d.get("workload") == workload:
-            best = d
+            best = d if best is None else {**best, **d}
     return best
+
+
+def build_workload(args, rank, world):
+    """This rank's {end: {kmers, windows}} and the units of the whole job per step."""
+    from approx_counter_amd.shard import shard_bounds
+    from tools import workload
+
+    ends = ("start", "end")
+    if args.scaling == "strong" or world == 1:
+        if args.sn >= 500_000:
+            full = workload.build_fast(n_reads=args.sn, k=args.k, sl=args.sl, lim=args.lim, seed=args.seed)
+        else:
+            full, _ = workload.build(n_reads=args.sn, read_len=args.read_len, k=args.k, sl=args.sl,
+                                     lim=args.lim, seed=args.seed)
+        units_job = sum(full[e]["kmers"].size * sum(int(w.size) for w in full[e]["windows"]) for e in ends)
+        if world == 1:
+            return full, units_job
+        wl = {}
+        for e in ends:
+            w = full[e]["windows"]
+            c = shard_bounds([len(x) for x in w], world)
+            wl[e] = {"kmers": full[e]["kmers"], "windows": w[c[rank]:c[rank + 1]]}
+        return wl, units_job
+    if args.sn >= 500_000:
+        wl = workload.build_fast(n_reads=args.sn, k=args.k, sl=args.sl, lim=args.lim, seed=args.seed + 7919 * rank)
+        if rank:  # the same candidates on every rank (rank 0's)
+            c0 = workload.build_fast(n_reads=20_000, k=args.k, sl=args.sl, lim=args.lim, seed=args.seed)
+            for e in ends:
+                wl[e]["kmers"] = c0[e]["kmers"]
+    else:
+        wl, _ = workload.build(n_reads=args.sn, read_len=args.read_len, k=args.k, sl=args.sl, lim=args.lim,
+                               seed=args.seed, shard=rank, n_shards=world)
+    units_rank = sum(wl[e]["kmers"].size * sum(int(w.size) for w in wl[e]["windows"]) for e in ends)
+    return wl, units_rank * world
 
 
 def main():
@@ -152,95 +229,44 @@ def main():
             dist.init_process_group(backend)
 
     import approx_counter_amd as ac
-    from tools import workload
 
-    wl, _ = workload.build(n_reads=args.sn, read_len=args.read_len, k=args.k, sl=args.sl,
-                           lim=args.lim, seed=args.seed, shard=rank, n_shards=world)
+    wl, units_job = build_workload(args, rank, world)
     ends = ("start", "end")
     n_c = [int(wl[e]["kmers"].size) for e in ends]
-    packed = {e: ac.pack_windows(wl[e]["windows"]) for e in ends}
-    base_segs = [ac.DeviceSegment.upload(wl[e]["kmers"], packed[e], device=dev) for e in ends]
-    n_slots = max(1, args.inflight)
-    # rank 0 of a 1-GPU run also times two batches in flight (informational `inflight_2`)
-    extra_slot = world == 1 and n_slots == 1 and not args.no_inflight_probe
-    n_build = n_slots + (1 if extra_slot else 0)
-    # One slot per batch in flight: its own counter context (device scratch, queue counters),
-    # its own stream and two count vectors.  With N > 1 ranks the RCCL all-reduce of a slot's
-    # step runs on the communicator's stream while that slot counts its next step into the
-    # other vector.
-    slots = []
-    for si in range(n_build):
-        counter_s = ac.ApproxCounter(local)
-        st = torch.cuda.current_stream(dev) if si == 0 else torch.cuda.Stream(dev)
-        bufs = [torch.zeros(sum(n_c), dtype=torch.int32, device=dev) for _ in range(2)]
-        seg_sets = []
-        for buf in bufs:
-            off, ss = 0, []
-            for seg, n in zip(base_segs, n_c):
-                s2 = copy.copy(seg)
-                s2.counts = buf[off:off + n]
-                off += n
-                ss.append(s2)
-            seg_sets.append(ss)
-        slots.append(dict(counter=counter_s, stream=st, bufs=bufs, seg_sets=seg_sets,
-                          arrays=[ac.ApproxCounter.segment_array(ss) for ss in seg_sets],
-                          pending=[None, None], n=0))
-    counter = slots[0]["counter"]
-    segs = slots[0]["seg_sets"][0]
     bases = [sum(int(w.size) for w in wl[e]["windows"]) for e in ends]
-    units = sum(n * b for n, b in zip(n_c, bases))
-    sp = slots[0]["stream"].cuda_stream
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    units_rank = sum(n * b for n, b in zip(n_c, bases))
+    jobs = ac.Jobs([(wl[e]["kmers"], ac.Dna5Sample.from_windows(wl[e]["windows"])) for e in ends])
+    counter = ac.ApproxCounter(local)
+    stream = torch.cuda.current_stream(dev)
+    d_counts = torch.zeros(max(1, jobs.n_counts), dtype=torch.int32, device=dev)
+    h_counts = torch.zeros(max(1, jobs.n_counts), dtype=torch.int32).pin_memory()
 
-    n_step = [0]
-
-    active = [n_slots]
-
-    def step(i=None):
-        sl = slots[n_step[0] % active[0]]
-        n_step[0] += 1
-        b = sl["n"] % 2
-        sl["n"] += 1
-        buf = sl["bufs"][b]
-        st = sl["stream"]
-        if sl["pending"][b] is not None:  # the buffer's previous all-reduce must finish first
-            with torch.cuda.stream(st):
-                sl["pending"][b].wait()
-            sl["pending"][b] = None
-        if i is not None:
-            evs[i][0].record(st)
-        # ac_error_count_device: the counts are stored by the launch itself (no memset)
-        sl["counter"].count_device(args.k, sl["arrays"][b], stream=st.cuda_stream)
-        if i is not None:
-            evs[i][1].record(st)
-        if world > 1:
+    # ---- the stage (value): host Dna5 buffers -> host counts ---------------------------------
+    if world == 1:
+        def step():
+            counter.count_jobs(args.k, jobs)  # pack, one DMA, one fused launch, counts back (synchronous)
+    else:
+        def step():
+            counter.submit_jobs(args.k, jobs, d_counts, stream=stream.cuda_stream)
             if backend == "nccl":
-                with torch.cuda.stream(st):
-                    sl["pending"][b] = dist.all_reduce(buf, async_op=True)
+                dist.all_reduce(d_counts)  # RCCL over xGMI, on the current stream
+                h_counts.copy_(d_counts, non_blocking=True)
+                stream.synchronize()
             else:
-                st.synchronize()
-                host = buf.cpu()
+                stream.synchronize()
+                host = d_counts.cpu()
                 dist.all_reduce(host)
-                buf.copy_(host)
-
-    def drain():
-        for sl in slots:
-            for b in range(2):
-                if sl["pending"][b] is not None:
-                    sl["pending"][b].wait()
-                    sl["pending"][b] = None
+                h_counts.copy_(host)
 
     for _ in range(args.warmup):
         step()
-    drain()
+    torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(i if i % max(1, args.event_every) == 0 else None)
-    t_enq = time.perf_counter() - t0  # host enqueue time of the K steps (diagnostic)
-    drain()
+    for _ in range(args.steps):
+        step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -249,98 +275,122 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    kern_ms = float(np.mean([evs[i][0].elapsed_time(evs[i][1])
-                             for i in range(0, args.steps, max(1, args.event_every))]))
-    geo = counter.last_launch()
 
-    if args.verify:
+    if args.verify and world == 1:  # (N > 1: tests/test_gpu_multirank.py covers the sharded path)
         import oracle
 
-        counter.count_device(args.k, segs, stream=sp)
+        got = counter.count_jobs(args.k, jobs)
+        for e, g in zip(ends, got):
+            assert np.array_equal(g, oracle.count_myers(args.k, wl[e]["kmers"], wl[e]["windows"])), e
+        print("verify ok: the stage's counts equal the oracle's", file=sys.stderr, flush=True)
+
+    # ---- kernel-only leg (device-resident inputs; the roofline's basis) ----------------------
+    kern_ms = None
+    geo = None
+    if not args.no_kernel_leg:
+        segs = [ac.DeviceSegment.upload(wl[e]["kmers"], ac.pack_windows(wl[e]["windows"]), device=dev) for e in ends]
+        arr = ac.ApproxCounter.segment_array(segs)
+        kc = ac.ApproxCounter(local)
+        for _ in range(args.warmup):
+            kc.count_device(args.k, arr, stream=stream.cuda_stream)
+        every = max(1, args.event_every)
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(0, args.steps, every)]
+        for i in range(args.steps):
+            if i % every == 0:
+                evs[i // every][0].record(stream)
+            kc.count_device(args.k, arr, stream=stream.cuda_stream)
+            if i % every == 0:
+                evs[i // every][1].record(stream)
         torch.cuda.synchronize(dev)
-        for e, seg in zip(ends, segs):
-            exp = oracle.count_myers(args.k, wl[e]["kmers"], wl[e]["windows"])
-            assert np.array_equal(seg.counts_numpy(), exp), f"parity failure on {e}"
+        kc.check(stream=stream.cuda_stream)
+        kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+        geo = kc.last_launch()
+        kc.close()
+
+    # ---- pipelined leg (informational, 1 GPU): host-buffer steps back to back ----------------
+    pipelined = None
+    if world == 1 and not args.no_pipelined:
+        bufs = [torch.zeros(max(1, jobs.n_counts), dtype=torch.int32, device=dev) for _ in range(2)]
+        hosts = [torch.zeros(max(1, jobs.n_counts), dtype=torch.int32).pin_memory() for _ in range(2)]
+
+        def pstep(i):
+            counter.submit_jobs(args.k, jobs, bufs[i % 2], stream=stream.cuda_stream)
+            hosts[i % 2].copy_(bufs[i % 2], non_blocking=True)
+
+        for i in range(args.warmup):
+            pstep(i)
+        torch.cuda.synchronize(dev)
+        tp = time.perf_counter()
+        for i in range(args.steps):
+            pstep(i)
+        torch.cuda.synchronize(dev)
+        elp = time.perf_counter() - tp
+        counter.check(stream=stream.cuda_stream)
+        pipelined = {"value": units_rank * args.steps / elp, "unit": "kmer*bp/s", "ms_per_step": elp / args.steps * 1e3,
+                     "note": "same host-buffer steps via ac_error_count_jobs_submit + async D2H, not synchronised per "
+                             "step: step i+1's packing and DMA overlap step i's kernel (independent -mr runs)"}
 
     if rank == 0:
         P = min(32 // args.k, 4)
+        reads_note = (f"{args.sn} reads sharded over {world} ranks" if world > 1 and args.scaling == "strong"
+                      else f"{args.sn} reads/rank")
         workload_name = (f"{args.config}: k={args.k} sn={args.sn} sl={args.sl} lim={args.lim}, "
-                         f"start+end ends fused, {args.sn} reads/rank")
-        ops = OPS_PER_BASE_WORD / P * units  # algorithmic lane-ops per launch (one rank)
-        achieved = ops / (kern_ms * 1e-3)
-        sample_bytes = SAMPLE_BYTES_PER_BASE * sum(bases) + 12 * sum(n_c)  # sample + kmers in + counts out
-        tr = load_traffic(workload_name)
+                         f"start+end ends fused, {reads_note}")
         out = {
             "metric": METRIC,
-            "value": units * args.steps * world / elapsed,
+            "value": units_job * args.steps / elapsed,
             "unit": "kmer*bp/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling if world > 1 else "weak",
             "vs_baseline": None,
             "dtype": "u32",
-            "data": "synthetic (seeded reads, SURVEY.md 8(d)); inputs resident in HBM",
-            "config": {"workload": workload_name, "k": args.k, "sn_per_rank": args.sn, "sl": args.sl,
-                       "lim": args.lim, "candidates": n_c, "kmer_bp_per_rank_step": units,
-                       "batches_in_flight": n_slots,
-                       "parallelism": f"window shards x{world}, {'RCCL' if backend == 'nccl' else backend} "
-                                      f"all-reduce of counts" if world > 1 else "1 GPU"},
-            "kernel_ms": kern_ms,
-            "host_enqueue_ms_per_step": t_enq / args.steps * 1e3,
-            "kernel_kmer_bp_per_s": units / (kern_ms * 1e-3),
-            "launch": geo,
-            "roofline": {"bound": "valu", "achieved": achieved / 1e12, "peak": VALU_PEAK_OPS / 1e12,
-                         "unit": "Tops/s", "frac": achieved / VALU_PEAK_OPS,
-                         "traffic": tr["hbm_bytes_per_launch"] if tr else None,
-                         "note": f"int32 VALU lane-ops, {OPS_PER_BASE_WORD}/P per kmer*bp (P={P}); HIP events "
-                                 f"around every {max(1, args.event_every)}th timed launch; traffic from "
-                                 f"{os.path.basename(tr['source']) if tr else 'n/a'}"},
-            "roofline_hbm": {"bound": "hbm (informational)", "achieved": sample_bytes / (kern_ms * 1e-3) / 1e9,
-                             "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                             "frac": sample_bytes / (kern_ms * 1e-3) / HBM_PEAK,
-                             "algorithmic_bytes_per_launch": sample_bytes},
+            "data": DATA_NOTE,
+            "config": {"workload": workload_name, "k": args.k, "sn": args.sn, "sl": args.sl, "lim": args.lim,
+                       "candidates": n_c, "kmer_bp_per_step": units_job, "kmer_bp_per_rank_step": units_rank,
+                       "stage": "Dna5 host buffers -> pack (host pool, pinned) -> 1 DMA -> 1 fused launch (both ends)"
+                                + (" -> RCCL all-reduce" if world > 1 else "") + " -> counts D2H",
+                       "parallelism": (f"{args.scaling} window shards x{world}, "
+                                       f"{'RCCL' if backend == 'nccl' else backend} all-reduce of counts")
+                       if world > 1 else "1 GPU"},
         }
-        if world == 1 and not args.no_host_boundary:
-            # The drop-in entry point hands over host buffers (ac_error_count: H2D of the packed
-            # sample and candidates, the kernel, D2H of the counts), one call per read end.  Reported
-            # beside `value`, never as it.
-            reps = max(5, args.steps // 5)
-            for e in ends:
-                counter.count(args.k, wl[e]["kmers"], packed[e])
-            t_h = time.perf_counter()
-            for _ in range(reps):
-                for e in ends:
-                    counter.count(args.k, wl[e]["kmers"], packed[e])
-            host_s = (time.perf_counter() - t_h) / reps
-            out["host_boundary"] = {"value": units / host_s, "unit": "kmer*bp/s", "ms_per_step": host_s * 1e3,
-                                    "note": "ac_error_count with host buffers (PCIe-inclusive: H2D of the 2-bit "
-                                            "sample + candidates, kernel, D2H of counts), both ends, synchronous"}
-        if extra_slot:
-            # Two batches in flight: the same steps dealt alternately to two counter contexts on
-            # two streams, so one launch's tail overlaps the next one's start.
-            # Reported beside `value` (which keeps one batch in flight and per-launch kernel
-            # times), never as it.
-            active[0] = 2
-            for _ in range(args.warmup):
-                step()
-            torch.cuda.synchronize(dev)
-            t2 = time.perf_counter()
-            for _ in range(args.steps):
-                step()
-            torch.cuda.synchronize(dev)
-            el2 = time.perf_counter() - t2
-            active[0] = n_slots
-            out["inflight_2"] = {"value": units * args.steps / el2, "unit": "kmer*bp/s",
-                                 "ms_per_step": el2 / args.steps * 1e3,
-                                 "note": "2 batches in flight (2 contexts, 2 streams), same steps and workload"}
+        if kern_ms is not None:
+            ops = OPS_PER_BASE_WORD / P * units_rank  # algorithmic lane-ops per launch (this rank)
+            achieved = ops / (kern_ms * 1e-3)
+            pmc = load_pmc(workload_name.replace(reads_note, f"{args.sn} reads/rank")) if world == 1 else None
+            sample_bytes = SAMPLE_BYTES_PER_BASE * sum(bases) + 12 * sum(n_c)  # sample + kmers in + counts out
+            roof = {"bound": "valu", "achieved": achieved / 1e12, "peak": VALU_PEAK_OPS / 1e12, "unit": "Tops/s",
+                    "frac": achieved / VALU_PEAK_OPS,
+                    "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
+                    "frac_survey_basis": SURVEY_OPS_PER_UNIT * units_rank / (kern_ms * 1e-3) / VALU_PEAK_OPS,
+                    "note": f"int32 VALU lane-ops, {OPS_PER_BASE_WORD}/P per kmer*bp (P={P}) over the kernel-only "
+                            f"time (HIP events around every {max(1, args.event_every)}th launch); frac_survey_basis = "
+                            f"the same time on SURVEY.md 8(d)'s 20 ops per kmer*bp (> 1 means that op model "
+                            f"overestimates a P-packed NFA, not skipped work: counts are bit-exact); PMC from "
+                            f"{pmc.get('source') if pmc else 'n/a'}"}
+            if pmc and pmc.get("sq_insts_valu_per_launch"):
+                model = OPS_PER_BASE_WORD / P * units_rank / 64.0  # wave instructions
+                roof["sq_insts_valu"] = {"measured_per_launch": pmc["sq_insts_valu_per_launch"],
+                                         "model_per_launch": model,
+                                         "ratio": pmc["sq_insts_valu_per_launch"] / model}
+            out["kernel_ms"] = kern_ms
+            out["kernel_kmer_bp_per_s"] = units_rank / (kern_ms * 1e-3)
+            out["launch"] = geo
+            out["roofline"] = roof
+            out["roofline_hbm"] = {"bound": "hbm (informational)",
+                                   "achieved": sample_bytes / (kern_ms * 1e-3) / 1e9, "peak": HBM_PEAK / 1e9,
+                                   "unit": "GB/s", "frac": sample_bytes / (kern_ms * 1e-3) / HBM_PEAK,
+                                   "algorithmic_bytes_per_launch": sample_bytes}
+        if pipelined:
+            out["pipelined"] = pipelined
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(wl, args.k, args.cpu_seconds)
         print(json.dumps(out), flush=True)
-    for sl in slots:
-        sl["counter"].close()
+    counter.close()
     if world > 1:
         dist.destroy_process_group()
 

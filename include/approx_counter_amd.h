@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define AC_ABI_VERSION 1
+#define AC_ABI_VERSION 2
 
 typedef int32_t ac_status;
 #define AC_OK 0
@@ -194,6 +194,69 @@ uint64_t ac_image_bases(const uint32_t* seq_len, uint32_t n);
 ac_status ac_pack_windows(const uint8_t* dna5, const uint64_t* seq_start, const uint32_t* seq_len,
                           uint32_t n, uint32_t* codes, uint32_t* nmask, uint64_t* start,
                           uint32_t* length, uint64_t n_bases);
+
+/*
+ * The sample exactly as errorCount receives it: a StringSet<Dna5String>
+ * (approx_counter.cpp:38, filled by sampleSequences 415-476), one byte per
+ * base.  Window i is bases[offset[i] .. offset[i] + length[i]); bases are
+ * Dna5 ordinals (0..3 = A C G T, anything else = N; SeqAn's ordValue).
+ * Windows may overlap or come in any order.
+ */
+typedef struct ac_dna5_windows {
+    const uint8_t* bases;
+    const uint64_t* offset;
+    const uint32_t* length;
+    uint32_t n_windows;
+} ac_dna5_windows;
+
+/* One errorCount call (approx_counter.cpp:922) over a Dna5 sample. */
+typedef struct ac_job {
+    const uint64_t* kmers; /* dna2int layout (approx_counter.cpp:55-62)         */
+    uint32_t n_kmers;
+    ac_dna5_windows sample;
+    uint64_t* counts;      /* host, n_kmers; ignored by ac_error_count_jobs_submit */
+} ac_job;
+
+/*
+ * errorCount (approx_counter.cpp:531-601) for up to AC_MAX_JOBS calls that
+ * share k -- both read ends of one run (the loop at 858-953) -- in one
+ * synchronous call, host buffers in and out: jobs[j].counts[i] = M1 count of
+ * jobs[j].kmers[i] over jobs[j].sample.  The whole stage runs here: the Dna5
+ * windows are packed to 2-bit codes + N bitmap by the host worker pool
+ * straight into a pinned staging block, sent in one DMA, counted by ONE fused
+ * kernel launch over all jobs, and the counts come back in one DMA.  On an
+ * ac_create_multi context every job's windows are split into contiguous shards
+ * balanced by bases, one per device, and the shard counts are summed.
+ * Replaces the index build (537-541), the OpenMP search loop (547-599) and
+ * results[kmer] = total (595-596) of each call.
+ */
+#define AC_MAX_JOBS 4
+ac_status ac_error_count_jobs(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint32_t n_jobs);
+
+/*
+ * The same stage without the way back, for callers that combine shards with
+ * a device collective (one process per GPU, RCCL all-reduce of the count
+ * vector): packs and sends the jobs and launches the count
+ * kernel on `hip_stream`, which writes uint32 counts to DEVICE memory
+ * d_counts (jobs concatenated in order, sum of n_kmers entries).  Returns once
+ * the host inputs have been consumed (packed into the context's staging
+ * block); the device work is asynchronous on `hip_stream`.  Consecutive
+ * submits on one context must use the same stream.  Single-device contexts.
+ */
+ac_status ac_error_count_jobs_submit(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint32_t n_jobs,
+                                     uint32_t* d_counts, void* hip_stream);
+
+/*
+ * Device-side error check.  The count kernels never read outside a window's
+ * image: a window that is misaligned or reaches past n_bases is skipped, and
+ * the kernel records that in a context-owned device word instead of failing
+ * silently.  The host-buffer entry points check the word themselves (they
+ * synchronise); after the asynchronous *_device entry points call ac_check:
+ * it waits for `hip_stream`, reads and clears the word, and returns
+ * AC_ERR_INVALID ("malformed window skipped") or AC_ERR_INTERNAL (kernel
+ * set-up fault) if a launch since the last check hit one, AC_OK otherwise.
+ */
+ac_status ac_check(ac_ctx* ctx, void* hip_stream);
 
 /*
  * Launch geometry actually used for the last device launch of ctx (for

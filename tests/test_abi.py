@@ -27,7 +27,7 @@ def test_library_targets_gfx950():
 
 
 def test_abi_version():
-    assert _lib.load().ac_abi_version() == 1
+    assert _lib.load().ac_abi_version() == 2
 
 
 def test_pack_layout():
@@ -85,3 +85,23 @@ def test_image_too_small_rejected():
                            nmask.ctypes.data_as(_lib.p32), np.zeros(1, np.uint64).ctypes.data_as(_lib.p64),
                            np.zeros(1, np.uint32).ctypes.data_as(_lib.p32), ctypes.c_uint64(32))
     assert st == _lib.AC_ERR_INVALID
+
+
+def test_pack_matches_reference_packing_random():
+    """ac_pack_windows (the AVX2 packer shared with the jobs stage) against a
+    plain numpy packing: random lengths 0..200, ordinals 0..255 (> 3 = N)."""
+    rng = np.random.default_rng(3)
+    wins = [rng.choice(np.array([0, 1, 2, 3, 0, 1, 2, 3, 4, 5, 200], np.uint8), size=int(n))
+            for n in rng.integers(0, 200, size=300)]
+    s = ac.pack_windows(wins)
+    exp_codes = np.zeros_like(s.codes)
+    exp_nmask = np.zeros_like(s.nmask)
+    pos = 0
+    for w in wins:
+        b = pos + np.arange(w.size)
+        isn = w > 3
+        np.bitwise_or.at(exp_nmask, b[isn] // 32, (np.uint32(1) << (b[isn] % 32).astype(np.uint32)))
+        np.bitwise_or.at(exp_codes, b // 16, ((w & 3).astype(np.uint32) << (2 * (b % 16)).astype(np.uint32)))
+        pos += (w.size + 31) // 32 * 32
+    assert np.array_equal(s.nmask, exp_nmask)
+    assert np.array_equal(s.codes, exp_codes)

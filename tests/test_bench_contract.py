@@ -20,7 +20,7 @@ def test_default_workload_is_cfg2(monkeypatch):
     monkeypatch.setattr(sys, "argv", ["bench.py"])
     a = bench.parse()
     assert (a.gpus, a.k, a.sn, a.sl, a.lim) == (1, 16, 10_000, 100, 500)
-    assert a.inflight == 1  # the headline value keeps one batch in flight
+    assert a.scaling == "weak"  # every rank its own sn reads (per-GPU work fixed)
     assert a.steps > 0 and a.warmup >= 0
 
 
@@ -29,3 +29,15 @@ def test_config_overrides(monkeypatch):
     a = bench.parse()
     assert (a.k, a.sn, a.sl, a.lim, a.steps, a.warmup) == (22, 100_000, 150, 1000, 3, 1)
     assert a.read_len >= 2 * a.sl  # every read long enough for both ends
+
+
+def test_cfg4_is_strong_scaling(monkeypatch):
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--config", "cfg4"])
+    a = bench.parse()
+    assert (a.k, a.sn, a.sl, a.lim, a.scaling) == (16, 1_000_000, 100, 500, "strong")
+
+
+def test_cpu_share_reports_nproc():
+    n, quota = bench.cpu_share()
+    assert n == len(os.sched_getaffinity(0))
+    assert quota is None or quota > 0

@@ -2,16 +2,14 @@
 
 cfg3 (k=16, 100k reads, lim=2000) and cfg5 (k=22, sl=150, lim=1000): bit-exact
 against the oracle over every candidate, both ends fused in one launch.
-cfg4 (k=16, 1M windows per end, lim=500): size-independent properties -- the
-whole launch equals the sum of 8 window shards accumulated on the device (the
-multi-GPU identity), and a random subset of candidates equals the oracle."""
+cfg4 (k=16, 1M windows per end, lim=500): bit-exact against the oracle over
+every candidate and window, plus the shard-accumulation identity."""
 import numpy as np
 import pytest
 
 import approx_counter_amd as ac
 import oracle
 from tools import workload
-from tools.synth import make_windows_fast
 
 pytestmark = pytest.mark.gpu
 THREADS = 16
@@ -37,19 +35,22 @@ def test_full_config_bit_exact(counter, cfg):
         assert np.array_equal(g, oracle.count_myers(cfg["k"], km, w, THREADS))
 
 
-def test_cfg4_shards_and_sampled_candidates(counter):
+def test_cfg4_full_parity_and_shards(counter):
+    """cfg4 (k=16, 1M windows per end, 500 candidates): the product stage
+    (ac_error_count_jobs, both ends fused) against the oracle over EVERY candidate
+    and window (1.005e11 kmer*bp, ~25 s on 16 threads), and 8 window shards
+    accumulated on the device equal to the whole (the multi-GPU identity)."""
     import torch
 
     k, n = 16, 1_000_000
-    ends = [make_windows_fast(n, 100, seed=11)[0], make_windows_fast(n, 101, seed=12, at_end=True)[0]]
-    parts = []
-    for w in ends:
-        cand = workload.exact_topk([r for r in w[:20_000]], k, 500)
-        parts.append((np.array([c for c, _ in cand], np.uint64), w))
-    whole = fused_counts(counter, k, parts)
-    rng = np.random.default_rng(0)
-    for (km, w), g in zip(parts, whole):
-        # 8 window shards accumulated into one vector == one launch
+    wl = workload.build_fast(n_reads=n, k=k, sl=100, lim=500, seed=11)
+    parts = [(wl[e]["kmers"], wl[e]["windows"]) for e in ("start", "end")]
+    assert all(km.size == 500 for km, _ in parts)
+    got = counter.count_jobs(k, [(km, ac.Dna5Sample.from_windows(w)) for km, w in parts])
+    for (km, w), g in zip(parts, got):
+        assert np.array_equal(g, oracle.count_myers(k, km, w, THREADS))
+        assert g.max() > n  # adapter k-mers occur in most windows
+    for (km, w), g in zip(parts, got):
         bounds = np.linspace(0, n, 9).astype(int)
         acc = ac.DeviceSegment.upload(km, ac.pack_windows(w[bounds[0]:bounds[1]]))
         counter.count_device(k, [acc])
@@ -59,7 +60,3 @@ def test_cfg4_shards_and_sampled_candidates(counter):
             counter.count_device(k, [s], accumulate=True)
         torch.cuda.synchronize()
         assert np.array_equal(acc.counts_numpy(), g)
-        # oracle on a sample of candidates over all 1M windows
-        pick = np.unique(np.concatenate([np.arange(8), rng.choice(km.size, 16, replace=False)]))
-        assert np.array_equal(g[pick], oracle.count_myers(k, km[pick], w, THREADS))
-        assert g.max() > n  # adapter k-mers occur in most windows

@@ -1,0 +1,42 @@
+#!/usr/bin/env python3
+"""Device-resident count-kernel launches of one BASELINE configuration, for
+rocprofv3 PMC passes and kernel traces that must see only the kernel (the
+bench's stage reads its inputs from pinned host memory, which changes the
+memory counters).  Same workload and launch as bench.py's kernel leg.
+
+    rocprofv3 --pmc SQ_INSTS_VALU -d gpurun_out/pmc_valu -o run -- \
+        python3 tools/kernel_run.py --config cfg2 --launches 20
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="cfg2")
+    ap.add_argument("--launches", type=int, default=20)
+    a = ap.parse_args()
+    import torch
+
+    import approx_counter_amd as ac
+    import bench
+
+    sys.argv = ["bench.py", "--config", a.config]
+    args = bench.parse()
+    wl, _ = bench.build_workload(args, 0, 1)
+    segs = [ac.DeviceSegment.upload(wl[e]["kmers"], ac.pack_windows(wl[e]["windows"])) for e in ("start", "end")]
+    arr = ac.ApproxCounter.segment_array(segs)
+    with ac.ApproxCounter(0) as c:
+        for _ in range(a.launches):
+            c.count_device(args.k, arr)
+        torch.cuda.synchronize()
+        c.check()
+        print(f"{a.launches} launches of {a.config}; geometry {c.last_launch()}")
+
+
+if __name__ == "__main__":
+    main()

@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--fetch", required=True)
     ap.add_argument("--write", required=True)
     ap.add_argument("--workload", required=True)
+    ap.add_argument("--valu", help="directory of a SQ_INSTS_VALU pass (optional)")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     fetch, nf = mean_counter(a.fetch, "FETCH_SIZE")
@@ -50,6 +51,10 @@ def main():
          "dispatches": [nf, nw], "hbm_bytes_per_launch": (2.0 * fetch + write) * 1024.0,
          "correction": "2 x FETCH_SIZE (gfx950 half-count, MI355X_MICROARCH.md HBM) + WRITE_SIZE, KB -> B",
          "source": os.path.basename(a.out)}
+    if a.valu:  # wave-level VALU instructions per launch (bench.py compares them with the 9.5/P model)
+        valu, nv = mean_counter(a.valu, "SQ_INSTS_VALU")
+        d["sq_insts_valu_per_launch"] = valu
+        d["dispatches"].append(nv)
     with open(a.out, "w") as fh:
         json.dump(d, fh, indent=1)
     print(json.dumps(d))
