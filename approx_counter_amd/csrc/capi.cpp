@@ -663,7 +663,9 @@ ac_status ac_exact_count_device(ac_ctx* ctx, uint32_t k, const ac_windows* dev, 
     AC_HIP(ctx, hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
     // Table: a power of two >= 1.5 x the image size (an upper bound on k-mer
-    // positions): load <= 2/3 even when every position is a new k-mer.
+    // positions): load <= 2/3 even when every position is a new k-mer.  (1.25 x,
+    // 2^24 slots at 10^5 windows: insert 530 -> 644 us from the longer probe
+    // chains, scan 139 -> 104 us; profiles/r02_exact_log.md.)
     uint64_t slots = 1024;
     while (slots < dev->n_bases + dev->n_bases / 2) slots <<= 1;
     // Kept entries seen >= EXACT_LIST_MIN (2) times: at most n_bases / 2 (+ the all-T 32-mer).

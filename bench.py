@@ -127,34 +127,42 @@ def cpu_baseline(wl, k, seconds):
     ends = ("start", "end")
     bases = {e: sum(int(w.size) for w in wl[e]["windows"]) for e in ends}
 
-    def leg(threads, frac_cands, budget):
-        sub = {e: wl[e]["kmers"][: max(1, int(round(wl[e]["kmers"].size * frac_cands)))] for e in ends}
-        units = sum(sub[e].size * bases[e] for e in ends)
+    def run(threads, frac):
+        sub = {e: wl[e]["kmers"][: max(1, int(round(wl[e]["kmers"].size * frac)))] for e in ends}
         t = time.perf_counter()
         for e in ends:
             oracle.count_myers(k, sub[e], wl[e]["windows"], threads)
-        dt1 = max(time.perf_counter() - t, 1e-6)
-        reps = max(1, int(budget / dt1))
+        return sum(sub[e].size * bases[e] for e in ends), time.perf_counter() - t
+
+    def leg(threads, frac_cands, budget):
+        # a probe on a few candidates sizes the sample: the full workload repeated when one
+        # pass fits the budget, else the largest candidate fraction that does (cfg3-cfg5)
+        u0, t0 = run(threads, min(frac_cands, 0.02))
+        rate0 = u0 / max(t0, 1e-6)
+        full = sum(wl[e]["kmers"].size * bases[e] for e in ends) * frac_cands
+        frac = frac_cands if full / rate0 <= budget else max(0.002, frac_cands * budget / (full / rate0))
+        units, dt1 = run(threads, frac)
+        reps = max(1, int(budget / max(dt1, 1e-6)))
         t = time.perf_counter()
         for _ in range(reps):
-            for e in ends:
-                oracle.count_myers(k, sub[e], wl[e]["windows"], threads)
+            run(threads, frac)
         dt = time.perf_counter() - t
         return units * reps / dt, units, reps, dt
 
     v, units, reps, dt = leg(nproc, 1.0, seconds * 0.5)
     out = {"value": v, "unit": "kmer*bp/s", "cores": nproc, "kind": "port",
-           "sample": f"the full workload (both ends, {units:.4g} kmer*bp) x {reps} = {dt:.1f} s on {nproc} OpenMP "
+           "sample": f"both ends, {units:.4g} kmer*bp per pass (all windows; all candidates when a pass fits "
+                     f"the budget, else a prefix of them) x {reps} = {dt:.1f} s on {nproc} OpenMP "
                      f"threads (nproc; cgroup CPU quota {quota if quota else 'none'}); oracle/ac_oracle.c Myers "
                      f"bit-vector, OpenMP over candidates (restated CPU path: SeqAn is absent, SURVEY.md 8(c))"}
     if quota and int(quota) < nproc:
         q = max(1, int(quota))
         vq, units, reps, dt = leg(q, 1.0, seconds * 0.25)
         out["quota_threads"] = {"value": vq, "threads": q,
-                                "sample": f"full workload x {reps} = {dt:.1f} s on {q} threads (the cgroup quota)"}
+                                "sample": f"{units:.4g} kmer*bp x {reps} = {dt:.1f} s on {q} threads (the cgroup quota)"}
     v1, units, reps, dt = leg(1, 0.05, seconds * 0.25)
     out["one_thread"] = {"value": v1, "threads": 1,
-                         "sample": f"5% of the candidates of both ends over all windows ({units:.4g} kmer*bp) x {reps} "
+                         "sample": f"a prefix (<= 5%) of the candidates of both ends over all windows ({units:.4g} kmer*bp) x {reps} "
                                    f"= {dt:.1f} s"}
     return out
 
