@@ -47,8 +47,9 @@ struct ac_ctx {
     // working set (table keys, table counts, small scalars + histogram, forbidden, gather out)
     void* s_buf[4] = {nullptr, nullptr, nullptr, nullptr};
     size_t s_cap[4] = {0, 0, 0, 0};
-    void* e_buf[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
-    size_t e_cap[6] = {0, 0, 0, 0, 0, 0};
+    // (+ the partitioned path's keys, parts, chist, gsum, bstart, phist: e_buf[6..11])
+    void* e_buf[12] = {};
+    size_t e_cap[12] = {};
     // Count-kernel scratch, one set per stream a launch may run on at the same
     // time as another (the parts of a jobs call, AC_STAGE_MAX_PARTS).
     struct Scratch {
@@ -662,31 +663,32 @@ ac_status ac_exact_count_device(ac_ctx* ctx, uint32_t k, const ac_windows* dev, 
         return fail(ctx, AC_ERR_INVALID, "NULL output or forbidden array");
     AC_HIP(ctx, hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
-    // Table: a power of two >= 1.5 x the image size (an upper bound on k-mer
-    // positions): load <= 2/3 even when every position is a new k-mer.  (1.25 x,
-    // 2^24 slots at 10^5 windows: insert 530 -> 644 us from the longer probe
-    // chains, scan 139 -> 104 us; profiles/r02_exact_log.md.)
-    uint64_t slots = 1024;
-    while (slots < dev->n_bases + dev->n_bases / 2) slots <<= 1;
-    // Kept entries seen >= EXACT_LIST_MIN (2) times: at most n_bases / 2 (+ the all-T 32-mer).
-    const uint64_t list_cap = dev->n_bases / 2 + 2;
+    // k <= 16 takes the partitioned path (exact_count.hip: dense keys, bucket
+    // partition, per-bucket LDS count; no global table); k > 16, or a bucket
+    // that outgrows its LDS table, the hash-table path.  AC_EXACT_HASH=1
+    // forces the hash table (A/B).
+    const bool compact = k <= acamd::EXACT_COMPACT_MAX_K;
+    static const bool force_hash = std::getenv("AC_EXACT_HASH") != nullptr;
+    bool partitioned = compact && !force_hash;
+    // k-mer positions <= image bases: the capacity of the dense key arrays,
+    // and of the list when every kept entry must be listed (threshold 1).
+    const uint64_t key_cap = std::max<uint64_t>(32, dev->n_bases);
+    // Up to 8,192 buckets of <= ~2,048 keys (the per-bucket LDS table holds
+    // 4,096; the histogram / scatter kernels keep one LDS cursor per bucket):
+    // larger samples take the hash table.
+    if (key_cap > (uint64_t(8192) << 11)) partitioned = false;
+    const uint64_t list_cap = partitioned ? key_cap + 2 : dev->n_bases / 2 + 2;
     // small block: special[0..1] u32, had_n u64 @16, n_out u64 @24, n_list u64 @32, err u32 @40,
-    // hist[EXACT_HIST_BINS] u32 @64
+    // overflow u32 @44, n_keys u64 @48, hist[EXACT_HIST_BINS] u32 @64
     const size_t small_bytes = 64 + sizeof(uint32_t) * EXACT_HIST_BINS;
     std::vector<uint64_t> fb(forbidden, forbidden + n_forbidden);
     std::sort(fb.begin(), fb.end());
     fb.erase(std::unique(fb.begin(), fb.end()), fb.end());
-    // k <= 16: compact 8-byte slots (key and count in one word, exact_count.h)
-    const bool compact = k <= acamd::EXACT_COMPACT_MAX_K;
-    const size_t slot_bytes = compact ? sizeof(unsigned long long) : sizeof(acamd::ExactSlot);
-    if (ac_status s2 = grow(ctx, &ctx->e_buf[0], &ctx->e_cap[0], slot_bytes * slots)) return s2;
     if (ac_status s2 = grow(ctx, &ctx->e_buf[1], &ctx->e_cap[1], (sizeof(uint64_t) + sizeof(uint32_t)) * list_cap))
         return s2;
     if (ac_status s2 = grow(ctx, &ctx->e_buf[2], &ctx->e_cap[2], small_bytes)) return s2;
     if (ac_status s2 = grow(ctx, &ctx->e_buf[3], &ctx->e_cap[3], sizeof(uint64_t) * std::max<size_t>(1, fb.size())))
         return s2;
-    AC_HIP(ctx, hipMemsetAsync(ctx->e_buf[0], 0, slot_bytes * slots, st));
-    AC_HIP(ctx, hipMemsetAsync(ctx->e_buf[2], 0, small_bytes, st));
     if (!fb.empty())
         AC_HIP(ctx, hipMemcpyAsync(ctx->e_buf[3], fb.data(), sizeof(uint64_t) * fb.size(), hipMemcpyHostToDevice, st));
     char* small = (char*)ctx->e_buf[2];
@@ -699,16 +701,14 @@ ac_status ac_exact_count_device(ac_ctx* ctx, uint32_t k, const ac_windows* dev, 
     a.n_bases = dev->n_bases;
     a.n_windows = dev->n_windows;
     a.k = k;
-    a.table = (acamd::ExactSlot*)ctx->e_buf[0];
-    a.ctable = (unsigned long long*)ctx->e_buf[0];
     a.compact = compact ? 1u : 0u;
-    a.slots = slots;
-    a.mask = slots - 1;
     a.special = (uint32_t*)small;
     a.had_n = (unsigned long long*)(small + 16);
     a.n_out = (unsigned long long*)(small + 24);
     a.n_list = (unsigned long long*)(small + 32);
     a.err = (uint32_t*)(small + 40);
+    a.overflow = (uint32_t*)(small + 44);
+    a.n_keys = (unsigned long long*)(small + 48);
     a.hist = (uint32_t*)(small + 64);
     a.list_keys = (uint64_t*)ctx->e_buf[1];
     a.list_cnts = (uint32_t*)((char*)ctx->e_buf[1] + sizeof(uint64_t) * list_cap);
@@ -716,18 +716,62 @@ ac_status ac_exact_count_device(ac_ctx* ctx, uint32_t k, const ac_windows* dev, 
     a.lc_threshold = lc_threshold;
     a.forbidden = (const uint64_t*)ctx->e_buf[3];
     a.n_forbidden = (uint32_t)fb.size();
-    AC_HIP(ctx, acamd::launch_exact_insert(a, st));
-    AC_HIP(ctx, acamd::launch_exact_scan(a, st));
+    a.list_min = EXACT_LIST_MIN;
     std::vector<char> h_small(small_bytes);
-    AC_HIP(ctx, hipMemcpyAsync(h_small.data(), small, small_bytes, hipMemcpyDeviceToHost, st));
-    AC_HIP(ctx, hipStreamSynchronize(st));
+    if (partitioned) {
+        // buckets: about 1,024-2,048 keys each (the LDS table holds 4,096)
+        uint32_t nb_log2 = 6;
+        while (nb_log2 < 13 && (key_cap >> nb_log2) > 2048) ++nb_log2;
+        a.nb_log2 = nb_log2;
+        a.key_cap = key_cap;
+        a.n_chunks = (uint32_t)((key_cap + EXACT_CHUNK - 1) / EXACT_CHUNK);
+        a.n_groups = (a.n_chunks + EXACT_GROUP - 1) / EXACT_GROUP;
+        const size_t NB = size_t(1) << nb_log2;
+        if (ac_status s2 = grow(ctx, &ctx->e_buf[6], &ctx->e_cap[6], sizeof(uint32_t) * key_cap)) return s2;
+        if (ac_status s2 = grow(ctx, &ctx->e_buf[7], &ctx->e_cap[7], sizeof(uint32_t) * key_cap)) return s2;
+        if (ac_status s2 = grow(ctx, &ctx->e_buf[8], &ctx->e_cap[8], sizeof(uint32_t) * NB * a.n_chunks)) return s2;
+        if (ac_status s2 = grow(ctx, &ctx->e_buf[9], &ctx->e_cap[9], sizeof(uint32_t) * NB * a.n_groups)) return s2;
+        if (ac_status s2 = grow(ctx, &ctx->e_buf[10], &ctx->e_cap[10], sizeof(uint32_t) * (NB + 1))) return s2;
+        if (ac_status s2 = grow(ctx, &ctx->e_buf[11], &ctx->e_cap[11], sizeof(uint32_t) * NB * EXACT_PHIST)) return s2;
+        a.phist = (uint32_t*)ctx->e_buf[11];
+        a.keys = (uint32_t*)ctx->e_buf[6];
+        a.parts = (uint32_t*)ctx->e_buf[7];
+        a.chist = (uint32_t*)ctx->e_buf[8];
+        a.gsum = (uint32_t*)ctx->e_buf[9];
+        a.bstart = (uint32_t*)ctx->e_buf[10];
+        AC_HIP(ctx, hipMemsetAsync(small, 0, small_bytes, st));
+        AC_HIP(ctx, acamd::launch_exact_partitioned(a, st));
+        AC_HIP(ctx, hipMemcpyAsync(h_small.data(), small, small_bytes, hipMemcpyDeviceToHost, st));
+        AC_HIP(ctx, hipStreamSynchronize(st));
+        if (*(const uint32_t*)(h_small.data() + 44)) partitioned = false;  // a bucket overflowed its LDS table
+    }
+    if (!partitioned) {
+        // Table: a power of two >= 1.5 x the image size (an upper bound on k-mer
+        // positions): load <= 2/3 even when every position is a new k-mer.  (1.25 x,
+        // 2^24 slots at 10^5 windows: insert 530 -> 644 us from the longer probe
+        // chains, scan 139 -> 104 us; profiles/r02_exact_log.md.)
+        uint64_t slots = 1024;
+        while (slots < dev->n_bases + dev->n_bases / 2) slots <<= 1;
+        const size_t slot_bytes = compact ? sizeof(unsigned long long) : sizeof(acamd::ExactSlot);
+        if (ac_status s2 = grow(ctx, &ctx->e_buf[0], &ctx->e_cap[0], slot_bytes * slots)) return s2;
+        a.table = (acamd::ExactSlot*)ctx->e_buf[0];
+        a.ctable = (unsigned long long*)ctx->e_buf[0];
+        a.slots = slots;
+        a.mask = slots - 1;
+        AC_HIP(ctx, hipMemsetAsync(ctx->e_buf[0], 0, slot_bytes * slots, st));
+        AC_HIP(ctx, hipMemsetAsync(small, 0, small_bytes, st));
+        AC_HIP(ctx, acamd::launch_exact_insert(a, st));
+        AC_HIP(ctx, acamd::launch_exact_scan(a, st));
+        AC_HIP(ctx, hipMemcpyAsync(h_small.data(), small, small_bytes, hipMemcpyDeviceToHost, st));
+        AC_HIP(ctx, hipStreamSynchronize(st));
+    }
     if (ac_status rc = device_error(ctx, *(const uint32_t*)(h_small.data() + 40))) return rc;
     const uint32_t* hist = (const uint32_t*)(h_small.data() + 64);
     uint64_t kept = 0;
     for (int i = 0; i < EXACT_HIST_BINS; ++i) kept += hist[i];
     if (n_distinct) *n_distinct = kept;
     if (had_n) *had_n = *(const unsigned long long*)(h_small.data() + 16);
-    const uint64_t n_list = *(const unsigned long long*)(h_small.data() + 32);
+    uint64_t n_list = *(const unsigned long long*)(h_small.data() + 32);
     if (n_list > list_cap) return fail(ctx, AC_ERR_INTERNAL, "exact count: candidate list overflow");
     // Threshold: solid mode keeps count >= solid; otherwise the largest count c
     // such that at least `limit` kept entries have count >= c (all if fewer).
@@ -747,6 +791,20 @@ ac_status ac_exact_count_device(ac_ctx* ctx, uint32_t k, const ac_windows* dev, 
             }
         }
     }
+    bool from_list = thr >= EXACT_LIST_MIN;
+    if (!from_list && partitioned) {
+        // threshold 1: list every kept entry (the count kernel again, listing only)
+        a.list_min = 1;
+        a.emit_only = 1;
+        AC_HIP(ctx, hipMemsetAsync(a.n_list, 0, sizeof(unsigned long long), st));
+        AC_HIP(ctx, acamd::launch_exact_part_count(a, st));
+        unsigned long long nl = 0;
+        AC_HIP(ctx, hipMemcpyAsync(&nl, a.n_list, sizeof nl, hipMemcpyDeviceToHost, st));
+        AC_HIP(ctx, hipStreamSynchronize(st));
+        n_list = nl;
+        if (n_list > list_cap) return fail(ctx, AC_ERR_INTERNAL, "exact count: candidate list overflow");
+        from_list = true;
+    }
     // (a solid threshold past the last bin is applied exactly on the gathered list)
     const uint64_t gather_cap = std::max<uint64_t>(1, due);
     if (ac_status s2 = grow(ctx, &ctx->e_buf[4], &ctx->e_cap[4], sizeof(uint64_t) * gather_cap)) return s2;
@@ -755,7 +813,7 @@ ac_status ac_exact_count_device(ac_ctx* ctx, uint32_t k, const ac_windows* dev, 
     a.out_keys = (uint64_t*)ctx->e_buf[4];
     a.out_cnts = (uint32_t*)ctx->e_buf[5];
     a.out_cap = gather_cap;
-    AC_HIP(ctx, acamd::launch_exact_gather(a, thr >= EXACT_LIST_MIN, n_list, st));
+    AC_HIP(ctx, acamd::launch_exact_gather(a, from_list, n_list, st));
     unsigned long long got = 0;
     AC_HIP(ctx, hipMemcpyAsync(&got, a.n_out, sizeof got, hipMemcpyDeviceToHost, st));
     AC_HIP(ctx, hipStreamSynchronize(st));

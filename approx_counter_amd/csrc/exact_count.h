@@ -65,11 +65,42 @@ struct ExactArgs {
     uint32_t* out_cnts;
     unsigned long long* n_out;
     uint64_t out_cap;
+    // Partitioned path (k <= 16): every k-mer position's key
+    // written densely (`keys`, n_keys of them), a per-chunk histogram of their
+    // bucket (hash high bits) in `chist` ([chunk][bucket], turned into each
+    // chunk's offset within its bucket), bucket starts in `bstart` (nb + 1),
+    // the keys scattered bucket by bucket into `parts`, then one workgroup per
+    // bucket counts its keys in LDS.  No global hash table.
+    uint32_t* keys;
+    uint32_t* parts;
+    unsigned long long* n_keys;
+    uint32_t* chist;
+    uint32_t* gsum;    // [group][bucket] partial column sums of chist
+    uint32_t* bstart;  // nb + 1
+    uint32_t nb_log2;
+    uint32_t n_chunks;  // launch bound: ceil(key capacity / EXACT_CHUNK)
+    uint32_t n_groups;  // ceil(n_chunks / EXACT_GROUP)
+    uint64_t key_cap;
+    uint32_t list_min;   // the count kernel lists kept entries with count >= list_min
+    uint32_t emit_only;  // 1: list only (the histogram and distinct count were taken by an earlier pass)
+    uint32_t* overflow;  // set when a bucket outgrows the count kernel's LDS table
+    uint32_t* phist;     // [bucket][EXACT_PHIST] partial histograms of the count kernel (counts 1..EXACT_PHIST)
 };
+
+#define EXACT_PHIST 32  // per-bucket partial histogram bins (counts 1..32; larger counts go straight to hist)
+
+#define EXACT_CHUNK 16384  // dense keys per histogram / scatter workgroup
+#define EXACT_GROUP 32     // chunks per partial column sum
+#define EXACT_BUCKET_SLOTS 4096  // LDS counting table of the per-bucket kernel (32 KB of keys + counts)
 
 hipError_t launch_exact_insert(const ExactArgs& a, hipStream_t stream);
 hipError_t launch_exact_scan(const ExactArgs& a, hipStream_t stream);
 // from_list: gather from the scan's compacted list of n_list entries, else from the table
 hipError_t launch_exact_gather(const ExactArgs& a, bool from_list, uint64_t n_list, hipStream_t stream);
+// Partitioned path (k <= 16): keys, bucket partition, per-bucket count (fills
+// hist / list / special like insert + scan).  `count_only` re-runs just the
+// per-bucket count (with a.list_min / a.emit_only) on the partition already built.
+hipError_t launch_exact_partitioned(const ExactArgs& a, hipStream_t stream);
+hipError_t launch_exact_part_count(const ExactArgs& a, hipStream_t stream);
 
 }  // namespace acamd

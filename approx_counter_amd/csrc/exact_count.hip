@@ -426,7 +426,407 @@ __global__ __launch_bounds__(EXACT_THREADS) void exact_gather_list_kernel(ExactA
     app.sync_flush(true);
 }
 
+// ---------------------------------------------------------------------------
+// Partitioned path (k <= 16).  The hash-table insert above is bound by its
+// random read-modify-write atomics in HBM (~7.5M at 10^5 windows, ~380 us of
+// a 540 us insert; profiles/r02_exact_log.md).  Here every step streams:
+//   keys     each window block writes its k-mer keys densely (one reservation
+//            per 1,024 positions), no aggregation
+//   hist     per chunk of EXACT_CHUNK keys, the count of keys per bucket
+//            (bucket = high bits of the key's hash)
+//   colscan  chunk offsets inside each bucket, bucket starts
+//   scatter  keys to their bucket's range (LDS cursors per bucket)
+//   count    one workgroup per bucket counts its keys in an LDS table and
+//            runs the low-complexity / forbidden filters, the histogram and
+//            the list of the scan kernel above
+// Keys are only grouped, never ordered, so nothing has to be stable.
+
+constexpr uint32_t MAX_NB_LOG2 = 13;
+constexpr uint32_t COUNT_PROBES = 64;
+
+__device__ __forceinline__ uint32_t bucket_of(uint32_t key, uint32_t nb_log2) {
+    return (uint32_t)(mix64(key) >> (64u - nb_log2));
+}
+
+// Keys of every k-mer position, written densely.  A thread takes SEG_POS
+// consecutive positions of one window: it gathers the first key's 2k bits and
+// N flags once and rolls the rest (one 2-bit code and one N flag per step),
+// instead of gathering every position's words anew.
+constexpr uint32_t SEG_POS = 16;
+
+__global__ __launch_bounds__(EXACT_THREADS) void part_keys_kernel(ExactArgs a) {
+    __shared__ uint32_t wseg[EXACT_WINDOWS_PER_BLOCK + 1];  // prefix sums of segments per window
+    __shared__ uint32_t wsum[EXACT_THREADS / 64];
+    __shared__ unsigned long long base_sh;
+    __shared__ uint32_t n_had;
+    const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+    const uint32_t w0 = blockIdx.x * EXACT_WINDOWS_PER_BLOCK;
+    const uint32_t nw = min((uint32_t)EXACT_WINDOWS_PER_BLOCK, a.n_windows - w0);
+    if (t == 0) {
+        uint32_t acc = 0;
+        for (uint32_t i = 0; i < nw; ++i) {
+            wseg[i] = acc;
+            const uint64_t st = a.start[w0 + i];
+            const uint32_t len = a.length[w0 + i];
+            const bool ok = !(st & 31u) && len <= a.n_bases && st <= a.n_bases - len;
+            if (!ok) atomicOr(a.err, AC_DEVERR_WINDOW);
+            const uint32_t npos = (ok && len >= a.k) ? len - a.k + 1u : 0u;
+            acc += (npos + SEG_POS - 1u) / SEG_POS;
+        }
+        wseg[nw] = acc;
+        n_had = 0;
+    }
+    __syncthreads();
+    const uint32_t total = wseg[nw];
+    const uint32_t k = a.k;
+    const uint64_t kmask = (1ull << k) - 1ull;
+    const uint32_t keymask = k == 16u ? 0xffffffffu : ((1u << (2u * k)) - 1u);
+    uint32_t had = 0;
+    for (uint32_t s0 = 0; s0 < total; s0 += EXACT_THREADS) {  // block-uniform rounds
+        const uint32_t sg = s0 + t;
+        uint32_t key[SEG_POS];
+        uint32_t valid = 0, c = 0;
+        if (sg < total) {
+            uint32_t i = 0;
+            while (wseg[i + 1] <= sg) ++i;
+            const uint64_t wst = a.start[w0 + i];
+            const uint32_t npos = a.length[w0 + i] - k + 1u;
+            const uint32_t p0 = (sg - wseg[i]) * SEG_POS;
+            const uint32_t np = min(SEG_POS, npos - p0);
+            const uint64_t b = wst + p0;
+            // the first position: gathered; N flags of bases b .. b + k + np - 2 (<= 47 bits)
+            uint32_t cur = (uint32_t)to_dna2int(gather_bits(a.codes, b, 2u, 2u * k, a.n_bases >> 4), k);
+            const uint64_t nbits = gather_bits(a.nmask, b, 1u, k + np - 1u, a.n_bases >> 5);
+            // codes of bases b + k .. b + k + np - 2 for the rolling steps (<= 15 bases: 30 bits)
+            const uint64_t nxt = np > 1u ? gather_bits(a.codes, b + k, 2u, 2u * (np - 1u), a.n_bases >> 4) : 0ull;
+#pragma unroll
+            for (uint32_t j = 0; j < SEG_POS; ++j) {
+                if (j < np) {
+                    if (j) cur = ((cur << 2) | (uint32_t)((nxt >> (2u * (j - 1u))) & 3u)) & keymask;
+                    if ((nbits >> j) & kmask) {
+                        ++had;  // count_kmers skips k-mers holding an N (approx_counter.cpp:498, 513-517)
+                    } else {
+                        key[j] = cur;
+                        valid |= 1u << j;
+                        ++c;
+                    }
+                }
+            }
+        }
+        uint32_t incl = c;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(incl, d, 64);
+            if ((int)lane >= d) incl += y;
+        }
+        if (lane == 63u) wsum[wv] = incl;
+        __syncthreads();
+        if (t == 0) {
+            uint32_t tot = 0;
+            for (uint32_t w = 0; w < EXACT_THREADS / 64; ++w) {
+                const uint32_t x = wsum[w];
+                wsum[w] = tot;
+                tot += x;
+            }
+            base_sh = tot ? atomicAdd(a.n_keys, (unsigned long long)tot) : 0ull;
+        }
+        __syncthreads();
+        uint64_t dst = base_sh + wsum[wv] + incl - c;
+#pragma unroll
+        for (uint32_t j = 0; j < SEG_POS; ++j)
+            if (valid & (1u << j)) {
+                if (dst < a.key_cap) a.keys[dst] = key[j];
+                ++dst;
+            }
+        __syncthreads();  // wsum / base_sh are reused by the next round
+    }
+    if (had) atomicAdd(&n_had, had);
+    __syncthreads();
+    if (t == 0 && n_had) atomicAdd(a.had_n, (unsigned long long)n_had);
+}
+
+__global__ __launch_bounds__(EXACT_THREADS) void part_hist_kernel(ExactArgs a) {
+    __shared__ uint32_t h[1u << MAX_NB_LOG2];
+    const uint32_t NB = 1u << a.nb_log2, t = threadIdx.x;
+    for (uint32_t i = t; i < NB; i += EXACT_THREADS) h[i] = 0;
+    __syncthreads();
+    const uint64_t n = min((unsigned long long)a.key_cap, *a.n_keys);
+    const uint64_t lo = (uint64_t)blockIdx.x * EXACT_CHUNK, hi = min(n, lo + EXACT_CHUNK);
+    for (uint64_t i = lo + t; i < hi; i += EXACT_THREADS) atomicAdd(&h[bucket_of(a.keys[i], a.nb_log2)], 1u);
+    __syncthreads();
+    uint32_t* row = a.chist + (uint64_t)blockIdx.x * NB;
+    for (uint32_t i = t; i < NB; i += EXACT_THREADS) row[i] = h[i];
+}
+
+// Column sums of EXACT_GROUP chunk rows: gsum[g][b].
+__global__ __launch_bounds__(EXACT_THREADS) void part_colsum_kernel(ExactArgs a) {
+    const uint32_t NB = 1u << a.nb_log2;
+    const uint32_t b = blockIdx.x * EXACT_THREADS + threadIdx.x, g = blockIdx.y;
+    if (b >= NB) return;
+    const uint32_t r1 = min(a.n_chunks, (g + 1) * EXACT_GROUP);
+    uint32_t sum = 0;
+    for (uint32_t r = g * EXACT_GROUP; r < r1; ++r) sum += a.chist[(uint64_t)r * NB + b];
+    a.gsum[(uint64_t)g * NB + b] = sum;
+}
+
+// Per bucket: exclusive prefix over the groups (in place) and the bucket total.
+__global__ __launch_bounds__(EXACT_THREADS) void part_groupscan_kernel(ExactArgs a) {
+    const uint32_t NB = 1u << a.nb_log2;
+    const uint32_t b = blockIdx.x * EXACT_THREADS + threadIdx.x;
+    if (b >= NB) return;
+    uint32_t run = 0;
+    for (uint32_t g = 0; g < a.n_groups; ++g) {
+        const uint32_t x = a.gsum[(uint64_t)g * NB + b];
+        a.gsum[(uint64_t)g * NB + b] = run;
+        run += x;
+    }
+    a.bstart[b] = run;
+}
+
+// Bucket totals -> exclusive starts (one workgroup of 1,024 threads, NB <= 8,192).
+__global__ __launch_bounds__(1024) void part_bucketscan_kernel(ExactArgs a) {
+    __shared__ uint32_t sums[1024];
+    const uint32_t NB = 1u << a.nb_log2, t = threadIdx.x;
+    const uint32_t per = (NB + 1023u) / 1024u, b0 = t * per;
+    uint32_t local = 0;
+    for (uint32_t b = b0; b < min(NB, b0 + per); ++b) local += a.bstart[b];
+    sums[t] = local;
+    __syncthreads();
+    for (uint32_t d = 1; d < 1024; d <<= 1) {  // Hillis-Steele inclusive scan
+        const uint32_t y = t >= d ? sums[t - d] : 0u;
+        __syncthreads();
+        sums[t] += y;
+        __syncthreads();
+    }
+    uint32_t run = sums[t] - local;
+    for (uint32_t b = b0; b < min(NB, b0 + per); ++b) {
+        const uint32_t x = a.bstart[b];
+        a.bstart[b] = run;
+        run += x;
+    }
+    if (t == 1023u) a.bstart[NB] = sums[1023];
+}
+
+// chist[r][b] <- global position of chunk r's first key of bucket b.
+__global__ __launch_bounds__(EXACT_THREADS) void part_offsets_kernel(ExactArgs a) {
+    const uint32_t NB = 1u << a.nb_log2;
+    const uint32_t b = blockIdx.x * EXACT_THREADS + threadIdx.x, g = blockIdx.y;
+    if (b >= NB) return;
+    uint32_t run = a.bstart[b] + a.gsum[(uint64_t)g * NB + b];
+    const uint32_t r1 = min(a.n_chunks, (g + 1) * EXACT_GROUP);
+    for (uint32_t r = g * EXACT_GROUP; r < r1; ++r) {
+        uint32_t* c = &a.chist[(uint64_t)r * NB + b];
+        const uint32_t x = *c;
+        *c = run;
+        run += x;
+    }
+}
+
+__global__ __launch_bounds__(EXACT_THREADS) void part_scatter_kernel(ExactArgs a) {
+    __shared__ uint32_t cur[1u << MAX_NB_LOG2];
+    const uint32_t NB = 1u << a.nb_log2, t = threadIdx.x;
+    const uint32_t* row = a.chist + (uint64_t)blockIdx.x * NB;
+    for (uint32_t i = t; i < NB; i += EXACT_THREADS) cur[i] = row[i];
+    __syncthreads();
+    const uint64_t n = min((unsigned long long)a.key_cap, *a.n_keys);
+    const uint64_t lo = (uint64_t)blockIdx.x * EXACT_CHUNK, hi = min(n, lo + EXACT_CHUNK);
+    for (uint64_t i = lo + t; i < hi; i += EXACT_THREADS) {
+        const uint32_t key = a.keys[i];
+        const uint32_t pos = atomicAdd(&cur[bucket_of(key, a.nb_log2)], 1u);
+        a.parts[pos] = key;
+    }
+}
+
+// One workgroup per bucket: count its keys in LDS, then filter, histogram and
+// list them like exact_scan_kernel (the all-T 16-mer, whose key + 1 wraps to
+// 0, is tallied in special[0] and handled by part_special_kernel).  LDS is
+// kept under 80 KB (two workgroups per CU): the table, a 32-bin histogram of
+// the counts 1..32 written out per bucket (phist, summed by
+// part_hist_reduce_kernel: thousands of buckets adding into the same few
+// global bins would serialise), larger counts straight to the global
+// histogram, and a small appender.  An adapter k-mer fills most of its
+// bucket with one key: a wave first merges the lanes holding its first lane's
+// key, so the LDS add on that slot is one per wave instead of one per lane.
+constexpr uint32_t COUNT_APPEND = 512;
+
+constexpr uint32_t COUNT_BATCH = 8;  // keys per thread loaded together (one memory latency per batch)
+
+__global__ __launch_bounds__(EXACT_THREADS) void part_count_kernel(ExactArgs a) {
+    constexpr uint32_t SLOTS = EXACT_BUCKET_SLOTS;
+    __shared__ uint32_t tk[SLOTS];  // key + 1; 0 = empty
+    __shared__ uint32_t tc[SLOTS];
+    __shared__ uint16_t occ[SLOTS];  // the slots claimed, in claim order: only they are scored and cleared
+    __shared__ uint32_t n_occ;
+    __shared__ uint32_t hist[EXACT_PHIST];  // counts 1 .. EXACT_PHIST
+    __shared__ uint64_t app_k[COUNT_APPEND];
+    __shared__ uint32_t app_c[COUNT_APPEND];
+    __shared__ uint32_t app_n;
+    __shared__ unsigned long long app_b;
+    __shared__ uint32_t n_allt;
+    const uint32_t t = threadIdx.x;
+    const uint32_t NB = 1u << a.nb_log2;
+    for (uint32_t i = t; i < SLOTS; i += EXACT_THREADS) {
+        tk[i] = 0;
+        tc[i] = 0;
+    }
+    if (t == 0) {
+        n_allt = 0;
+        app_n = 0;
+        n_occ = 0;
+    }
+    BlockAppender app{a.list_keys, a.list_cnts, a.n_list, a.list_cap, app_k, app_c, &app_n, &app_b};
+    // Persistent: workgroup g counts buckets g, g + grid, ...; between buckets
+    // only the claimed slots are cleared.
+    for (uint32_t b = blockIdx.x; b < NB; b += gridDim.x) {
+        for (uint32_t i = t; i < EXACT_PHIST; i += EXACT_THREADS) hist[i] = 0;
+        __syncthreads();
+        const uint32_t lo = a.bstart[b], hi = a.bstart[b + 1];
+        uint32_t allt = 0;
+        for (uint32_t i0 = lo; i0 < hi; i0 += EXACT_THREADS * COUNT_BATCH) {  // block-uniform batches
+            uint32_t kb[COUNT_BATCH];
+#pragma unroll
+            for (uint32_t r = 0; r < COUNT_BATCH; ++r) {
+                const uint32_t i = i0 + r * EXACT_THREADS + t;
+                kb[r] = i < hi ? a.parts[i] : 0u;
+            }
+#pragma unroll
+            for (uint32_t r = 0; r < COUNT_BATCH; ++r) {
+                const uint32_t i = i0 + r * EXACT_THREADS + t;
+                const bool have = i < hi;
+                const uint32_t key = kb[r], stored = key + 1u;
+                // lanes holding the wave's first key: one add of their number
+                const uint32_t k0 = __builtin_amdgcn_readfirstlane(key);
+                const uint64_t same = __ballot(have && key == k0);
+                uint32_t add = 1u;
+                bool go = have;
+                if (have && key == k0) {
+                    go = __lane_id() == (uint32_t)__builtin_ctzll(same);
+                    add = (uint32_t)__popcll(same);
+                }
+                if (go && !stored) {
+                    allt += add;
+                    go = false;
+                }
+                if (go) {
+                    uint32_t h = (uint32_t)mix64(key) & (SLOTS - 1u);
+                    uint32_t probe = 0;
+                    for (; probe < COUNT_PROBES; ++probe) {
+                        uint32_t cur = tk[h];
+                        if (cur == 0u) {
+                            cur = atomicCAS(&tk[h], 0u, stored);
+                            if (cur == 0u) {  // claimed: list the slot for scoring and clearing
+                                cur = stored;
+                                occ[atomicAdd(&n_occ, 1u)] = (uint16_t)h;
+                            }
+                        }
+                        if (cur == stored) {
+                            atomicAdd(&tc[h], add);
+                            break;
+                        }
+                        h = (h + 1u) & (SLOTS - 1u);
+                    }
+                    if (probe == COUNT_PROBES) atomicOr(a.overflow, 1u);  // the host falls back to the hash table
+                }
+            }
+        }
+        if (allt) atomicAdd(&n_allt, allt);
+        __syncthreads();
+        uint32_t ones = 0;
+        const uint32_t m = n_occ;
+        for (uint32_t s0 = 0; s0 < m; s0 += EXACT_THREADS) {  // block-uniform trips over the claimed slots
+            uint32_t c = 0;
+            uint64_t key = 0;
+            if (s0 + t < m) {
+                const uint32_t s = occ[s0 + t];
+                key = tk[s] - 1u;
+                c = tc[s];
+                tk[s] = 0;  // cleared for the next bucket
+                tc[s] = 0;
+                if (complexity(key, a.k) >= a.lc_threshold) c = 0;  // haveLowComplexity (214-234)
+                else if (is_forbidden(a, key)) c = 0;              // isForbiddenKmer (330-332)
+            }
+            if (!a.emit_only && c) {
+                if (c == 1u) ++ones;
+                else if (c <= EXACT_PHIST) atomicAdd(&hist[c - 1u], 1u);
+                else atomicAdd(&a.hist[min(c, (uint32_t)EXACT_HIST_BINS - 1u)], 1u);
+            }
+            app.push(c && c >= a.list_min, key, c);
+            // flush when the next trip's pushes might not fit (block-uniform test after a barrier)
+            __syncthreads();
+            if (app_n + EXACT_THREADS > COUNT_APPEND) app.sync_flush(true);
+        }
+        for (int off = 32; off; off >>= 1) ones += __shfl_xor(ones, off);
+        if (__lane_id() == 0 && ones) atomicAdd(&hist[0], ones);
+        __syncthreads();
+        if (!a.emit_only)
+            for (uint32_t i = t; i < EXACT_PHIST; i += EXACT_THREADS) a.phist[(uint64_t)b * EXACT_PHIST + i] = hist[i];
+        if (t == 0) n_occ = 0;
+        // (the next bucket's first barrier orders these against its inserts)
+    }
+    app.sync_flush(true);
+    if (t == 0 && n_allt && !a.emit_only) atomicAdd(&a.special[0], n_allt);
+}
+
+// hist[c] += sum over buckets of phist[bucket][c - 1], c = 1..EXACT_PHIST: one
+// workgroup per bin.
+__global__ __launch_bounds__(EXACT_THREADS) void part_hist_reduce_kernel(ExactArgs a) {
+    __shared__ uint32_t red[EXACT_THREADS / 64];
+    const uint32_t NB = 1u << a.nb_log2, bin = blockIdx.x, t = threadIdx.x;
+    uint32_t sum = 0;
+    for (uint32_t b = t; b < NB; b += EXACT_THREADS) sum += a.phist[(uint64_t)b * EXACT_PHIST + bin];
+    for (int off = 32; off; off >>= 1) sum += __shfl_xor(sum, off);
+    if ((t & 63u) == 0) red[t >> 6] = sum;
+    __syncthreads();
+    if (t == 0) {
+        uint32_t tot = 0;
+        for (uint32_t w = 0; w < EXACT_THREADS / 64; ++w) tot += red[w];
+        if (tot) atomicAdd(&a.hist[bin + 1u], tot);
+    }
+}
+
+// The all-T 16-mer (counted apart in special[0]): filters, histogram, list.
+__global__ void part_special_kernel(ExactArgs a) {
+    const uint32_t c = a.special[0];
+    if (!c) return;
+    const uint64_t key = 0xffffffffull;
+    if (complexity(key, a.k) >= a.lc_threshold || is_forbidden(a, key)) return;
+    if (!a.emit_only) atomicAdd(&a.hist[min(c, (uint32_t)EXACT_HIST_BINS - 1u)], 1u);
+    if (c >= a.list_min) {
+        const unsigned long long i = atomicAdd(a.n_list, 1ull);
+        if (i < a.list_cap) {
+            a.list_keys[i] = key;
+            a.list_cnts[i] = c;
+        }
+    }
+}
+
 }  // namespace
+
+hipError_t launch_exact_part_count(const ExactArgs& a, hipStream_t stream) {
+    // persistent workgroups: three per CU (LDS ~46 KB each)
+    const uint32_t grid = std::min<uint32_t>(1u << a.nb_log2, 256u * 3u);
+    hipLaunchKernelGGL(part_count_kernel, dim3(grid), dim3(EXACT_THREADS), 0, stream, a);
+    if (!a.emit_only)
+        hipLaunchKernelGGL(part_hist_reduce_kernel, dim3(EXACT_PHIST), dim3(EXACT_THREADS), 0, stream, a);
+    hipLaunchKernelGGL(part_special_kernel, dim3(1), dim3(1), 0, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_exact_partitioned(const ExactArgs& a, hipStream_t stream) {
+    if (a.nb_log2 < 6 || a.nb_log2 > MAX_NB_LOG2) return hipErrorInvalidValue;
+    const uint32_t NB = 1u << a.nb_log2;
+    const uint32_t wblocks = (a.n_windows + EXACT_WINDOWS_PER_BLOCK - 1) / EXACT_WINDOWS_PER_BLOCK;
+    if (wblocks) hipLaunchKernelGGL(part_keys_kernel, dim3(wblocks), dim3(EXACT_THREADS), 0, stream, a);
+    const dim3 cols((NB + EXACT_THREADS - 1) / EXACT_THREADS), cols_groups(cols.x, a.n_groups);
+    hipLaunchKernelGGL(part_hist_kernel, dim3(a.n_chunks), dim3(EXACT_THREADS), 0, stream, a);
+    hipLaunchKernelGGL(part_colsum_kernel, cols_groups, dim3(EXACT_THREADS), 0, stream, a);
+    hipLaunchKernelGGL(part_groupscan_kernel, cols, dim3(EXACT_THREADS), 0, stream, a);
+    hipLaunchKernelGGL(part_bucketscan_kernel, dim3(1), dim3(1024), 0, stream, a);
+    hipLaunchKernelGGL(part_offsets_kernel, cols_groups, dim3(EXACT_THREADS), 0, stream, a);
+    hipLaunchKernelGGL(part_scatter_kernel, dim3(a.n_chunks), dim3(EXACT_THREADS), 0, stream, a);
+    if (hipError_t e = hipGetLastError()) return e;
+    return launch_exact_part_count(a, stream);
+}
 
 hipError_t launch_exact_insert(const ExactArgs& a, hipStream_t stream) {
     const uint32_t blocks = (a.n_windows + EXACT_WINDOWS_PER_BLOCK - 1) / EXACT_WINDOWS_PER_BLOCK;
