@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cctype>
 #include <chrono>
 #include <cstdlib>
 #include <cstdio>
@@ -410,6 +411,14 @@ ac_status ac_create(ac_ctx** out, int device) {
         return st;
     }
     ctx->cu_count = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    {  // the host pool packs into memory this GPU reads: prefer the CPUs local to its PCIe root
+        char bus[64] = {0};
+        if (hipDeviceGetPCIBusId(bus, sizeof bus, device) == hipSuccess) {
+            for (char* c = bus; *c; ++c) *c = (char)std::tolower((unsigned char)*c);
+            const std::string path = std::string("/sys/bus/pci/devices/") + bus + "/local_cpulist";
+            acamd::set_host_cpus(acamd::read_cpulist(path.c_str()));
+        }
+    }
     if ((e = hipMalloc(&ctx->d_err, sizeof(uint32_t))) != hipSuccess ||
         (e = hipMemset(ctx->d_err, 0, sizeof(uint32_t))) != hipSuccess ||
         (e = hipHostMalloc(&ctx->h_err, sizeof(uint32_t), hipHostMallocDefault)) != hipSuccess) {
@@ -943,7 +952,13 @@ inline size_t align256(size_t x) { return (x + 255) / 256 * 256; }
 struct StageTrace {
     bool on = std::getenv("AC_STAGE_TRACE") != nullptr;
     double sum[8] = {};
+    double cur[8] = {};
     uint64_t calls = 0;
+    std::vector<std::vector<double>> per_call;  // AC_STAGE_TRACE=2: every call's phases
+    void end_call() {
+        if (std::getenv("AC_STAGE_TRACE")[0] == '2') per_call.emplace_back(cur, cur + 8);
+        for (double& x : cur) x = 0.0;
+    }
     void skip_warmup() {  // the first calls allocate: leave them out of the means
         if (calls == 5) {
             for (double& x : sum) x = 0.0;
@@ -956,6 +971,11 @@ struct StageTrace {
         std::fprintf(stderr, "[ac stage trace] %llu calls (first 5 left out), mean us:", (unsigned long long)calls);
         for (int i = 0; i < 8; ++i) std::fprintf(stderr, " %s %.1f", names[i], sum[i] / n);
         std::fprintf(stderr, "\n");
+        for (size_t c = 0; c < per_call.size(); ++c) {
+            std::fprintf(stderr, "[ac stage call %zu]", c);
+            for (int i = 0; i < 8; ++i) std::fprintf(stderr, " %s %.1f", names[i], per_call[c][i]);
+            std::fprintf(stderr, "\n");
+        }
     }
 };
 StageTrace g_trace;
@@ -1041,6 +1061,9 @@ ac_status check_jobs(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint32_t n_job
 // and launches the fused count kernel, whose counts go to d_counts (job j at
 // d_counts + sum of the earlier n_kmers) or, when NULL, to the slot's counts
 // area.  Records the slot's event after the launch.
+// Staging slots: a synchronous call's part q always uses slot q (the same
+// pinned pages every call: with the zero-copy stage the GPU's translations of
+// them stay cached); submits alternate between the last two slots.
 ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan& p, hipStream_t stream,
                            uint32_t* d_counts, int part = 0, uint32_t wave_div = 0) {
     using acamd::image_span;
@@ -1072,6 +1095,7 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
         if (!g_trace.on) return;
         const double t = now_us();
         g_trace.sum[i] += t - tt;
+        g_trace.cur[i] += t - tt;
         tt = t;
     };
     if (total_w <= (1u << 18)) {  // a serial pass is cheaper than a pool round trip up to ~256k windows
@@ -1110,8 +1134,12 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
     }
     p.total = off;
     // The slot: wait until the launch that last read it has finished, grow it.
-    p.slot = (int)ctx->next_slot;
-    ctx->next_slot = (ctx->next_slot + 1u) % (2u * AC_STAGE_MAX_PARTS);
+    if (d_counts) {
+        p.slot = AC_STAGE_MAX_PARTS + (int)ctx->next_slot;
+        ctx->next_slot ^= 1u;
+    } else {
+        p.slot = part;
+    }
     ac_ctx::Slot& sl = ctx->slot[p.slot];
     if (sl.pending) {
         AC_HIP(ctx, hipEventSynchronize(sl.ev));
@@ -1287,6 +1315,7 @@ ac_status ac_error_count_jobs(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint3
         if (g_trace.on && g + 1 == units.size()) {
             const double t = now_us();
             g_trace.sum[6] += t - t_sync;
+            g_trace.cur[6] += t - t_sync;
             t_sync = t;
         }
         ac_ctx::Slot& sl = u.c->slot[u.plan.slot];
@@ -1304,8 +1333,10 @@ ac_status ac_error_count_jobs(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint3
     }
     if (g_trace.on) {
         g_trace.sum[7] += now_us() - t_sync;
+        g_trace.cur[7] += now_us() - t_sync;
         ++g_trace.calls;
         g_trace.skip_warmup();
+        g_trace.end_call();
     }
     return first_err;
 }

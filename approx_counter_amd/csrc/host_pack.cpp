@@ -7,7 +7,10 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
+
+#include <pthread.h>
 
 namespace acamd {
 
@@ -22,10 +25,18 @@ int64_t now_ns() {
 
 }  // namespace
 
-WorkPool::WorkPool(unsigned n_threads) {
+WorkPool::WorkPool(unsigned n_threads, const std::vector<int>& cpus) {
     const char* s = std::getenv("AC_HOST_SPIN_US");
     spin_ns_ = (s ? std::atoll(s) : 2000) * 1000;  // 2 ms: consecutive calls find the workers spinning
-    for (unsigned i = 1; i < std::max(1u, n_threads); ++i) threads_.emplace_back([this] { worker(); });
+    for (unsigned i = 1; i < std::max(1u, n_threads); ++i) {
+        threads_.emplace_back([this] { worker(); });
+        if (!cpus.empty()) {
+            cpu_set_t set;
+            CPU_ZERO(&set);
+            CPU_SET(cpus[(i - 1) % cpus.size()], &set);
+            (void)pthread_setaffinity_np(threads_.back().native_handle(), sizeof set, &set);
+        }
+    }
 }
 
 WorkPool::~WorkPool() {
@@ -97,18 +108,65 @@ void WorkPool::run(uint32_t n, const std::function<void(uint32_t)>& fn) {
     }
 }
 
-WorkPool& host_pool() {
-    static WorkPool pool([] {
-        unsigned n = 0;
-        if (const char* s = std::getenv("AC_HOST_THREADS")) n = (unsigned)std::max(1, std::atoi(s));
-        if (!n) {
-            cpu_set_t set;
-            unsigned cpus = std::thread::hardware_concurrency();
-            if (sched_getaffinity(0, sizeof set, &set) == 0) cpus = (unsigned)CPU_COUNT(&set);
-            n = std::max(1u, std::min(16u, cpus));
+namespace {
+std::mutex g_cpus_m;
+std::vector<int> g_cpus;
+}  // namespace
+
+void set_host_cpus(const std::vector<int>& cpus) {
+    std::lock_guard<std::mutex> lk(g_cpus_m);
+    if (g_cpus.empty()) g_cpus = cpus;
+}
+
+std::vector<int> read_cpulist(const char* path) {
+    std::vector<int> out;
+    FILE* f = std::fopen(path, "r");
+    if (!f) return out;
+    char buf[4096];
+    const size_t n = std::fread(buf, 1, sizeof buf - 1, f);
+    std::fclose(f);
+    buf[n] = 0;
+    for (char* p = buf; *p;) {
+        char* e;
+        const long a = std::strtol(p, &e, 10);
+        if (e == p) break;
+        long b = a;
+        p = e;
+        if (*p == '-') {
+            b = std::strtol(p + 1, &e, 10);
+            p = e;
         }
-        return n;
-    }());
+        for (long c = a; c <= b && c < CPU_SETSIZE; ++c) out.push_back((int)c);
+        if (*p == ',') ++p;
+        else break;
+    }
+    return out;
+}
+
+WorkPool& host_pool() {
+    static WorkPool pool(
+        [] {
+            unsigned n = 0;
+            if (const char* s = std::getenv("AC_HOST_THREADS")) n = (unsigned)std::max(1, std::atoi(s));
+            if (!n) {
+                cpu_set_t set;
+                unsigned cpus = std::thread::hardware_concurrency();
+                if (sched_getaffinity(0, sizeof set, &set) == 0) cpus = (unsigned)CPU_COUNT(&set);
+                n = std::max(1u, std::min(16u, cpus));
+            }
+            return n;
+        }(),
+        [] {
+            std::vector<int> use;
+            const char* pin = std::getenv("AC_HOST_PIN");
+            if (pin && std::atoi(pin) == 0) return use;
+            cpu_set_t set;
+            if (sched_getaffinity(0, sizeof set, &set) != 0) return use;
+            std::lock_guard<std::mutex> lk(g_cpus_m);
+            for (int c : g_cpus)
+                if (CPU_ISSET(c, &set)) use.push_back(c);
+            return use;
+        }());
     return pool;
 }
 

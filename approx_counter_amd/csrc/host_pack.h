@@ -21,7 +21,8 @@ namespace acamd {
 // the whole cfg2 stage ~150 us) and then sleep on a condition variable.
 class WorkPool {
 public:
-    explicit WorkPool(unsigned n_threads);  // total participants, caller included
+    // total participants, caller included; worker i is pinned to cpus[i % size] when cpus is non-empty
+    explicit WorkPool(unsigned n_threads, const std::vector<int>& cpus = {});
     ~WorkPool();
     WorkPool(const WorkPool&) = delete;
     WorkPool& operator=(const WorkPool&) = delete;
@@ -51,8 +52,14 @@ private:
 
 // The process-wide pool of the host-buffer entry points.  Size: the
 // AC_HOST_THREADS environment variable, else min(16, CPUs this process may
-// run on); AC_HOST_THREADS=1 packs on the calling thread alone.
+// run on); AC_HOST_THREADS=1 packs on the calling thread alone.  Its workers
+// are pinned to the CPUs given to set_host_cpus() before the pool's first use
+// (the CPUs local to the GPU's PCIe root: the packed block they write is read
+// by that GPU), minus those the process may not use; AC_HOST_PIN=0 disables.
 WorkPool& host_pool();
+void set_host_cpus(const std::vector<int>& cpus);
+// CPUs of a sysfs cpulist ("0-63,128-191"); empty if unreadable.
+std::vector<int> read_cpulist(const char* path);
 
 // Image bases a window of `len` bases occupies (windows start on 32-base
 // boundaries, include/approx_counter_amd.h).
