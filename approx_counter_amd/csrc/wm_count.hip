@@ -134,7 +134,10 @@ typedef const __attribute__((address_space(4))) uint64_t* cu64p;
 typedef const __attribute__((address_space(4))) uint32_t* cu32p;
 __device__ __forceinline__ void load_desc(const uint64_t* start, const uint32_t* length, uint32_t w, uint64_t& base,
                                           uint32_t& len) {
-#ifndef AC_VECTOR_DESC
+#if defined(AC_TIMING_UNIFORM_DESC)  // timing-only A/B: equal windows at a 128-base stride, no descriptor loads
+    base = (uint64_t)w * 128u;
+    len = __builtin_amdgcn_readfirstlane(((cu32p)length)[0]);
+#elif !defined(AC_VECTOR_DESC)
     base = ((cu64p)start)[w];
     len = ((cu32p)length)[w];
 #else
@@ -386,6 +389,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
 #pragma unroll
         for (int p = 0; p < P; ++p) lds.cnt[p * 64 + lane] = 0u;
     }
+    stamp(wave, 7);  // diagnostic builds: the wave's own prologue done, before the barrier
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     stamp(wave, 1);
 

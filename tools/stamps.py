@@ -48,7 +48,13 @@ def main():
     print(f"waves={n} geometry={geo}")
     print("                 p0      p10     p50     p90    p100  (us)")
     print("start        ", pct(us[:, 0]))
+    pre = (raw[:, 7] - t0) / 100.0
+    wib = np.arange(n) % 4  # wave in workgroup (waves are numbered blockIdx * 4 + wib)
     print("prologue len ", pct(us[:, 1] - us[:, 0]))
+    print("  own part   ", pct(pre - us[:, 0]), "(entry -> before the barrier)")
+    print("  own, wave 0", pct((pre - us[:, 0])[wib == 0]), "(k-mer loads + ~Eq table)")
+    print("  own, others", pct((pre - us[:, 0])[wib != 0]))
+    print("  barrier    ", pct(us[:, 1] - pre))
     print("main len     ", pct(us[:, 2] - us[:, 1]))
     print("atomics len  ", pct(us[:, 3] - us[:, 2]))
     print("end          ", pct(us[:, 3]))
