@@ -453,15 +453,18 @@ __device__ __forceinline__ uint32_t bucket_of(uint32_t key, uint32_t nb_log2) {
 // N flags once and rolls the rest (one 2-bit code and one N flag per step),
 // instead of gathering every position's words anew.
 constexpr uint32_t SEG_POS = 16;
+// Windows per keys workgroup: ~100-bp windows make 6 segments each, so 42 of
+// them fill the 256 threads once (16 windows left 62 % of the threads idle).
+constexpr uint32_t KEYS_WINDOWS = 42;
 
 __global__ __launch_bounds__(EXACT_THREADS) void part_keys_kernel(ExactArgs a) {
-    __shared__ uint32_t wseg[EXACT_WINDOWS_PER_BLOCK + 1];  // prefix sums of segments per window
+    __shared__ uint32_t wseg[KEYS_WINDOWS + 1];  // prefix sums of segments per window
     __shared__ uint32_t wsum[EXACT_THREADS / 64];
     __shared__ unsigned long long base_sh;
     __shared__ uint32_t n_had;
     const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
-    const uint32_t w0 = blockIdx.x * EXACT_WINDOWS_PER_BLOCK;
-    const uint32_t nw = min((uint32_t)EXACT_WINDOWS_PER_BLOCK, a.n_windows - w0);
+    const uint32_t w0 = blockIdx.x * KEYS_WINDOWS;
+    const uint32_t nw = min(KEYS_WINDOWS, a.n_windows - w0);
     if (t == 0) {
         uint32_t acc = 0;
         for (uint32_t i = 0; i < nw; ++i) {
@@ -815,7 +818,7 @@ hipError_t launch_exact_part_count(const ExactArgs& a, hipStream_t stream) {
 hipError_t launch_exact_partitioned(const ExactArgs& a, hipStream_t stream) {
     if (a.nb_log2 < 6 || a.nb_log2 > MAX_NB_LOG2) return hipErrorInvalidValue;
     const uint32_t NB = 1u << a.nb_log2;
-    const uint32_t wblocks = (a.n_windows + EXACT_WINDOWS_PER_BLOCK - 1) / EXACT_WINDOWS_PER_BLOCK;
+    const uint32_t wblocks = (a.n_windows + KEYS_WINDOWS - 1) / KEYS_WINDOWS;
     if (wblocks) hipLaunchKernelGGL(part_keys_kernel, dim3(wblocks), dim3(EXACT_THREADS), 0, stream, a);
     const dim3 cols((NB + EXACT_THREADS - 1) / EXACT_THREADS), cols_groups(cols.x, a.n_groups);
     hipLaunchKernelGGL(part_hist_kernel, dim3(a.n_chunks), dim3(EXACT_THREADS), 0, stream, a);
