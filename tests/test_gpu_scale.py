@@ -1,7 +1,8 @@
 """BASELINE.json configurations 3-5 at full size on the GPU.
 
 cfg3 (k=16, 100k reads, lim=2000) and cfg5 (k=22, sl=150, lim=1000): bit-exact
-against the oracle over every candidate, both ends fused in one launch.
+against the oracle over every candidate, both ends fused in one launch, through
+the device-segment entry point and through the host-buffer stage.
 cfg4 (k=16, 1M windows per end, lim=500): bit-exact against the oracle over
 every candidate and window, plus the shard-accumulation identity."""
 import numpy as np
@@ -31,8 +32,11 @@ def test_full_config_bit_exact(counter, cfg):
     parts = [(wl[e]["kmers"], wl[e]["windows"]) for e in ("start", "end")]
     assert all(km.size == cfg["lim"] for km, _ in parts)
     got = fused_counts(counter, cfg["k"], parts)
-    for (km, w), g in zip(parts, got):
-        assert np.array_equal(g, oracle.count_myers(cfg["k"], km, w, THREADS))
+    staged = counter.count_jobs(cfg["k"], [(km, ac.Dna5Sample.from_windows(w)) for km, w in parts])
+    for (km, w), g, s in zip(parts, got, staged):
+        exp = oracle.count_myers(cfg["k"], km, w, THREADS)
+        assert np.array_equal(g, exp)  # device segments, one fused launch
+        assert np.array_equal(s, exp)  # the product stage: Dna5 host buffers -> host counts
 
 
 def test_cfg4_full_parity_and_shards(counter):
