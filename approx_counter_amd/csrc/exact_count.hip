@@ -204,6 +204,23 @@ __device__ __forceinline__ float complexity(uint64_t kmer, uint32_t k) {
     return (float)sum / (float)(2 * ((int)k - 2));
 }
 
+// The same score for k <= 16: at most 15 dimers, so each of the 16 dimer
+// counts fits a 4-bit field of one 64-bit register (one shift + add per dimer).
+__device__ __forceinline__ float complexity16(uint32_t kmer, uint32_t k) {
+    uint64_t c = 0;
+    for (uint32_t i = 0; i + 1 < k; ++i) {
+        c += 1ull << (4u * (kmer & 15u));
+        kmer >>= 2;
+    }
+    uint32_t sum = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const uint32_t v = (uint32_t)(c >> (4 * i)) & 15u;
+        sum += v * (v - 1u);  // 0 * (0 - 1) wraps to 0, as in the reference
+    }
+    return (float)sum / (float)(2 * ((int)k - 2));
+}
+
 __device__ __forceinline__ bool is_forbidden(const ExactArgs& a, uint64_t key) {
     uint32_t lo = 0, hi = a.n_forbidden;
     while (lo < hi) {
@@ -679,7 +696,18 @@ __global__ __launch_bounds__(EXACT_THREADS) void part_count_kernel(ExactArgs a) 
     }
     BlockAppender app{a.list_keys, a.list_cnts, a.n_list, a.list_cap, app_k, app_c, &app_n, &app_b};
     // Persistent: workgroup g counts buckets g, g + grid, ...; between buckets
-    // only the claimed slots are cleared.
+    // only the claimed slots are cleared.  The first batch of keys of the next
+    // bucket is requested before this bucket is scored, so its load latency
+    // hides behind the scoring.
+    uint32_t nxt[COUNT_BATCH];
+    auto load_batch = [&](uint32_t* dst, uint32_t i0, uint32_t hi) __attribute__((always_inline)) {
+#pragma unroll
+        for (uint32_t r = 0; r < COUNT_BATCH; ++r) {
+            const uint32_t i = i0 + r * EXACT_THREADS + t;
+            dst[r] = i < hi ? a.parts[i] : 0u;
+        }
+    };
+    if (blockIdx.x < NB) load_batch(nxt, a.bstart[blockIdx.x], a.bstart[blockIdx.x + 1]);
     for (uint32_t b = blockIdx.x; b < NB; b += gridDim.x) {
         for (uint32_t i = t; i < EXACT_PHIST; i += EXACT_THREADS) hist[i] = 0;
         __syncthreads();
@@ -687,10 +715,11 @@ __global__ __launch_bounds__(EXACT_THREADS) void part_count_kernel(ExactArgs a) 
         uint32_t allt = 0;
         for (uint32_t i0 = lo; i0 < hi; i0 += EXACT_THREADS * COUNT_BATCH) {  // block-uniform batches
             uint32_t kb[COUNT_BATCH];
+            if (i0 == lo) {
 #pragma unroll
-            for (uint32_t r = 0; r < COUNT_BATCH; ++r) {
-                const uint32_t i = i0 + r * EXACT_THREADS + t;
-                kb[r] = i < hi ? a.parts[i] : 0u;
+                for (uint32_t r = 0; r < COUNT_BATCH; ++r) kb[r] = nxt[r];
+            } else {
+                load_batch(kb, i0, hi);
             }
 #pragma unroll
             for (uint32_t r = 0; r < COUNT_BATCH; ++r) {
@@ -733,6 +762,7 @@ __global__ __launch_bounds__(EXACT_THREADS) void part_count_kernel(ExactArgs a) 
             }
         }
         if (allt) atomicAdd(&n_allt, allt);
+        if (b + gridDim.x < NB) load_batch(nxt, a.bstart[b + gridDim.x], a.bstart[b + gridDim.x + 1]);
         __syncthreads();
         uint32_t ones = 0;
         const uint32_t m = n_occ;
@@ -745,7 +775,7 @@ __global__ __launch_bounds__(EXACT_THREADS) void part_count_kernel(ExactArgs a) 
                 c = tc[s];
                 tk[s] = 0;  // cleared for the next bucket
                 tc[s] = 0;
-                if (complexity(key, a.k) >= a.lc_threshold) c = 0;  // haveLowComplexity (214-234)
+                if (complexity16((uint32_t)key, a.k) >= a.lc_threshold) c = 0;  // haveLowComplexity (214-234)
                 else if (is_forbidden(a, key)) c = 0;              // isForbiddenKmer (330-332)
             }
             if (!a.emit_only && c) {
