@@ -89,7 +89,7 @@ struct ExactArgs {
 
 #define EXACT_PHIST 32  // per-bucket partial histogram bins (counts 1..32; larger counts go straight to hist)
 
-#define EXACT_CHUNK 16384  // dense keys per histogram / scatter workgroup
+#define EXACT_CHUNK 16384  // dense keys per histogram / scatter workgroup (65,536: histogram 26 -> 79 us, scatter unchanged)
 #define EXACT_GROUP 32     // chunks per partial column sum
 #define EXACT_BUCKET_SLOTS 4096  // LDS counting table of the per-bucket kernel (32 KB of keys + counts)
 
