@@ -48,7 +48,7 @@ struct ac_ctx {
     // working set (table keys, table counts, small scalars + histogram, forbidden, gather out)
     void* s_buf[4] = {nullptr, nullptr, nullptr, nullptr};
     size_t s_cap[4] = {0, 0, 0, 0};
-    // (+ the partitioned path's keys, parts, chist, gsum, bstart, phist: e_buf[6..11])
+    // (+ the partitioned path's keys, parts, tmp, h1/h2/stot, bstart, phist: e_buf[6..11])
     void* e_buf[12] = {};
     size_t e_cap[12] = {};
     // Count-kernel scratch, one set per stream a launch may run on at the same
@@ -733,20 +733,24 @@ ac_status ac_exact_count_device(ac_ctx* ctx, uint32_t k, const ac_windows* dev, 
         while (nb_log2 < 13 && (key_cap >> nb_log2) > 2048) ++nb_log2;
         a.nb_log2 = nb_log2;
         a.key_cap = key_cap;
+        a.s_log2 = nb_log2 > 7 ? 7 : nb_log2;  // 128 super-buckets of <= 64 buckets
         a.n_chunks = (uint32_t)((key_cap + EXACT_CHUNK - 1) / EXACT_CHUNK);
-        a.n_groups = (a.n_chunks + EXACT_GROUP - 1) / EXACT_GROUP;
-        const size_t NB = size_t(1) << nb_log2;
+        a.n_chunks2 = a.n_chunks + (1u << a.s_log2);
+        const size_t NB = size_t(1) << nb_log2, S = size_t(1) << a.s_log2;
+        const size_t h1 = S * a.n_chunks, h2 = (NB / S) * a.n_chunks2;
         if (ac_status s2 = grow(ctx, &ctx->e_buf[6], &ctx->e_cap[6], sizeof(uint32_t) * key_cap)) return s2;
         if (ac_status s2 = grow(ctx, &ctx->e_buf[7], &ctx->e_cap[7], sizeof(uint32_t) * key_cap)) return s2;
-        if (ac_status s2 = grow(ctx, &ctx->e_buf[8], &ctx->e_cap[8], sizeof(uint32_t) * NB * a.n_chunks)) return s2;
-        if (ac_status s2 = grow(ctx, &ctx->e_buf[9], &ctx->e_cap[9], sizeof(uint32_t) * NB * a.n_groups)) return s2;
+        if (ac_status s2 = grow(ctx, &ctx->e_buf[8], &ctx->e_cap[8], sizeof(uint32_t) * key_cap)) return s2;
+        if (ac_status s2 = grow(ctx, &ctx->e_buf[9], &ctx->e_cap[9], sizeof(uint32_t) * (h1 + h2 + S))) return s2;
         if (ac_status s2 = grow(ctx, &ctx->e_buf[10], &ctx->e_cap[10], sizeof(uint32_t) * (NB + 1))) return s2;
         if (ac_status s2 = grow(ctx, &ctx->e_buf[11], &ctx->e_cap[11], sizeof(uint32_t) * NB * EXACT_PHIST)) return s2;
         a.phist = (uint32_t*)ctx->e_buf[11];
         a.keys = (uint32_t*)ctx->e_buf[6];
         a.parts = (uint32_t*)ctx->e_buf[7];
-        a.chist = (uint32_t*)ctx->e_buf[8];
-        a.gsum = (uint32_t*)ctx->e_buf[9];
+        a.tmp = (uint32_t*)ctx->e_buf[8];
+        a.h1 = (uint32_t*)ctx->e_buf[9];
+        a.h2 = a.h1 + h1;
+        a.stot = a.h2 + h2;
         a.bstart = (uint32_t*)ctx->e_buf[10];
         AC_HIP(ctx, hipMemsetAsync(small, 0, small_bytes, st));
         AC_HIP(ctx, acamd::launch_exact_partitioned(a, st));

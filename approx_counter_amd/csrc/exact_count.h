@@ -66,20 +66,23 @@ struct ExactArgs {
     unsigned long long* n_out;
     uint64_t out_cap;
     // Partitioned path (k <= 16): every k-mer position's key
-    // written densely (`keys`, n_keys of them), a per-chunk histogram of their
-    // bucket (hash high bits) in `chist` ([chunk][bucket], turned into each
-    // chunk's offset within its bucket), bucket starts in `bstart` (nb + 1),
-    // the keys scattered bucket by bucket into `parts`, then one workgroup per
-    // bucket counts its keys in LDS.  No global hash table.
+    // written densely (`keys`, n_keys of them), moved into 2^s_log2
+    // super-buckets (`tmp`; per-chunk histogram h1 [chunk][super], sizes
+    // stot), then into the 2^nb_log2 buckets (`parts`; per level-2 chunk
+    // histogram h2 [chunk][sub]; bucket starts bstart, nb + 1 of them); one
+    // workgroup per bucket counts its keys in LDS.  No global hash table.
     uint32_t* keys;
+    uint32_t* tmp;
     uint32_t* parts;
     unsigned long long* n_keys;
-    uint32_t* chist;
-    uint32_t* gsum;    // [group][bucket] partial column sums of chist
+    uint32_t* h1;
+    uint32_t* h2;
+    uint32_t* stot;
     uint32_t* bstart;  // nb + 1
     uint32_t nb_log2;
-    uint32_t n_chunks;  // launch bound: ceil(key capacity / EXACT_CHUNK)
-    uint32_t n_groups;  // ceil(n_chunks / EXACT_GROUP)
+    uint32_t s_log2;    // super-buckets: nb_log2 - s_log2 <= 6
+    uint32_t n_chunks;  // level-1 grid: ceil(key capacity / EXACT_CHUNK)
+    uint32_t n_chunks2; // level-2 grid bound: n_chunks + 2^s_log2
     uint64_t key_cap;
     uint32_t list_min;   // the count kernel lists kept entries with count >= list_min
     uint32_t emit_only;  // 1: list only (the histogram and distinct count were taken by an earlier pass)
@@ -89,8 +92,9 @@ struct ExactArgs {
 
 #define EXACT_PHIST 32  // per-bucket partial histogram bins (counts 1..32; larger counts go straight to hist)
 
-#define EXACT_CHUNK 16384  // dense keys per histogram / scatter workgroup (65,536: histogram 26 -> 79 us, scatter unchanged)
-#define EXACT_GROUP 32     // chunks per partial column sum
+#define EXACT_CHUNK 8192  // keys per histogram / scatter workgroup of either partition level (16,384: 2 scatter workgroups per CU, level-2 scatter 37 us)
+#define EXACT_MAX_SUPER 128  // level-1 super-buckets (at most)
+#define EXACT_MAX_SUB 64     // buckets per super-bucket (at most)
 #define EXACT_BUCKET_SLOTS 4096  // LDS counting table of the per-bucket kernel (32 KB of keys + counts)
 
 hipError_t launch_exact_insert(const ExactArgs& a, hipStream_t stream);

@@ -461,8 +461,60 @@ __global__ __launch_bounds__(EXACT_THREADS) void exact_gather_list_kernel(ExactA
 constexpr uint32_t MAX_NB_LOG2 = 13;
 constexpr uint32_t COUNT_PROBES = 64;
 
+// Hash of a k <= 16 key for the partition (its top bits pick the bucket) and
+// the per-bucket LDS table (its low bits pick the slot): a 32-bit mixer
+// (two u32 multiplies; the 64-bit murmur finaliser costs ~8 quarter-rate
+// multiplies and the partition hashes every key five times).
+__device__ __forceinline__ uint32_t part_hash(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+
 __device__ __forceinline__ uint32_t bucket_of(uint32_t key, uint32_t nb_log2) {
-    return (uint32_t)(mix64(key) >> (64u - nb_log2));
+    return part_hash(key) >> (32u - nb_log2);
+}
+
+// Exclusive prefix of a block's values (thread t holds x); returns the total.
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t& excl, uint32_t* wsum) {
+    const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+    uint32_t incl = x;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(incl, d, 64);
+        if ((int)lane >= d) incl += y;
+    }
+    if (lane == 63u) wsum[wv] = incl;
+    __syncthreads();
+    uint32_t before = 0, total = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < EXACT_THREADS / 64; ++w) {
+        before += w < wv ? wsum[w] : 0u;
+        total += wsum[w];
+    }
+    __syncthreads();  // wsum may be reused
+    excl = before + incl - x;
+    return total;
+}
+
+// LDS bin counter add for the active lanes of a wave, returning each lane's
+// rank among the adds to its bin.  The lanes sharing the first active lane's
+// bin take one add of their number: a chunk of an adapter-heavy bucket is
+// mostly one key, and 64 same-address LDS atomics serialise.  Used by the
+// level-2 histogram (16 -> 14 us); in hist1 and the scatters the extra
+// ballot / bpermute cost more than the merging saved (9 -> 11, 23 -> 29,
+// 37 -> 49 us; profiles/r02_exact_log.md).
+__device__ __forceinline__ uint32_t wave_bin_add(uint32_t* cnt, uint32_t b) {
+    const uint32_t b0 = __builtin_amdgcn_readfirstlane(b);
+    const uint64_t same = __ballot(b == b0);
+    const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(same >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)same, 0u));
+    uint32_t old = 0;
+    if (b != b0 || pre == 0) old = atomicAdd(&cnt[b], b == b0 ? (uint32_t)__popcll(same) : 1u);
+    const uint32_t base = __shfl(old, __ffsll((unsigned long long)same) - 1, 64);
+    return b == b0 ? base + pre : old;
 }
 
 // Keys of every k-mer position, written densely.  A thread takes SEG_POS
@@ -482,19 +534,23 @@ __global__ __launch_bounds__(EXACT_THREADS) void part_keys_kernel(ExactArgs a) {
     const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
     const uint32_t w0 = blockIdx.x * KEYS_WINDOWS;
     const uint32_t nw = min(KEYS_WINDOWS, a.n_windows - w0);
-    if (t == 0) {
-        uint32_t acc = 0;
-        for (uint32_t i = 0; i < nw; ++i) {
-            wseg[i] = acc;
-            const uint64_t st = a.start[w0 + i];
-            const uint32_t len = a.length[w0 + i];
+    {  // segments per window: thread i < nw takes window w0 + i, a block scan makes wseg
+        uint32_t nseg = 0;
+        if (t < nw) {
+            const uint64_t st = a.start[w0 + t];
+            const uint32_t len = a.length[w0 + t];
             const bool ok = !(st & 31u) && len <= a.n_bases && st <= a.n_bases - len;
             if (!ok) atomicOr(a.err, AC_DEVERR_WINDOW);
             const uint32_t npos = (ok && len >= a.k) ? len - a.k + 1u : 0u;
-            acc += (npos + SEG_POS - 1u) / SEG_POS;
+            nseg = (npos + SEG_POS - 1u) / SEG_POS;
         }
-        wseg[nw] = acc;
-        n_had = 0;
+        uint32_t excl;
+        const uint32_t tot = block_excl_scan(nseg, excl, wsum);
+        if (t < nw) wseg[t] = excl;
+        if (t == 0) {
+            wseg[nw] = tot;
+            n_had = 0;
+        }
     }
     __syncthreads();
     const uint32_t total = wseg[nw];
@@ -507,8 +563,11 @@ __global__ __launch_bounds__(EXACT_THREADS) void part_keys_kernel(ExactArgs a) {
         uint32_t key[SEG_POS];
         uint32_t valid = 0, c = 0;
         if (sg < total) {
-            uint32_t i = 0;
-            while (wseg[i + 1] <= sg) ++i;
+            uint32_t i = 0, r = nw;  // the window holding segment sg: the last i with wseg[i] <= sg
+            while (r - i > 1) {
+                const uint32_t m = (i + r) >> 1;
+                if (wseg[m] <= sg) i = m; else r = m;
+            }
             const uint64_t wst = a.start[w0 + i];
             const uint32_t npos = a.length[w0 + i] - k + 1u;
             const uint32_t p0 = (sg - wseg[i]) * SEG_POS;
@@ -565,96 +624,232 @@ __global__ __launch_bounds__(EXACT_THREADS) void part_keys_kernel(ExactArgs a) {
     if (t == 0 && n_had) atomicAdd(a.had_n, (unsigned long long)n_had);
 }
 
-__global__ __launch_bounds__(EXACT_THREADS) void part_hist_kernel(ExactArgs a) {
-    __shared__ uint32_t h[1u << MAX_NB_LOG2];
-    const uint32_t NB = 1u << a.nb_log2, t = threadIdx.x;
-    for (uint32_t i = t; i < NB; i += EXACT_THREADS) h[i] = 0;
-    __syncthreads();
-    const uint64_t n = min((unsigned long long)a.key_cap, *a.n_keys);
-    const uint64_t lo = (uint64_t)blockIdx.x * EXACT_CHUNK, hi = min(n, lo + EXACT_CHUNK);
-    for (uint64_t i = lo + t; i < hi; i += EXACT_THREADS) atomicAdd(&h[bucket_of(a.keys[i], a.nb_log2)], 1u);
-    __syncthreads();
-    uint32_t* row = a.chist + (uint64_t)blockIdx.x * NB;
-    for (uint32_t i = t; i < NB; i += EXACT_THREADS) row[i] = h[i];
+// Two-level partition of the dense keys into the NB = 2^nb_log2 buckets (a
+// bucket = the top nb_log2 bits of the key's hash).  One pass into 8,192
+// buckets leaves ~2 keys per bucket in a chunk: the per-chunk histogram is as
+// large as the keys and the scatter is one isolated 4-byte write per key
+// (hist + scans + scatter 166 us at 10^5 windows; profiles/r02_exact_log.md).
+// Level 1 moves the keys into S = 2^s_log2 super-buckets (the top s_log2 bits),
+// level 2 splits each super-bucket into its SUB = NB / S buckets.  Both levels
+// work on chunks of EXACT_CHUNK keys, so a super-bucket swollen by one
+// adapter k-mer is still split over many workgroups.
+
+__device__ __forceinline__ uint32_t super_of(uint32_t key, uint32_t s_log2) {
+    return part_hash(key) >> (32u - s_log2);
 }
 
-// Column sums of EXACT_GROUP chunk rows: gsum[g][b].
-__global__ __launch_bounds__(EXACT_THREADS) void part_colsum_kernel(ExactArgs a) {
-    const uint32_t NB = 1u << a.nb_log2;
-    const uint32_t b = blockIdx.x * EXACT_THREADS + threadIdx.x, g = blockIdx.y;
-    if (b >= NB) return;
-    const uint32_t r1 = min(a.n_chunks, (g + 1) * EXACT_GROUP);
-    uint32_t sum = 0;
-    for (uint32_t r = g * EXACT_GROUP; r < r1; ++r) sum += a.chist[(uint64_t)r * NB + b];
-    a.gsum[(uint64_t)g * NB + b] = sum;
-}
-
-// Per bucket: exclusive prefix over the groups (in place) and the bucket total.
-__global__ __launch_bounds__(EXACT_THREADS) void part_groupscan_kernel(ExactArgs a) {
-    const uint32_t NB = 1u << a.nb_log2;
-    const uint32_t b = blockIdx.x * EXACT_THREADS + threadIdx.x;
-    if (b >= NB) return;
-    uint32_t run = 0;
-    for (uint32_t g = 0; g < a.n_groups; ++g) {
-        const uint32_t x = a.gsum[(uint64_t)g * NB + b];
-        a.gsum[(uint64_t)g * NB + b] = run;
-        run += x;
+// f(key) for the keys src[lo, hi), the workgroup's threads striding; PART_BATCH
+// loads per thread are issued before their keys are used.
+constexpr uint32_t PART_BATCH = 8;
+template <class F>
+__device__ __forceinline__ void for_keys(const uint32_t* src, uint64_t lo, uint64_t hi, F f) {
+    const uint32_t t = threadIdx.x;
+    for (uint64_t i0 = lo; i0 < hi; i0 += EXACT_THREADS * PART_BATCH) {
+        uint32_t v[PART_BATCH];
+#pragma unroll
+        for (uint32_t r = 0; r < PART_BATCH; ++r) {
+            const uint64_t i = i0 + r * EXACT_THREADS + t;
+            v[r] = i < hi ? src[i] : 0u;
+        }
+#pragma unroll
+        for (uint32_t r = 0; r < PART_BATCH; ++r)
+            if (i0 + r * EXACT_THREADS + t < hi) f(v[r]);
     }
-    a.bstart[b] = run;
 }
 
-// Bucket totals -> exclusive starts (one workgroup of 1,024 threads, NB <= 8,192).
-__global__ __launch_bounds__(1024) void part_bucketscan_kernel(ExactArgs a) {
-    __shared__ uint32_t sums[1024];
-    const uint32_t NB = 1u << a.nb_log2, t = threadIdx.x;
-    const uint32_t per = (NB + 1023u) / 1024u, b0 = t * per;
+// Keys the partition holds: every position key, capped at the buffers' size.
+__device__ __forceinline__ uint32_t part_n(const ExactArgs& a) {
+    return (uint32_t)min((unsigned long long)a.key_cap, *a.n_keys);
+}
+
+// Level 1, per chunk: h1[chunk][s] = its keys in super-bucket s.
+__global__ __launch_bounds__(EXACT_THREADS) void part_hist1_kernel(ExactArgs a) {
+    __shared__ uint32_t h[EXACT_MAX_SUPER];
+    const uint32_t S = 1u << a.s_log2, t = threadIdx.x;
+    for (uint32_t i = t; i < S; i += EXACT_THREADS) h[i] = 0;
+    __syncthreads();
+    const uint32_t n = part_n(a);
+    const uint64_t lo = (uint64_t)blockIdx.x * EXACT_CHUNK, hi = min((uint64_t)n, lo + EXACT_CHUNK);
+    for_keys(a.keys, lo, hi, [&](uint32_t key) { atomicAdd(&h[super_of(key, a.s_log2)], 1u); });
+    __syncthreads();
+    for (uint32_t i = t; i < S; i += EXACT_THREADS) a.h1[(uint64_t)blockIdx.x * S + i] = h[i];
+}
+
+// Level 1, per super-bucket (one workgroup each): h1[.][s] -> each chunk's
+// offset inside super-bucket s; stot[s] = the super-bucket's size.
+__global__ __launch_bounds__(EXACT_THREADS) void part_scan1_kernel(ExactArgs a) {
+    __shared__ uint32_t wsum[EXACT_THREADS / 64];
+    const uint32_t S = 1u << a.s_log2, s = blockIdx.x, t = threadIdx.x;
+    const uint32_t per = (a.n_chunks + EXACT_THREADS - 1) / EXACT_THREADS;
+    const uint32_t r0 = min(a.n_chunks, t * per), r1 = min(a.n_chunks, r0 + per);
     uint32_t local = 0;
-    for (uint32_t b = b0; b < min(NB, b0 + per); ++b) local += a.bstart[b];
-    sums[t] = local;
-    __syncthreads();
-    for (uint32_t d = 1; d < 1024; d <<= 1) {  // Hillis-Steele inclusive scan
-        const uint32_t y = t >= d ? sums[t - d] : 0u;
-        __syncthreads();
-        sums[t] += y;
-        __syncthreads();
-    }
-    uint32_t run = sums[t] - local;
-    for (uint32_t b = b0; b < min(NB, b0 + per); ++b) {
-        const uint32_t x = a.bstart[b];
-        a.bstart[b] = run;
-        run += x;
-    }
-    if (t == 1023u) a.bstart[NB] = sums[1023];
-}
-
-// chist[r][b] <- global position of chunk r's first key of bucket b.
-__global__ __launch_bounds__(EXACT_THREADS) void part_offsets_kernel(ExactArgs a) {
-    const uint32_t NB = 1u << a.nb_log2;
-    const uint32_t b = blockIdx.x * EXACT_THREADS + threadIdx.x, g = blockIdx.y;
-    if (b >= NB) return;
-    uint32_t run = a.bstart[b] + a.gsum[(uint64_t)g * NB + b];
-    const uint32_t r1 = min(a.n_chunks, (g + 1) * EXACT_GROUP);
-    for (uint32_t r = g * EXACT_GROUP; r < r1; ++r) {
-        uint32_t* c = &a.chist[(uint64_t)r * NB + b];
+    for (uint32_t r = r0; r < r1; ++r) local += a.h1[(uint64_t)r * S + s];
+    uint32_t run;
+    const uint32_t total = block_excl_scan(local, run, wsum);
+    for (uint32_t r = r0; r < r1; ++r) {
+        uint32_t* c = &a.h1[(uint64_t)r * S + s];
         const uint32_t x = *c;
         *c = run;
         run += x;
     }
+    if (t == 0) a.stot[s] = total;
 }
 
-__global__ __launch_bounds__(EXACT_THREADS) void part_scatter_kernel(ExactArgs a) {
-    __shared__ uint32_t cur[1u << MAX_NB_LOG2];
-    const uint32_t NB = 1u << a.nb_log2, t = threadIdx.x;
-    const uint32_t* row = a.chist + (uint64_t)blockIdx.x * NB;
-    for (uint32_t i = t; i < NB; i += EXACT_THREADS) cur[i] = row[i];
-    __syncthreads();
-    const uint64_t n = min((unsigned long long)a.key_cap, *a.n_keys);
-    const uint64_t lo = (uint64_t)blockIdx.x * EXACT_CHUNK, hi = min(n, lo + EXACT_CHUNK);
-    for (uint64_t i = lo + t; i < hi; i += EXACT_THREADS) {
-        const uint32_t key = a.keys[i];
-        const uint32_t pos = atomicAdd(&cur[bucket_of(key, a.nb_log2)], 1u);
-        a.parts[pos] = key;
+// Every workgroup of the later steps rebuilds, from stot, the super-buckets'
+// starts (sstart[0..S]) and the first level-2 chunk of each (cbeg[0..S]).
+__device__ __forceinline__ void super_layout(const ExactArgs& a, uint32_t* sstart, uint32_t* cbeg, uint32_t* wsum) {
+    const uint32_t S = 1u << a.s_log2, t = threadIdx.x;
+    const uint32_t v = t < S ? a.stot[t] : 0u;
+    const uint32_t c = (v + EXACT_CHUNK - 1u) / EXACT_CHUNK;
+    uint32_t ev, ec;
+    const uint32_t tv = block_excl_scan(v, ev, wsum);
+    const uint32_t tc = block_excl_scan(c, ec, wsum);
+    if (t < S) {
+        sstart[t] = ev;
+        cbeg[t] = ec;
     }
+    if (t == 0) {
+        sstart[S] = tv;
+        cbeg[S] = tc;
+    }
+    __syncthreads();
+}
+
+// Scatter of one chunk (n <= EXACT_CHUNK keys src[lo, lo + n)) into bins:
+// the keys are first grouped by bin in LDS (`stage`), then written out in that
+// order, so each bin's keys leave as one contiguous run at gcur[bin] (the
+// chunk's global start in that bin) instead of as isolated 4-byte stores.
+// `cnt` (nbins <= EXACT_THREADS, zeroed by the caller) and `stage` are LDS.
+constexpr uint32_t SCATTER_PER = EXACT_CHUNK / EXACT_THREADS;
+template <class Bin>
+__device__ __forceinline__ void staged_scatter(const uint32_t* __restrict__ src, uint64_t lo, uint32_t n,
+                                               uint32_t* __restrict__ dst, uint32_t nbins, uint32_t* cnt,
+                                               const uint32_t* gcur, uint32_t* stage, uint32_t* wsum, Bin bin) {
+    const uint32_t t = threadIdx.x;
+    uint32_t key[SCATTER_PER], rank[SCATTER_PER];
+#pragma unroll
+    for (uint32_t r = 0; r < SCATTER_PER; ++r) {
+        const uint32_t i = r * EXACT_THREADS + t;
+        key[r] = i < n ? src[lo + i] : 0u;
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < SCATTER_PER; ++r)
+        if (r * EXACT_THREADS + t < n) rank[r] = atomicAdd(&cnt[bin(key[r])], 1u);
+    __syncthreads();
+    uint32_t lstart;
+    block_excl_scan(t < nbins ? cnt[t] : 0u, lstart, wsum);
+    if (t < nbins) cnt[t] = lstart;
+    __syncthreads();
+#pragma unroll
+    for (uint32_t r = 0; r < SCATTER_PER; ++r)
+        if (r * EXACT_THREADS + t < n) stage[cnt[bin(key[r])] + rank[r]] = key[r];
+    __syncthreads();
+    for (uint32_t i = t; i < n; i += EXACT_THREADS) {
+        const uint32_t k = stage[i], b = bin(k);
+        dst[gcur[b] + (i - cnt[b])] = k;
+    }
+}
+
+// Level 1 scatter: each chunk's keys to its ranges of the super-buckets (LDS cursors).
+__global__ __launch_bounds__(EXACT_THREADS) void part_scatter1_kernel(ExactArgs a) {
+    __shared__ uint32_t sstart[EXACT_MAX_SUPER + 1], cbeg[EXACT_MAX_SUPER + 1], wsum[EXACT_THREADS / 64];
+    __shared__ uint32_t cur[EXACT_MAX_SUPER], cnt[EXACT_MAX_SUPER];
+    __shared__ uint32_t stage[EXACT_CHUNK];
+    const uint32_t S = 1u << a.s_log2, t = threadIdx.x;
+    super_layout(a, sstart, cbeg, wsum);
+    for (uint32_t i = t; i < S; i += EXACT_THREADS) {
+        cur[i] = sstart[i] + a.h1[(uint64_t)blockIdx.x * S + i];
+        cnt[i] = 0;
+    }
+    __syncthreads();
+    const uint32_t n = part_n(a);
+    const uint64_t lo = (uint64_t)blockIdx.x * EXACT_CHUNK;
+    if (lo >= n) return;
+    const uint32_t s_log2 = a.s_log2;
+    staged_scatter(a.keys, lo, (uint32_t)min((uint64_t)EXACT_CHUNK, n - lo), a.tmp, S, cnt, cur, stage, wsum,
+                   [=](uint32_t key) { return super_of(key, s_log2); });
+}
+
+// Level-2 chunk i: its super-bucket and key range [lo, hi) in tmp; false past the last chunk.
+__device__ __forceinline__ bool chunk2(const ExactArgs& a, const uint32_t* sstart, const uint32_t* cbeg, uint32_t i,
+                                       uint32_t& s, uint32_t& lo, uint32_t& hi) {
+    const uint32_t S = 1u << a.s_log2;
+    if (i >= cbeg[S]) return false;
+    uint32_t l = 0, r = S;  // the last s with cbeg[s] <= i (super-buckets without chunks share cbeg)
+    while (r - l > 1) {
+        const uint32_t m = (l + r) >> 1;
+        if (cbeg[m] <= i) l = m; else r = m;
+    }
+    s = l;
+    lo = sstart[s] + (i - cbeg[s]) * EXACT_CHUNK;
+    hi = min(sstart[s + 1], lo + EXACT_CHUNK);
+    return true;
+}
+
+// Level 2, per chunk of a super-bucket: h2[chunk][j] = its keys in sub-bucket j.
+__global__ __launch_bounds__(EXACT_THREADS) void part_hist2_kernel(ExactArgs a) {
+    __shared__ uint32_t sstart[EXACT_MAX_SUPER + 1], cbeg[EXACT_MAX_SUPER + 1], wsum[EXACT_THREADS / 64];
+    __shared__ uint32_t h[EXACT_MAX_SUB];
+    const uint32_t SUB = 1u << (a.nb_log2 - a.s_log2), t = threadIdx.x;
+    super_layout(a, sstart, cbeg, wsum);
+    uint32_t s, lo, hi;
+    if (!chunk2(a, sstart, cbeg, blockIdx.x, s, lo, hi)) return;
+    for (uint32_t j = t; j < SUB; j += EXACT_THREADS) h[j] = 0;
+    __syncthreads();
+    for_keys(a.tmp, lo, hi, [&](uint32_t key) { wave_bin_add(h, bucket_of(key, a.nb_log2) & (SUB - 1u)); });
+    __syncthreads();
+    for (uint32_t j = t; j < SUB; j += EXACT_THREADS) a.h2[(uint64_t)blockIdx.x * SUB + j] = h[j];
+}
+
+// Level 2, per super-bucket (one wave each, lane j = sub-bucket j): bucket
+// starts bstart[s * SUB + j] (and bstart[NB]), h2 -> each chunk's cursor.
+__global__ __launch_bounds__(EXACT_THREADS) void part_scan2_kernel(ExactArgs a) {
+    __shared__ uint32_t sstart[EXACT_MAX_SUPER + 1], cbeg[EXACT_MAX_SUPER + 1], wsum[EXACT_THREADS / 64];
+    const uint32_t S = 1u << a.s_log2, SUB = 1u << (a.nb_log2 - a.s_log2);
+    super_layout(a, sstart, cbeg, wsum);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t s = blockIdx.x * (EXACT_THREADS / 64) + (threadIdx.x >> 6);
+    if (s >= S) return;
+    const uint32_t c0 = cbeg[s], c1 = cbeg[s + 1];
+    uint32_t tot = 0;
+    if (lane < SUB)
+        for (uint32_t c = c0; c < c1; ++c) tot += a.h2[(uint64_t)c * SUB + lane];
+    uint32_t incl = tot;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(incl, d, 64);
+        if ((int)lane >= d) incl += y;
+    }
+    uint32_t run = sstart[s] + incl - tot;
+    if (lane < SUB) {
+        a.bstart[s * SUB + lane] = run;
+        for (uint32_t c = c0; c < c1; ++c) {
+            uint32_t* p = &a.h2[(uint64_t)c * SUB + lane];
+            const uint32_t x = *p;
+            *p = run;
+            run += x;
+        }
+    }
+    if (s == S - 1u && lane == 0) a.bstart[S * SUB] = sstart[S];
+}
+
+// Level 2 scatter: a chunk's keys to their buckets in `parts`.
+__global__ __launch_bounds__(EXACT_THREADS) void part_scatter2_kernel(ExactArgs a) {
+    __shared__ uint32_t sstart[EXACT_MAX_SUPER + 1], cbeg[EXACT_MAX_SUPER + 1], wsum[EXACT_THREADS / 64];
+    __shared__ uint32_t cur[EXACT_MAX_SUB], cnt[EXACT_MAX_SUB];
+    __shared__ uint32_t stage[EXACT_CHUNK];
+    const uint32_t SUB = 1u << (a.nb_log2 - a.s_log2), t = threadIdx.x;
+    super_layout(a, sstart, cbeg, wsum);
+    uint32_t s, lo, hi;
+    if (!chunk2(a, sstart, cbeg, blockIdx.x, s, lo, hi)) return;
+    for (uint32_t j = t; j < SUB; j += EXACT_THREADS) {
+        cur[j] = a.h2[(uint64_t)blockIdx.x * SUB + j];
+        cnt[j] = 0;
+    }
+    __syncthreads();
+    const uint32_t nb_log2 = a.nb_log2;
+    staged_scatter(a.tmp, lo, hi - lo, a.parts, SUB, cnt, cur, stage, wsum,
+                   [=](uint32_t key) { return bucket_of(key, nb_log2) & (SUB - 1u); });
 }
 
 // One workgroup per bucket: count its keys in LDS, then filter, histogram and
@@ -740,7 +935,7 @@ __global__ __launch_bounds__(EXACT_THREADS) void part_count_kernel(ExactArgs a) 
                     go = false;
                 }
                 if (go) {
-                    uint32_t h = (uint32_t)mix64(key) & (SLOTS - 1u);
+                    uint32_t h = part_hash(key) & (SLOTS - 1u);
                     uint32_t probe = 0;
                     for (; probe < COUNT_PROBES; ++probe) {
                         uint32_t cur = tk[h];
@@ -850,13 +1045,17 @@ hipError_t launch_exact_partitioned(const ExactArgs& a, hipStream_t stream) {
     const uint32_t NB = 1u << a.nb_log2;
     const uint32_t wblocks = (a.n_windows + KEYS_WINDOWS - 1) / KEYS_WINDOWS;
     if (wblocks) hipLaunchKernelGGL(part_keys_kernel, dim3(wblocks), dim3(EXACT_THREADS), 0, stream, a);
-    const dim3 cols((NB + EXACT_THREADS - 1) / EXACT_THREADS), cols_groups(cols.x, a.n_groups);
-    hipLaunchKernelGGL(part_hist_kernel, dim3(a.n_chunks), dim3(EXACT_THREADS), 0, stream, a);
-    hipLaunchKernelGGL(part_colsum_kernel, cols_groups, dim3(EXACT_THREADS), 0, stream, a);
-    hipLaunchKernelGGL(part_groupscan_kernel, cols, dim3(EXACT_THREADS), 0, stream, a);
-    hipLaunchKernelGGL(part_bucketscan_kernel, dim3(1), dim3(1024), 0, stream, a);
-    hipLaunchKernelGGL(part_offsets_kernel, cols_groups, dim3(EXACT_THREADS), 0, stream, a);
-    hipLaunchKernelGGL(part_scatter_kernel, dim3(a.n_chunks), dim3(EXACT_THREADS), 0, stream, a);
+    const uint32_t S = 1u << a.s_log2;
+    if (a.s_log2 > a.nb_log2 || S > EXACT_MAX_SUPER || (NB >> a.s_log2) > EXACT_MAX_SUB || !a.n_chunks ||
+        a.n_chunks2 < a.n_chunks + S)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(part_hist1_kernel, dim3(a.n_chunks), dim3(EXACT_THREADS), 0, stream, a);
+    hipLaunchKernelGGL(part_scan1_kernel, dim3(S), dim3(EXACT_THREADS), 0, stream, a);
+    hipLaunchKernelGGL(part_scatter1_kernel, dim3(a.n_chunks), dim3(EXACT_THREADS), 0, stream, a);
+    hipLaunchKernelGGL(part_hist2_kernel, dim3(a.n_chunks2), dim3(EXACT_THREADS), 0, stream, a);
+    hipLaunchKernelGGL(part_scan2_kernel, dim3((S + EXACT_THREADS / 64 - 1) / (EXACT_THREADS / 64)), dim3(EXACT_THREADS),
+                       0, stream, a);
+    hipLaunchKernelGGL(part_scatter2_kernel, dim3(a.n_chunks2), dim3(EXACT_THREADS), 0, stream, a);
     if (hipError_t e = hipGetLastError()) return e;
     return launch_exact_part_count(a, stream);
 }

@@ -57,6 +57,7 @@ def main():
     print("  barrier    ", pct(us[:, 1] - pre))
     print("main len     ", pct(us[:, 2] - us[:, 1]))
     print("atomics len  ", pct(us[:, 3] - us[:, 2]))
+    print("main end     ", pct(us[:, 2]))
     print("end          ", pct(us[:, 3]))
     # per candidate group: end times (a group's waves only steal within the group)
     grp = raw[:, 6] >> 16
