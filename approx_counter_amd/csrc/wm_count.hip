@@ -203,7 +203,7 @@ __device__ __forceinline__ void tid_tail(TidNfa& s, uint32_t code, uint32_t nm, 
 template <int P>
 __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
     const uint32_t lane = threadIdx.x & 63u;
-    // Workgroup b serves block-queue b mod nqb (all its waves on one candidate
+    // Workgroup b serves one block-queue (all its waves on one candidate
     // group); its waves take the block-queue's AC_WAVES_PER_BLOCK sub-queues.
     const uint32_t wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t wave = (uint64_t)blockIdx.x * WAVES_PER_BLOCK + wib;
@@ -214,7 +214,28 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
     // Workgroups are dealt round-robin over the block-queues, so every
     // sub-queue is served by waves of every dispatch age (see the work-queue
     // comment below); q -> (segment, candidate group g, sub-queue j of that group).
-    const uint32_t q = (blockIdx.x % nqb) * WAVES_PER_BLOCK + wib, rank = blockIdx.x / nqb;
+    const uint32_t rank = blockIdx.x / nqb;
+#ifndef AC_PLAIN_DEAL  // A/B: the plain b mod nqb deal
+    // Rank r's workgroups are dealt to the block-queues rotated by shift(r):
+    // with a plain b mod nqb deal every workgroup a CU receives belongs to one
+    // block-queue, so each candidate group ran on a fixed slice of the chip
+    // and inherited its speed (stamps: group median ends 93-101 us, the same
+    // order run after run), with no stealing across groups to even it out.
+    // Rotated, a CU's workgroups come from all groups and every group runs on
+    // every XCD: group median ends 95.1-96.1 us, cfg2 kernel 109.6 -> 103.8 us
+    // (profiles/r01_kernel_log.md, round 2).
+    auto shift = [&](uint32_t r) { return (r + (r >> 3) * 4u) % nqb; };
+    const uint32_t bq = (blockIdx.x % nqb + shift(rank)) % nqb;
+    // workgroups dealt to block-queue qb (a complete rank gives each one; the
+    // partial last rank the blocks % nqb queues from shift(last) on)
+    auto wgs_of = [&](uint32_t qb) {
+        return blocks / nqb + ((qb + nqb - shift(blocks / nqb)) % nqb < blocks % nqb ? 1u : 0u);
+    };
+#else
+    const uint32_t bq = blockIdx.x % nqb;
+    auto wgs_of = [&](uint32_t qb) { return blocks / nqb + (qb < blocks % nqb ? 1u : 0u); };
+#endif
+    const uint32_t q = bq * WAVES_PER_BLOCK + wib;
     int si = 0;
 #pragma unroll
     for (int i = 1; i < AC_MAX_SEGS; ++i)
@@ -293,7 +314,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
     auto waves_in = [&](uint32_t jj) {  // waves dealt to sub-queue (g, jj): their first items are static
         const uint32_t qq = sg.queue_begin + g * sg.subq + jj;
         const uint32_t qb = qq / WAVES_PER_BLOCK;  // one wave of every workgroup dealt to block-queue qb
-        return blocks / nqb + (qb < blocks % nqb ? 1u : 0u);
+        return wgs_of(qb);
     };
 #ifndef AC_STRIDED_ITEMS
     // Sub-queue jj holds the contiguous items [first(jj), first(jj) + n_in(jj)):
@@ -526,8 +547,8 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
         asm volatile("" ::"v"(sink));
         // Workgroups serving group g: those dealt to its subq / WPB block-queues.
         const uint32_t qb0 = (sg.queue_begin + g * sg.subq) / WAVES_PER_BLOCK, nq = sg.subq / WAVES_PER_BLOCK;
-        const uint32_t rem = blocks % nqb;
-        const uint32_t n_wg = nq * (blocks / nqb) + (rem > qb0 ? min(rem - qb0, nq) : 0u);
+        uint32_t n_wg = 0;
+        for (uint32_t i = 0; i < nq; ++i) n_wg += wgs_of(qb0 + i);
         uint32_t* ticket = a.tickets + (uint64_t)(sg.ticket_begin + g) * AC_QUEUE_LINE;
         uint32_t t = 0;
         if (lane == 0) t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
