@@ -110,6 +110,8 @@ def load():
     L.ac_error_count_jobs_submit.restype = ctypes.c_int
     L.ac_check.argtypes = [vp, vp]
     L.ac_check.restype = ctypes.c_int
+    L.ac_stage_mode.argtypes = [vp]
+    L.ac_stage_mode.restype = ctypes.c_int
     _lib = L
     return L
 

@@ -236,6 +236,10 @@ class ApproxCounter:
         if st:
             check(st, self._h)
 
+    def stage_mode(self) -> int:
+        """ac_stage_mode: 1 zero-copy, 0 DMA, -1 not decided yet (count_jobs probes both first)."""
+        return int(self._L.ac_stage_mode(self._h))
+
     def check(self, stream=None) -> None:
         """ac_check: raise if a device launch since the last check skipped a malformed window."""
         check(self._L.ac_check(self._h, ctypes.c_void_p(stream or 0)), self._h)

@@ -89,6 +89,10 @@ struct ac_ctx {
         bool pending = false;
     } slot[2 * AC_STAGE_MAX_PARTS];
     uint32_t next_slot = 0;
+    // zero-copy vs DMA choice of the host-buffer stage (ac_stage_mode)
+    int zc_choice = -1;
+    uint32_t zc_probe = 0;
+    std::vector<double> zc_us[2];
 };
 
 namespace {
@@ -999,6 +1003,7 @@ struct JobPlan {
     size_t off_start[AC_MAX_JOBS] = {}, off_len[AC_MAX_JOBS] = {}, off_counts[AC_MAX_JOBS] = {};
     size_t off_err = 0, total = 0;
     int slot = 0;
+    bool zc = true;  // this call's transfer mode (zero-copy or DMA)
 };
 
 // AC_STAGE_PARTS (1 or 2, default 1) and AC_STAGE_SPLIT (first part's share of
@@ -1018,19 +1023,43 @@ int stage_parts() {
 // the contiguous item ranges of the work queues make each XCD read a slice of
 // the sample; it saves the DMA (1.2 MB, ~27 us at cfg2), the ~9 us
 // DMA-to-kernel dependency and the D2H blit.
-// AC_STAGE_HOSTALLOC=coherent|noncoherent: the pinned block's flags (A/B).
-bool stage_zerocopy() {
-    static const bool v = [] {
+// AC_STAGE_HOSTALLOC=coherent|noncoherent|wc: the pinned block's flags (A/B).
+int stage_zerocopy_env() {  // 1 / 0 forced by AC_STAGE_ZEROCOPY, -1 = automatic
+    static const int v = [] {
         const char* e = std::getenv("AC_STAGE_ZEROCOPY");
-        return !e || std::atoi(e) != 0;
+        return e ? (std::atoi(e) != 0 ? 1 : 0) : -1;
     }();
     return v;
+}
+// Zero-copy won on one box (the kernel took the same time as on device-resident
+// input) and lost badly on another (kernel + completion 217 vs 107 us, host
+// under other tenants' load), so an undecided context probes:
+// its synchronous calls alternate zero-copy / DMA until ZC_PROBES timed calls
+// of each (after one untimed, cold call of each), then keeps the faster by
+// median.  Submits use zero-copy until the choice is made.
+constexpr uint32_t ZC_PROBES = 4;
+bool stage_zerocopy(const ac_ctx* ctx, bool sync) {
+    if (stage_zerocopy_env() >= 0) return stage_zerocopy_env() == 1;
+    if (ctx->zc_choice >= 0) return ctx->zc_choice == 1;
+    return !sync || ctx->zc_probe % 2 == 0;
+}
+void stage_zerocopy_record(ac_ctx* ctx, bool zc, double us) {
+    if (stage_zerocopy_env() >= 0 || ctx->zc_choice >= 0) return;
+    if (ctx->zc_probe++ >= 2) ctx->zc_us[zc ? 1 : 0].push_back(us);
+    if (ctx->zc_us[0].size() >= ZC_PROBES && ctx->zc_us[1].size() >= ZC_PROBES) {
+        auto median = [](std::vector<double> v) {
+            std::sort(v.begin(), v.end());
+            return v[v.size() / 2];
+        };
+        ctx->zc_choice = median(ctx->zc_us[1]) <= median(ctx->zc_us[0]) ? 1 : 0;
+    }
 }
 unsigned stage_host_flags() {
     static const unsigned v = [] {
         const char* e = std::getenv("AC_STAGE_HOSTALLOC");
         if (e && std::string(e) == "coherent") return (unsigned)hipHostMallocCoherent;
         if (e && std::string(e) == "noncoherent") return (unsigned)hipHostMallocNonCoherent;
+        if (e && std::string(e) == "wc") return (unsigned)hipHostMallocWriteCombined;
         return (unsigned)hipHostMallocDefault;
     }();
     return v;
@@ -1150,7 +1179,7 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
         sl.pending = false;
     }
     if (!sl.ev) AC_HIP(ctx, hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming));
-    const bool zc = stage_zerocopy();
+    const bool zc = p.zc;
     if (sl.h_cap < p.total) {
         if (sl.h) (void)hipHostFree(sl.h);
         sl.h = nullptr;
@@ -1302,6 +1331,8 @@ ac_status ac_error_count_jobs(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint3
     }
     // Units are staged one after another on the host pool; a unit's DMA and
     // kernel run while the next one is packed.
+    const double t_call = now_us();
+    for (Unit& u : units) u.plan.zc = stage_zerocopy(u.c, true);
     for (size_t g = 0; g < units.size(); ++g) {
         Unit& u = units[g];
         AC_HIP(u.c, hipSetDevice(u.c->device));
@@ -1335,6 +1366,11 @@ ac_status ac_error_count_jobs(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint3
             for (uint32_t i = 0; i < jobs[j].n_kmers; ++i) jobs[j].counts[i] += hc[i];
         }
     }
+    if (first_err == AC_OK) {
+        const double us = now_us() - t_call;
+        for (size_t g = 0; g < units.size(); ++g)  // once per context (parts of one device share it)
+            if (g == 0 || units[g].c != units[g - 1].c) stage_zerocopy_record(units[g].c, units[g].plan.zc, us);
+    }
     if (g_trace.on) {
         g_trace.sum[7] += now_us() - t_sync;
         g_trace.cur[7] += now_us() - t_sync;
@@ -1361,7 +1397,14 @@ ac_status ac_error_count_jobs_submit(ac_ctx* ctx, uint32_t k, const ac_job* jobs
         p.lo[j] = 0;
         p.hi[j] = jobs[j].sample.n_windows;
     }
+    p.zc = stage_zerocopy(ctx, false);
     return stage_and_launch(ctx, k, jobs, p, (hipStream_t)hip_stream, d_counts);
+}
+
+int ac_stage_mode(const ac_ctx* ctx) {
+    if (!ctx) return -1;
+    if (stage_zerocopy_env() >= 0) return stage_zerocopy_env();
+    return ctx->zc_choice;
 }
 
 #ifdef AC_STAMPS

@@ -284,6 +284,15 @@ def main():
         geo = kc.last_launch()
         kc.close()
 
+    # ---- transfer path of the host-buffer stage (untimed): the library times its first
+    # synchronous calls with zero-copy and with DMA, alternately, and keeps the faster
+    # (ac_stage_mode; the winner depends on the host's PCIe / memory latency under load).
+    tune_calls = 0
+    while counter.stage_mode() < 0 and tune_calls < 32:
+        counter.count_jobs(args.k, jobs)
+        tune_calls += 1
+    stage_path = {1: "zero-copy", 0: "dma"}.get(counter.stage_mode(), "undecided")
+
     # ---- pipelined leg (informational, 1 GPU): host-buffer steps back to back, max(steps, 100)
     # of them.  Run before the stage: the zero-copy path itself runs ~8 % slower for its first
     # ~80 calls (profiles/r02_trace_percall2.log), so the stage is timed in steady state; one
@@ -315,7 +324,7 @@ def main():
     # ---- the stage (value): host Dna5 buffers -> host counts ---------------------------------
     if world == 1:
         def step():
-            counter.count_jobs(args.k, jobs)  # pack, one fused zero-copy launch, counts back (synchronous)
+            counter.count_jobs(args.k, jobs)  # pack, one fused launch, counts back (synchronous)
     else:
         def step():
             counter.submit_jobs(args.k, jobs, d_counts, stream=stream.cuda_stream)
@@ -378,9 +387,13 @@ def main():
             "data": DATA_NOTE,
             "config": {"workload": workload_name, "k": args.k, "sn": args.sn, "sl": args.sl, "lim": args.lim,
                        "candidates": n_c, "kmer_bp_per_step": units_job, "kmer_bp_per_rank_step": units_rank,
-                       "stage": "Dna5 host buffers -> pack (host pool, pinned) -> 1 fused zero-copy launch (both ends)"
-                                + (" -> RCCL all-reduce -> counts D2H" if world > 1 else
-                                   " -> counts written to pinned host memory by the kernel"),
+                       "stage": ("Dna5 host buffers -> pack (host pool, pinned) -> "
+                                 + ("1 fused launch reading the pinned block (zero-copy)" if stage_path == "zero-copy"
+                                    else "1 DMA in -> 1 fused launch") + " (both ends)"
+                                 + (" -> RCCL all-reduce -> counts D2H" if world > 1 else
+                                    (" -> counts written to pinned host memory by the kernel"
+                                     if stage_path == "zero-copy" else " -> 1 DMA of the counts back"))),
+                       "stage_path": stage_path,
                        "parallelism": (f"{args.scaling} window shards x{world}, "
                                        f"{'RCCL' if backend == 'nccl' else backend} all-reduce of counts")
                        if world > 1 else "1 GPU"},
@@ -389,6 +402,9 @@ def main():
             d = np.diff(np.array([t0] + marks)) * 1e3
             out["step_ms"] = {"min": float(d.min()), "p50": float(np.median(d)), "max": float(d.max())}
         out["stage_cold_call_ms"] = cold_ms
+        out["stage_path_choice"] = {"path": stage_path, "untimed_calls": tune_calls,
+                                    "note": "zero-copy vs DMA chosen by the library from its first synchronous "
+                                            "calls, timed both ways (ac_stage_mode)"}
         if kern_ms is not None:
             ops = OPS_PER_BASE_WORD / P * units_rank  # algorithmic lane-ops per launch (this rank)
             achieved = ops / (kern_ms * 1e-3)

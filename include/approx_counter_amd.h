@@ -259,6 +259,16 @@ ac_status ac_error_count_jobs_submit(ac_ctx* ctx, uint32_t k, const ac_job* jobs
 ac_status ac_check(ac_ctx* ctx, void* hip_stream);
 
 /*
+ * How ac_error_count_jobs moves the packed inputs (no reference counterpart):
+ * 1 = zero-copy (the kernel reads the pinned staging block over PCIe), 0 = one
+ * DMA in and one back, -1 = not decided yet.  Unless AC_STAGE_ZEROCOPY=1/0
+ * forces one, a context times its first synchronous calls both ways (they
+ * alternate; 10 calls) and keeps the faster: which one wins depends on the
+ * host (PCIe / host-memory latency under other load), not on the workload.
+ */
+int ac_stage_mode(const ac_ctx* ctx);
+
+/*
  * Launch geometry actually used for the last device launch of ctx (for
  * measurement): waves launched, windows per wave, candidate groups.
  */

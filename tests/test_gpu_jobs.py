@@ -173,3 +173,24 @@ def test_multi_context_shuffled_overlapping_windows():
     for shards in (2, 3, 5):
         with ac.ApproxCounter(n_gpus=shards) as multi:
             assert np.array_equal(multi.count(16, kmers, shuffled), exp), shards
+
+
+@pytest.mark.skipif("AC_STAGE_ZEROCOPY" in os.environ, reason="transfer path forced by the environment")
+def test_transfer_path_probe_both_ways_bit_exact():
+    """A fresh context alternates zero-copy and DMA over its first synchronous calls
+    (ac_stage_mode -1 until then), keeps the faster, and every call is bit-exact."""
+    a = cases.planted_case(31, 16, 200, 300, win_len=(0, 150), p_n=0.02)
+    b = cases.planted_case(32, 16, 90, 260, win_len=(80, 120))
+    exp = [oracle.count_myers(16, *a), oracle.count_myers(16, *b)]
+    c = ac.ApproxCounter(0)
+    try:
+        assert c.stage_mode() == -1
+        jobs = ac.Jobs([(a[0], _shuffled_sample(a[1], 5)), (b[0], ac.Dna5Sample.from_windows(b[1]))])
+        modes = []
+        for _ in range(12):
+            got = c.count_jobs(16, jobs)
+            assert np.array_equal(got[0], exp[0]) and np.array_equal(got[1], exp[1])
+            modes.append(c.stage_mode())
+        assert modes[8] == -1 and modes[9] in (0, 1) and len(set(modes[9:])) == 1, modes
+    finally:
+        c.close()
