@@ -264,6 +264,9 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
     const uint32_t* g_codes = (const uint32_t*)g_codes_g;
     const uint32_t* g_nmask = (const uint32_t*)g_nmask_g;
     const uint32_t m = a.m;
+    // An occurrence with <= 2 edits spans >= m - 2 bases: none ends in a window's
+    // first m - 3 bases, whose hit accumulation the first block skips (12 of them).
+    const bool skip_first = m >= 15u;
 
     uint32_t cand[P];
 #pragma unroll
@@ -448,7 +451,16 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
         };
         // step 1 (after block 0): the claim's result -> the next item's descriptor,
         // or the next window's first words
-        if (nfull0 >= 2u) block32(f0, 0u);
+        if (nfull0 >= 2u) {
+            if (skip_first) {  // bases 0-31, no hit accumulation over bases 0-11 (k >= 15)
+                const uint32_t code = __builtin_amdgcn_readlane(f0, 0u);
+                const uint32_t code2 = __builtin_amdgcn_readlane(f0, 1u);
+                const uint32_t nm = __builtin_amdgcn_readlane(f0, 16u);
+                tid_block32_first<P, TID_EB0>(s, code, code2, nm, eb);
+            } else {
+                block32(f0, 0u);
+            }
+        }
         if (last) {
             nitem = __builtin_amdgcn_readfirstlane(item_of(jc_waves + __builtin_amdgcn_readfirstlane(pending)));
             if (nitem < n_items) {

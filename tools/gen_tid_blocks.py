@@ -29,6 +29,7 @@ import sys
 AHEAD = 4  # LDS reads in flight ahead of the base being computed
 WAIT_PAIR = True  # one s_waitcnt per two bases (the SALU is the CU-shared resource)
 NE = AHEAD + 3  # rotating ~Eq registers (base i's is read by rows 0-2 at steps i..i+2)
+FIRST_SKIP = 12  # bases of a window's start with no possible occurrence end (k >= 15: k - 3 >= 12)
 
 
 def m0_setup(j, with_n, eb0):
@@ -46,7 +47,7 @@ def m0_setup(j, with_n, eb0):
     return s
 
 
-def block(nb, with_n, eb0):
+def block(nb, with_n, eb0, skip=0):
     """Skewed (software-pipelined) schedule: step s runs row 0 of base s, row 1 of
     base s-1 and row 2 of base s-2 -- three independent dependency chains per wave.
     Row r of base i needs row r of base i-1 and row r-1 of bases i-1 and i, all
@@ -96,6 +97,8 @@ def block(nb, with_n, eb0):
             if r > 0:
                 L.append(f"v_lshrrev_b32 {T(r, i)}, %[P], {D(r, i)}")
         for r, i in rows:
+            if i < skip:  # a window's first bases: no occurrence can end there (skip <= k - 3)
+                continue
             if i % 2 == 1:
                 L.append(f"v_bitop3_b32 %[a{r}], %[a{r}], {D(r, i - 1)}, {D(r, i)} bitop3:0x80")
             elif i == nb - 1:  # unpaired last base (odd nb)
@@ -107,18 +110,18 @@ def block(nb, with_n, eb0):
     return L
 
 
-def body(nb, eb0):
+def body(nb, eb0, skip=0):
     """Whole statement text: N-free chunks take the fast path, chunks with an N
     the N-aware one (same registers, so hipcc sees one statement)."""
     L = ["s_mov_b32 %[keep], m0", "s_cmp_lg_u32 %[nm], 0", "s_cbranch_scc1 .Lnpath%="]
-    L += block(nb, False, eb0)
+    L += block(nb, False, eb0, skip)
     L += ["s_branch .Lend%=", ".Lnpath%=:"]
-    L += block(nb, True, eb0)
+    L += block(nb, True, eb0, skip)
     L += [".Lend%=:", "s_mov_b32 m0, %[keep]"]
     return "\n".join(f'            "{ln}\\n\\t"' for ln in L)
 
 
-def emit(nb):
+def emit(nb, skip=0, name=None):
     extra = [f"code{i}" for i in range(2, (nb + 15) // 16 + 1)]
     code2_in = "".join(f', [{c}] "s"({c})' for c in extra)
     code2_arg = "".join(f", uint32_t {c}" for c in extra)
@@ -133,16 +136,16 @@ def emit(nb):
             : [code] "s"(code){code2_in}, [nm] "s"(nm), [eb] "s"(eb), [P] "n"(P)
             : "memory", "scc");"""
     return f"""template <int P, bool EB0>
-__device__ __forceinline__ void tid_block{nb}(TidNfa& s, uint32_t code{code2_arg}, uint32_t nm, uint32_t eb) {{
+__device__ __forceinline__ void {name or f"tid_block{nb}"}(TidNfa& s, uint32_t code{code2_arg}, uint32_t nm, uint32_t eb) {{
     uint32_t {decl};
     uint32_t t, keep;
     if constexpr (EB0) {{
         asm volatile(
-{body(nb, True)}
+{body(nb, True, skip)}
 {operands}
     }} else {{
         asm volatile(
-{body(nb, False)}
+{body(nb, False, skip)}
 {operands}
     }}
 }}
@@ -163,6 +166,11 @@ def main():
     ]
     for nb in (32, 16, 8, 4, 2, 1):  # 64-base blocks measured no faster (r01_kernel_log.md)
         parts.append(emit(nb))
+    # A window's first 32 bases without the hit accumulation of bases 0-11: an
+    # occurrence with <= 2 edits spans >= k - 2 bases, so none ends before base
+    # k - 3 (valid for k >= 15; wm_count.hip picks it then).
+    parts.append("// tid_block32 for a window's first 32 bases, k >= 15: no hit accumulation over bases 0-11.")
+    parts.append(emit(32, skip=FIRST_SKIP, name="tid_block32_first"))
     with open(OUT, "w") as fh:
         fh.write("\n".join(parts))
     print("wrote", OUT)
