@@ -190,7 +190,8 @@ float complexity(uint64_t kmer, uint32_t k) {
 
 ac_status check_sample(ac_ctx* ctx, const ac_windows* s) {
     if (!s) return fail(ctx, AC_ERR_INVALID, "sample is NULL");
-    if (s->n_bases % 32) return fail(ctx, AC_ERR_INVALID, "sample n_bases must be a multiple of 32");
+    if (s->n_bases % 32 || s->n_bases >= AC_MAX_IMAGE_BASES)
+        return fail(ctx, AC_ERR_INVALID, "sample n_bases must be a multiple of 32 below 2^34");
     if (s->n_windows && (!s->codes || !s->nmask || !s->start || !s->length))
         return fail(ctx, AC_ERR_INVALID, "sample has a NULL array");
     return AC_OK;
@@ -244,7 +245,8 @@ ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hi
         if (s.n_kmers && s.sample.n_windows &&
             (!s.sample.codes || !s.sample.nmask || !s.sample.start || !s.sample.length))
             return fail(ctx, AC_ERR_INVALID, "segment sample has a NULL array");
-        if (s.sample.n_bases % 32) return fail(ctx, AC_ERR_INVALID, "sample n_bases must be a multiple of 32");
+        if (s.sample.n_bases % 32 || s.sample.n_bases >= AC_MAX_IMAGE_BASES)
+            return fail(ctx, AC_ERR_INVALID, "sample n_bases must be a multiple of 32 below 2^34");
         const uint32_t groups = (s.n_kmers + cpw - 1) / cpw;
         items += (uint64_t)groups * s.sample.n_windows;
     }
@@ -490,7 +492,8 @@ ac_status error_count_one(ac_ctx* ctx, uint32_t k, const uint64_t* kmers, uint32
     if (n_kmers == 0) return AC_OK;
     if (!kmers || !counts || !sample) return fail(ctx, AC_ERR_INVALID, "NULL argument");
     const ac_windows& s = *sample;
-    if (s.n_bases % 32) return fail(ctx, AC_ERR_INVALID, "sample n_bases must be a multiple of 32");
+    if (s.n_bases % 32 || s.n_bases >= AC_MAX_IMAGE_BASES)
+        return fail(ctx, AC_ERR_INVALID, "sample n_bases must be a multiple of 32 below 2^34");
     if (s.n_windows && (!s.codes || !s.nmask || !s.start || !s.length))
         return fail(ctx, AC_ERR_INVALID, "sample has a NULL array");
     if (ac_status st = check_layout(ctx, s)) return st;

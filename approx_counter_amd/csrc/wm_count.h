@@ -6,6 +6,9 @@
 #define AC_MAX_SEGS 4    // segments fused into one launch (start + end ends, shards)
 #define AC_QUEUE_LINE 32  // u32 per queue counter: one 128-B line each (no false sharing between counters)
 #define AC_MAX_PACK 4    // candidates interleaved per 32-bit lane word (P = min(32/k, 4))
+// Largest window image (bases, exclusive): the count kernel reads it through buffer descriptors whose
+// byte offsets and sizes are 32-bit (2 bits per base: 2^34 bases = 4 GiB of code words).
+#define AC_MAX_IMAGE_BASES (1ull << 34)
 #ifndef AC_WAVES_PER_BLOCK
 #define AC_WAVES_PER_BLOCK 4  // waves per workgroup, all on one candidate group (shared ~Eq table, counts summed in LDS)
 #endif

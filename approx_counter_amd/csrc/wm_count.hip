@@ -153,19 +153,62 @@ struct TidTable {
     uint32_t e[5 * 64];
 };
 
-// Lane `lane`'s word of window bases [sb, sb + SEG): lanes 0-15 the 16 code
-// words, lanes 16-23 the 8 N-mask words.  One unconditional load per lane with
-// the index clamped to the window's last word (always inside the image): a word
-// past the window is never read as text (the chunk loop stops at the window
-// length), and a branch-free load keeps hipcc from waiting on it before the
-// window that uses it.
-__device__ __forceinline__ uint32_t tid_fetch(const uint32_t* __restrict__ codes, const uint32_t* __restrict__ nmask,
-                                              uint32_t len, uint32_t sb, uint32_t lane) {
-    const bool is_code = lane < 16u;
-    const uint32_t ci = min((sb >> 4) + lane, (len - 1u) >> 4);
-    const uint32_t ni = min((sb >> 5) + ((lane - 16u) & 7u), (len - 1u) >> 5);
-    const uint32_t* p = is_code ? codes + ci : nmask + ni;
-    return *p;
+// Lane `lane`'s word of window bases [sb, sb + 256): lanes 0-15 the 16 code
+// words, lanes 16-23 the 8 N-mask words, with the index clamped to the window's
+// last word (always inside the image): a word past the window is never read as
+// text (the chunk loop stops at the window length), and a branch-free load
+// keeps hipcc from waiting on it before the window that uses it.
+// Code lanes and N-mask lanes load through buffer descriptors of the
+// segment's two arrays (SGPRs) under complementary exec masks; the byte offset
+// is the window's (an SGPR) plus a per-lane constant (lane_off = 4 * word
+// within the segment).  The descriptors' range check (num_records = the
+// array's bytes, voffset included) returns 0 for a word past the image, so no
+// clamp: words past the window are never read as text (the chunk loop stops
+// at the window length).  One v_add per lane group and window.
+struct Image {
+    __amdgpu_buffer_rsrc_t codes, nmask;
+};
+// The two halves land in separate registers (merged by the consumer, tid_word):
+// one register for both would make the second load's address wait for the
+// first load to complete (the register is still being written for the other lanes).
+struct Fetch {
+    uint32_t c, n;
+};
+__device__ __forceinline__ void tid_fetch(Fetch& f, const Image& im, uint64_t pos, uint32_t lane, uint32_t lane_off) {
+    // (the two asm markers differ, so hipcc cannot merge the loads into one through a per-lane
+    // selected descriptor, which it would wrap in a waterfall loop)
+    if (lane < 16u) {
+        f.c = __builtin_amdgcn_raw_buffer_load_b32(im.codes, (uint32_t)(pos >> 2) + lane_off, 0, 0);
+        asm volatile("; code words");
+    } else {
+        f.n = __builtin_amdgcn_raw_buffer_load_b32(im.nmask, (uint32_t)(pos >> 3) + lane_off, 0, 0);
+        asm volatile("; N-mask words");
+    }
+}
+__device__ __forceinline__ uint32_t tid_word(const Fetch& f, uint32_t lane) { return lane < 16u ? f.c : f.n; }
+
+// start % 32 == 0 && length <= n_bases && start <= n_bases - length, on the
+// scalar unit (hipcc compares 64-bit values with VALU ops), written so that no
+// sum wraps: a start near 2^64 must not pass.
+__device__ __forceinline__ uint32_t window_valid(uint64_t base, uint32_t len, uint64_t nb) {
+#ifndef AC_VALU_VALID
+    uint32_t bad, t0, t1;
+    asm("s_sub_u32 %[t0], %[nbl], %[len]\n\t"
+        "s_subb_u32 %[t1], %[nbh], 0\n\t"  // scc: n_bases < length
+        "s_cselect_b32 %[bad], 1, 0\n\t"
+        "s_sub_u32 %[t0], %[t0], %[bl]\n\t"
+        "s_subb_u32 %[t1], %[t1], %[bh]\n\t"  // scc: n_bases - length < start
+        "s_cselect_b32 %[bad], 1, %[bad]\n\t"
+        "s_and_b32 %[t0], %[bl], 31\n\t"  // scc: misaligned start
+        "s_cselect_b32 %[bad], 1, %[bad]"
+        : [bad] "=&s"(bad), [t0] "=&s"(t0), [t1] "=&s"(t1)
+        : [nbl] "s"((uint32_t)nb), [nbh] "s"((uint32_t)(nb >> 32)), [len] "s"(len), [bl] "s"((uint32_t)base),
+          [bh] "s"((uint32_t)(base >> 32))
+        : "scc");
+    return bad ^ 1u;
+#else
+    return !(base & 31u) && len <= nb && base <= nb - len;
+#endif
 }
 
 // The workgroup's waves serve one candidate group and share one table, the
@@ -246,13 +289,18 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
     // sub-queues lie in one group.
     const uint32_t g = ql / sg.subq, j = ql % sg.subq;
     // The segment's arrays, pinned in SGPRs for the whole launch: read through the `sg` reference hipcc reloaded them from
-    // the kernel arguments in every window, each load waited for on the spot.
-    // (codes / nmask kept as global-address-space pointers: an opaque generic
-    // pointer would make the window fetches flat loads, which also count in
-    // lgkmcnt and so would be waited for by the NFA blocks' LDS waits)
-    typedef const __attribute__((address_space(1))) uint32_t* gu32p;
-    gu32p g_codes_g = (gu32p)sg.codes;
-    gu32p g_nmask_g = (gu32p)sg.nmask;
+    // the kernel arguments in every window, each load waited for on the spot.  The image through buffer
+    // descriptors (range-checked fetches, tid_fetch); images are < 2^34 bases (checked on the host), so
+    // every byte offset fits 32 bits.
+    // (inputs pinned in SGPRs by an asm operand: hipcc must see them wave-uniform, or it wraps every
+    // fetch in a waterfall loop)
+    const uint32_t* codes_p = sg.codes;
+    const uint32_t* nmask_p = sg.nmask;
+    uint32_t code_bytes = (uint32_t)(sg.n_bases >> 2), nmask_bytes = (uint32_t)(sg.n_bases >> 3);
+    asm volatile("" : "+s"(codes_p), "+s"(nmask_p), "+s"(code_bytes), "+s"(nmask_bytes));
+    Image im;
+    im.codes = __builtin_amdgcn_make_buffer_rsrc((void*)codes_p, 0, (int)code_bytes, 0x00020000);
+    im.nmask = __builtin_amdgcn_make_buffer_rsrc((void*)nmask_p, 0, (int)nmask_bytes, 0x00020000);
     const uint64_t* g_start = sg.start;
     const uint32_t* g_length = sg.length;
     uint64_t g_nbases = sg.n_bases;
@@ -260,9 +308,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
     // pointer would turn the claim into a flat atomic, which also counts in
     // lgkmcnt and so would be waited for by the NFA blocks' LDS waits)
     uint32_t* g_queue = a.queue + ((uint64_t)a.bank * a.qstride + sg.queue_begin + g * sg.subq) * AC_QUEUE_LINE;
-    asm volatile("" : "+s"(g_codes_g), "+s"(g_nmask_g), "+s"(g_start), "+s"(g_length), "+s"(g_nbases));
-    const uint32_t* g_codes = (const uint32_t*)g_codes_g;
-    const uint32_t* g_nmask = (const uint32_t*)g_nmask_g;
+    asm volatile("" : "+s"(g_start), "+s"(g_length), "+s"(g_nbases));
     const uint32_t m = a.m;
     // An occurrence with <= 2 edits spans >= m - 2 bases: none ends in a window's
     // first m - 3 bases, whose hit accumulation the first block skips (12 of them).
@@ -383,15 +429,16 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
 
     // Window pipeline: the next window's first segment is fetched while the current one is counted.
     // (written so that no sum wraps: a start near 2^64 must not pass)
-    auto valid = [&](uint64_t base, uint32_t len) { return !(base & 31u) && len <= g_nbases && base <= g_nbases - len; };
+    auto valid = [&](uint64_t base, uint32_t len) { return window_valid(base, len, g_nbases) != 0u; };
     // an empty window reads no word (its start may be the image's end)
     auto fetchable = [&](uint64_t base, uint32_t len) { return len != 0u && valid(base, len); };
     uint64_t nbase = 0;
     uint32_t nlen = 0;
-    uint32_t nf = 0;
+    Fetch nf = {0u, 0u};
+    const uint32_t lane_off = (lane < 16u ? lane : (lane - 16u) & 7u) << 2;  // this lane's word of a segment, in bytes
     if (item < n_items) {
         load_desc(g_start, g_length, w, nbase, nlen);
-        if (fetchable(nbase, nlen)) nf = tid_fetch(g_codes + (nbase >> 4), g_nmask + (nbase >> 5), nlen, 0, lane);
+        if (fetchable(nbase, nlen)) tid_fetch(nf, im, nbase, lane, lane_off);
     }
 
     // ~Eq table, built by wave 0 of the workgroup (the waves share the
@@ -426,7 +473,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
         const uint32_t len = nlen;
         // Wait for this window's words here, before the next window's fetch is
         // issued: inside the chunk loop hipcc would otherwise wait for both.
-        uint32_t f0 = nf;
+        uint32_t f0 = tid_word(nf, lane);
         asm volatile("" : "+v"(f0));
         const uint32_t wn = w + 1;
         const bool last = wn >= item_end;  // the item's last window: claim the next item
@@ -441,8 +488,6 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
         const uint32_t nb0 = ok ? min(SEG, len) : 0u;
         const uint32_t nfull0 = nb0 >> 4;
         TidNfa s = {~0u, d1_init, d2_init, ~0u >> P, d1_init >> P, d2_init >> P, ~0u, d1_init, d2_init};
-        const uint32_t* __restrict__ codes = g_codes + (base >> 4);
-        const uint32_t* __restrict__ nmask = g_nmask + (base >> 5);
         auto block32 = [&](uint32_t f, uint32_t ch) __attribute__((always_inline)) {
             const uint32_t code = __builtin_amdgcn_readlane(f, ch);
             const uint32_t code2 = __builtin_amdgcn_readlane(f, ch + 1u);
@@ -467,12 +512,12 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
                 load_desc(g_start, g_length, nitem * chunk, nbase, nlen);
             }
         } else if (fetchable(nbase, nlen)) {
-            nf = tid_fetch(g_codes + (nbase >> 4), g_nmask + (nbase >> 5), nlen, 0, lane);
+            tid_fetch(nf, im, nbase, lane, lane_off);
         }
         // step 2 (after block 1): the next item's first words
         if (nfull0 >= 4u) block32(f0, 2u);
         if (last && nitem < n_items && fetchable(nbase, nlen))
-            nf = tid_fetch(g_codes + (nbase >> 4), g_nmask + (nbase >> 5), nlen, 0, lane);
+            tid_fetch(nf, im, nbase, lane, lane_off);
         if (ok) {
             auto segment = [&](uint32_t f, uint32_t sb, uint32_t ch) __attribute__((always_inline)) {
                 const uint32_t nb = min(SEG, len - sb);
@@ -491,7 +536,9 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
             };
             segment(f0, 0u, nfull0 >= 4u ? 4u : (nfull0 >= 2u ? 2u : 0u));
             for (uint32_t sb = SEG; sb < len; sb += SEG) {  // windows longer than one segment
-                uint32_t f = tid_fetch(codes, nmask, len, sb, lane);
+                Fetch ff;
+                tid_fetch(ff, im, base + sb, lane, lane_off);
+                uint32_t f = tid_word(ff, lane);
                 asm volatile("" : "+v"(f));
                 segment(f, sb, 0u);
             }
@@ -510,7 +557,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
                 if (item < n_items) {
                     load_desc(g_start, g_length, item * chunk, nbase, nlen);
                     if (fetchable(nbase, nlen))
-                        nf = tid_fetch(g_codes + (nbase >> 4), g_nmask + (nbase >> 5), nlen, 0, lane);
+                        tid_fetch(nf, im, nbase, lane, lane_off);
                 }
             }
             if (item < n_items) {

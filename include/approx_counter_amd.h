@@ -55,7 +55,7 @@ typedef struct ac_ctx ac_ctx;
  *           start[i] % 32 == 0 (each window begins on a 32-base boundary)
  *   length: window length in bases (sl for a start window, sl+1 for an end
  *           window, approx_counter.cpp:463/466); 0 is allowed
- *   n_bases: size of the image in bases, a multiple of 32
+ *   n_bases: size of the image in bases, a multiple of 32 below 2^34
  * All pointers are host pointers for ac_error_count() and device pointers for
  * the *_device entry points.
  */

@@ -194,3 +194,19 @@ def test_transfer_path_probe_both_ways_bit_exact():
         assert modes[8] == -1 and modes[9] in (0, 1) and len(set(modes[9:])) == 1, modes
     finally:
         c.close()
+
+
+def test_image_size_limit_rejected(counter):
+    """The count kernel addresses the image through 32-bit buffer offsets: a device
+    segment claiming 2^34 bases or more is refused up front (AC_ERR_INVALID), never
+    launched."""
+    kmers, wins = cases.planted_case(22, 16, 100, 10, win_len=(100, 101))
+    seg = ac.DeviceSegment.upload(kmers, ac.pack_windows(wins))
+    seg.n_bases = 1 << 34
+    with pytest.raises(ac.ApproxCounterError) as ei:
+        counter.count_device(16, [seg])
+    assert ei.value.status == 1 and "2^34" in str(ei.value)
+    seg.n_bases = ac.pack_windows(wins).n_bases  # the context still counts afterwards
+    counter.count_device(16, [seg])
+    counter.check()
+    assert np.array_equal(seg.counts_numpy(), oracle.count_myers(16, kmers, wins, 16))
