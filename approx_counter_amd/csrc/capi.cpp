@@ -1041,6 +1041,7 @@ int stage_zerocopy_env() {  // 1 / 0 forced by AC_STAGE_ZEROCOPY, -1 = automatic
 // of each (after one untimed, cold call of each), then keeps the faster by
 // median.  Submits use zero-copy until the choice is made.
 constexpr uint32_t ZC_PROBES = 4;
+constexpr uint64_t ZC_MAX_IMAGE_BYTES = 24ull << 20;  // 8 XCDs x 3 MB of L2 for their slices
 bool stage_zerocopy(const ac_ctx* ctx, bool sync) {
     if (stage_zerocopy_env() >= 0) return stage_zerocopy_env() == 1;
     if (ctx->zc_choice >= 0) return ctx->zc_choice == 1;
@@ -1169,6 +1170,16 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
         off = align256(off + sizeof(uint32_t) * jobs[j].n_kmers);
     }
     p.total = off;
+    // Zero-copy re-reads the image over PCIe once per candidate group whenever an XCD's L2
+    // (4 MB) cannot hold its slice of it: at cfg4 (96 MB) the zero-copy stage ran 15.8-18 ms
+    // against 13.7 ms with the DMA (profiles/r02_stage_ab_cfg4.log).  A call whose image
+    // exceeds ZC_MAX_IMAGE_BYTES takes the DMA path, and an undecided context decides DMA.
+    uint64_t image_bytes = 0;
+    for (uint32_t j = 0; j < p.n; ++j) image_bytes += p.n_bases[j] / 8 * 3;  // 2-bit codes + N bitmap
+    if (p.zc && image_bytes > ZC_MAX_IMAGE_BYTES && stage_zerocopy_env() < 0) {
+        p.zc = false;
+        if (ctx->zc_choice < 0) ctx->zc_choice = 0;
+    }
     // The slot: wait until the launch that last read it has finished, grow it.
     if (d_counts) {
         p.slot = AC_STAGE_MAX_PARTS + (int)ctx->next_slot;
