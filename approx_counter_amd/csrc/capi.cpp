@@ -1224,10 +1224,13 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
                                (uint32_t*)(h + p.off_nmask[j]), (uint64_t*)(h + p.off_start[j]) + r,
                                (uint32_t*)(h + p.off_len[j]) + r);
     };
+    char* d = zc ? (char*)sl.hd : (char*)sl.d;
+    // In both modes the kernel writes the error word and the counts straight into the pinned
+    // block (hd), so no copy comes back (profiles/r02_stage_dma_back_ab.log).
+    char* hd = (char*)sl.hd;
     pool.run((uint32_t)tasks.size(), pack);
     mark(2);
-    char* d = zc ? (char*)sl.hd : (char*)sl.d;
-    if (!zc) AC_HIP(ctx, hipMemcpyAsync(d, h, p.off_err + sizeof(uint32_t), hipMemcpyHostToDevice, stream));
+    if (!zc) AC_HIP(ctx, hipMemcpyAsync(d, h, p.off_err, hipMemcpyHostToDevice, stream));
     mark(3);
     ac_segment segs[AC_MAX_JOBS];
     uint64_t cbase = 0;
@@ -1239,7 +1242,7 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
         g.sample = ac_windows{(const uint32_t*)(d + p.off_codes[j]), (const uint32_t*)(d + p.off_nmask[j]),
                               (const uint64_t*)(d + p.off_start[j]), (const uint32_t*)(d + p.off_len[j]), nw,
                               p.n_bases[j]};
-        g.counts = d_counts ? d_counts + cbase : (uint32_t*)(d + p.off_counts[j]);
+        g.counts = d_counts ? d_counts + cbase : (uint32_t*)(hd + p.off_counts[j]);
         cbase += jobs[j].n_kmers;
     }
     // the synchronous path reads the error word back with the counts; a
@@ -1250,12 +1253,10 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
         if (!ctx->resident[P]) AC_HIP(ctx, acamd::resident_waves(P, ctx->cu_count, &ctx->resident[P]));
         cap = ctx->resident[P] / wave_div;
     }
-    if (ac_status st = launch(ctx, k, segs, p.n, stream, true, d_counts ? nullptr : (uint32_t*)(d + p.off_err), part,
+    if (ac_status st = launch(ctx, k, segs, p.n, stream, true, d_counts ? nullptr : (uint32_t*)(hd + p.off_err), part,
                               cap))
         return st;
     mark(4);
-    if (!d_counts && !zc)  // the way back: error word + counts
-        AC_HIP(ctx, hipMemcpyAsync(h + p.off_err, d + p.off_err, p.total - p.off_err, hipMemcpyDeviceToHost, stream));
     mark(5);
     AC_HIP(ctx, hipEventRecord(sl.ev, stream));
     sl.pending = true;

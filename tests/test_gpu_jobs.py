@@ -210,3 +210,27 @@ def test_image_size_limit_rejected(counter):
     counter.count_device(16, [seg])
     counter.check()
     assert np.array_equal(seg.counts_numpy(), oracle.count_myers(16, kmers, wins, 16))
+
+
+@pytest.mark.skipif("AC_STAGE_ZEROCOPY" in os.environ, reason="transfer path forced by the environment")
+def test_large_image_takes_dma_path():
+    """An image above the zero-copy limit (24 MB packed; zero-copy would re-read it over
+    PCIe per candidate group) is staged by DMA: a fresh context decides DMA at once
+    (ac_stage_mode 0), the kernel writes the counts into the pinned block, bit-exact."""
+    rng = np.random.default_rng(7)
+    n, L = 600_000, 100
+    win = rng.integers(0, 4, size=(n, L), dtype=np.uint8)
+    win[rng.integers(0, n, size=2000), rng.integers(0, L, size=2000)] = 4  # a few N
+    picks = rng.integers(0, n, size=12)
+    kmers = np.array([int(sum(int(b) << (2 * (15 - i)) for i, b in enumerate(win[p, 20:36]))) for p in picks],
+                     dtype=np.uint64)
+    sample = ac.Dna5Sample(win.reshape(-1), np.arange(n, dtype=np.uint64) * np.uint64(L),
+                           np.full(n, L, dtype=np.uint32))
+    c = ac.ApproxCounter(0)
+    try:
+        assert c.stage_mode() == -1
+        got = c.count_jobs(16, [(kmers, sample)])[0]
+        assert c.stage_mode() == 0
+    finally:
+        c.close()
+    assert np.array_equal(got, oracle.count_myers(16, kmers, win, 16))
