@@ -91,7 +91,8 @@ struct ac_ctx {
     uint32_t next_slot = 0;
     // zero-copy vs DMA choice of the host-buffer stage (ac_stage_mode)
     int zc_choice = -1;
-    uint32_t zc_probe = 0;
+    int zc_last = -1;  // 0: the last synchronous call was too large for zero-copy (ac_stage_mode)
+    uint32_t zc_probe = 0, zc_calls = 0;
     std::vector<double> zc_us[2];
 };
 
@@ -1007,6 +1008,7 @@ struct JobPlan {
     size_t off_err = 0, total = 0;
     int slot = 0;
     bool zc = true;  // this call's transfer mode (zero-copy or DMA)
+    bool zc_eligible = true;  // false: the image is too large for zero-copy (DMA, not measured)
 };
 
 // AC_STAGE_PARTS (1 or 2, default 1) and AC_STAGE_SPLIT (first part's share of
@@ -1036,24 +1038,39 @@ int stage_zerocopy_env() {  // 1 / 0 forced by AC_STAGE_ZEROCOPY, -1 = automatic
 }
 // Zero-copy won on one box (the kernel took the same time as on device-resident
 // input) and lost badly on another (kernel + completion 217 vs 107 us, host
-// under other tenants' load), so an undecided context probes:
-// its synchronous calls alternate zero-copy / DMA until ZC_PROBES timed calls
-// of each (after one untimed, cold call of each), then keeps the faster by
-// median.  Submits use zero-copy until the choice is made.
+// under other tenants' load), and on one box it turned slow in
+// the middle of a run (cfg3: 9.9 ms per step after fast probes), so a context
+// keeps measuring: its synchronous calls alternate zero-copy / DMA until
+// ZC_PROBES timed calls of each (after one untimed, cold call of each), it then
+// uses the faster by median of each path's last ZC_PROBES calls, and every
+// ZC_REPROBE-th call takes the other path to refresh that path's figures.
+// Submits use zero-copy until a choice exists.  Calls whose zero-copy would
+// move too much over PCIe take the DMA path and are not measured (below).
 constexpr uint32_t ZC_PROBES = 4;
-constexpr uint64_t ZC_MAX_IMAGE_BYTES = 24ull << 20;  // 8 XCDs x 3 MB of L2 for their slices
-bool stage_zerocopy(const ac_ctx* ctx, bool sync) {
+constexpr uint32_t ZC_REPROBE = 64;
+// Zero-copy reads the image once per candidate group wherever an XCD's L2 does
+// not keep it (on the slow boxes nothing is kept: ~55 GB/s of PCIe reads).  Up
+// to ZC_MAX_PCIE_BYTES of image x groups the measurements above decide (cfg2 6
+// MB, cfg5 100 MB, cfg3 150 MB: zero-copy 3.26-3.39 vs DMA 3.47-3.59 ms per cfg3
+// step on a fast box, profiles/r02_stage_auto_cfg3.log); beyond it (cfg4: 390
+// MB; zero-copy 15.8-18 vs DMA 13.7 ms per step) the call takes the DMA.
+constexpr uint64_t ZC_MAX_PCIE_BYTES = 256ull << 20;
+bool stage_zerocopy(ac_ctx* ctx, bool sync) {
     if (stage_zerocopy_env() >= 0) return stage_zerocopy_env() == 1;
-    if (ctx->zc_choice >= 0) return ctx->zc_choice == 1;
-    return !sync || ctx->zc_probe % 2 == 0;
+    if (ctx->zc_choice < 0) return !sync || ctx->zc_probe % 2 == 0;
+    if (sync && ++ctx->zc_calls % ZC_REPROBE == 0) return ctx->zc_choice != 1;  // refresh the other path
+    return ctx->zc_choice == 1;
 }
 void stage_zerocopy_record(ac_ctx* ctx, bool zc, double us) {
-    if (stage_zerocopy_env() >= 0 || ctx->zc_choice >= 0) return;
-    if (ctx->zc_probe++ >= 2) ctx->zc_us[zc ? 1 : 0].push_back(us);
+    if (stage_zerocopy_env() >= 0) return;
+    if (ctx->zc_choice < 0 && ctx->zc_probe++ < 2) return;  // the cold call of each path
+    std::vector<double>& v = ctx->zc_us[zc ? 1 : 0];
+    v.push_back(us);
+    if (v.size() > ZC_PROBES) v.erase(v.begin());
     if (ctx->zc_us[0].size() >= ZC_PROBES && ctx->zc_us[1].size() >= ZC_PROBES) {
-        auto median = [](std::vector<double> v) {
-            std::sort(v.begin(), v.end());
-            return v[v.size() / 2];
+        auto median = [](std::vector<double> x) {
+            std::sort(x.begin(), x.end());
+            return x[x.size() / 2];
         };
         ctx->zc_choice = median(ctx->zc_us[1]) <= median(ctx->zc_us[0]) ? 1 : 0;
     }
@@ -1170,16 +1187,13 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
         off = align256(off + sizeof(uint32_t) * jobs[j].n_kmers);
     }
     p.total = off;
-    // Zero-copy re-reads the image over PCIe once per candidate group whenever an XCD's L2
-    // (4 MB) cannot hold its slice of it: at cfg4 (96 MB) the zero-copy stage ran 15.8-18 ms
-    // against 13.7 ms with the DMA (profiles/r02_stage_ab_cfg4.log).  A call whose image
-    // exceeds ZC_MAX_IMAGE_BYTES takes the DMA path, and an undecided context decides DMA.
-    uint64_t image_bytes = 0;
-    for (uint32_t j = 0; j < p.n; ++j) image_bytes += p.n_bases[j] / 8 * 3;  // 2-bit codes + N bitmap
-    if (p.zc && image_bytes > ZC_MAX_IMAGE_BYTES && stage_zerocopy_env() < 0) {
-        p.zc = false;
-        if (ctx->zc_choice < 0) ctx->zc_choice = 0;
-    }
+    // Zero-copy's worst case moves the image over PCIe once per candidate group (ZC_MAX_PCIE_BYTES).
+    uint64_t pcie_bytes = 0;
+    const uint32_t cpw = acamd::cands_per_wave(acamd::pack_factor(k));
+    for (uint32_t j = 0; j < p.n; ++j)
+        pcie_bytes += p.n_bases[j] / 8 * 3 * ((jobs[j].n_kmers + cpw - 1) / cpw);  // 2-bit codes + N bitmap
+    p.zc_eligible = pcie_bytes <= ZC_MAX_PCIE_BYTES;
+    if (!p.zc_eligible && stage_zerocopy_env() < 0) p.zc = false;
     // The slot: wait until the launch that last read it has finished, grow it.
     if (d_counts) {
         p.slot = AC_STAGE_MAX_PARTS + (int)ctx->next_slot;
@@ -1384,7 +1398,9 @@ ac_status ac_error_count_jobs(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint3
     if (first_err == AC_OK) {
         const double us = now_us() - t_call;
         for (size_t g = 0; g < units.size(); ++g)  // once per context (parts of one device share it)
-            if (g == 0 || units[g].c != units[g - 1].c) stage_zerocopy_record(units[g].c, units[g].plan.zc, us);
+            if ((g == 0 || units[g].c != units[g - 1].c) && units[g].plan.zc_eligible)
+                stage_zerocopy_record(units[g].c, units[g].plan.zc, us);
+        units[0].c->zc_last = units[0].plan.zc_eligible ? -1 : 0;
     }
     if (g_trace.on) {
         g_trace.sum[7] += now_us() - t_sync;
@@ -1419,6 +1435,7 @@ ac_status ac_error_count_jobs_submit(ac_ctx* ctx, uint32_t k, const ac_job* jobs
 int ac_stage_mode(const ac_ctx* ctx) {
     if (!ctx) return -1;
     if (stage_zerocopy_env() >= 0) return stage_zerocopy_env();
+    if (ctx->zc_last == 0) return 0;  // the last call's image is DMA-only
     return ctx->zc_choice;
 }
 

@@ -284,9 +284,10 @@ def main():
         geo = kc.last_launch()
         kc.close()
 
-    # ---- transfer path of the host-buffer stage (untimed): the library times its first
-    # synchronous calls with zero-copy and with DMA, alternately, and keeps the faster
-    # (ac_stage_mode; the winner depends on the host's PCIe / memory latency under load).
+    # ---- transfer path of the host-buffer stage (untimed): large images always take the DMA;
+    # otherwise the library times its first synchronous calls with zero-copy and with DMA,
+    # alternately, and keeps the faster (ac_stage_mode; the winner depends on the host's
+    # PCIe / memory latency under load).
     tune_calls = 0
     while counter.stage_mode() < 0 and tune_calls < 32:
         counter.count_jobs(args.k, jobs)
@@ -392,7 +393,7 @@ def main():
                                     else "1 DMA in -> 1 fused launch") + " (both ends)"
                                  + (" -> RCCL all-reduce -> counts D2H" if world > 1 else
                                     (" -> counts written to pinned host memory by the kernel"
-                                     if stage_path == "zero-copy" else " -> 1 DMA of the counts back"))),
+                                     if stage_path == "zero-copy" else " -> counts written to pinned host memory by the kernel"))),
                        "stage_path": stage_path,
                        "parallelism": (f"{args.scaling} window shards x{world}, "
                                        f"{'RCCL' if backend == 'nccl' else backend} all-reduce of counts")
@@ -403,8 +404,9 @@ def main():
             out["step_ms"] = {"min": float(d.min()), "p50": float(np.median(d)), "max": float(d.max())}
         out["stage_cold_call_ms"] = cold_ms
         out["stage_path_choice"] = {"path": stage_path, "untimed_calls": tune_calls,
-                                    "note": "zero-copy vs DMA chosen by the library from its first synchronous "
-                                            "calls, timed both ways (ac_stage_mode)"}
+                                    "note": "zero-copy vs DMA chosen by the library (ac_stage_mode): DMA when "
+                                            "image x candidate groups > 256 MB, else timed both ways over the first "
+                                            "synchronous calls and re-checked every 64th call"}
         if kern_ms is not None:
             ops = OPS_PER_BASE_WORD / P * units_rank  # algorithmic lane-ops per launch (this rank)
             achieved = ops / (kern_ms * 1e-3)

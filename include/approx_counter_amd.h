@@ -261,10 +261,14 @@ ac_status ac_check(ac_ctx* ctx, void* hip_stream);
 /*
  * How ac_error_count_jobs moves the packed inputs (no reference counterpart):
  * 1 = zero-copy (the kernel reads the pinned staging block over PCIe), 0 = one
- * DMA in and one back, -1 = not decided yet.  Unless AC_STAGE_ZEROCOPY=1/0
- * forces one, a context times its first synchronous calls both ways (they
- * alternate; 10 calls) and keeps the faster: which one wins depends on the
- * host (PCIe / host-memory latency under other load), not on the workload.
+ * DMA in (either way the kernel writes the counts into the pinned block), -1 =
+ * not decided yet.  Unless AC_STAGE_ZEROCOPY=1/0 forces one: a call whose
+ * image x candidate groups exceeds 256 MB always takes the DMA (zero-copy may
+ * read the image over PCIe once per group) and then reports 0; for smaller
+ * calls a context times its first synchronous calls both ways (they alternate;
+ * 10 calls), uses the faster by median of each path's last 4 calls, and every
+ * 64th call takes the other path to keep its figures current: which one wins
+ * depends on the host (PCIe / host-memory latency under other load).
  */
 int ac_stage_mode(const ac_ctx* ctx);
 
