@@ -71,6 +71,13 @@ def load():
     vp = ctypes.c_void_p
     L.ac_abi_version.restype = ctypes.c_int
     L.ac_device_count.restype = ctypes.c_int
+    L.ac_comm_id_bytes.restype = ctypes.c_int
+    L.ac_comm_unique_id.argtypes = [vp, vp]
+    L.ac_comm_unique_id.restype = ctypes.c_int
+    L.ac_comm_init.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp]
+    L.ac_comm_init.restype = ctypes.c_int
+    L.ac_allreduce_counts.argtypes = [vp, vp, ctypes.c_uint64, vp]
+    L.ac_allreduce_counts.restype = ctypes.c_int
     L.ac_last_error.argtypes = [vp]
     L.ac_last_error.restype = ctypes.c_char_p
     L.ac_create.argtypes = [ctypes.POINTER(vp), ctypes.c_int]

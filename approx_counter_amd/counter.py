@@ -240,6 +240,24 @@ class ApproxCounter:
         """ac_stage_mode: 1 zero-copy, 0 DMA, -1 not decided yet (count_jobs probes both first)."""
         return int(self._L.ac_stage_mode(self._h))
 
+    # ---- multi-process data parallelism: the count all-reduce over RCCL (ac_comm_*) ----
+    def comm_unique_id(self) -> bytes:
+        """ac_comm_unique_id: a fresh RCCL unique id (rank 0 sends it to every rank)."""
+        buf = ctypes.create_string_buffer(self._L.ac_comm_id_bytes())
+        check(self._L.ac_comm_unique_id(self._h, buf), self._h)
+        return buf.raw
+
+    def comm_init(self, n_ranks: int, rank: int, unique_id: bytes) -> None:
+        """ac_comm_init: join the n_ranks-rank RCCL communicator as `rank`."""
+        buf = ctypes.create_string_buffer(bytes(unique_id), self._L.ac_comm_id_bytes())
+        check(self._L.ac_comm_init(self._h, int(n_ranks), int(rank), buf), self._h)
+
+    def allreduce_counts(self, d_counts, stream=None) -> None:
+        """ac_allreduce_counts: in-place uint32 sum of a device count tensor over the ranks."""
+        check(self._L.ac_allreduce_counts(self._h, ctypes.c_void_p(d_counts.data_ptr()),
+                                          ctypes.c_uint64(d_counts.numel()), ctypes.c_void_p(stream or 0)),
+              self._h)
+
     def check(self, stream=None) -> None:
         """ac_check: raise if a device launch since the last check skipped a malformed window."""
         check(self._L.ac_check(self._h, ctypes.c_void_p(stream or 0)), self._h)

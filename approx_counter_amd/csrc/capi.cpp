@@ -5,7 +5,9 @@
 // find<0,2> per candidate under OpenMP (547-599), this layer uploads the
 // packed sample once per call and launches one HIP kernel over the
 // candidate x window grid.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>  // types only: RCCL is resolved at run time (rccl() below)
 
 #include <algorithm>
 #include <cctype>
@@ -72,6 +74,8 @@ struct ac_ctx {
     uint32_t last_wpw = 0, last_groups = 0;
     // ac_create_multi: contexts of shards 1..n-1 (this context is shard 0)
     std::vector<ac_ctx*> peers;
+    // RCCL communicator of a multi-process job (ac_comm_init), or null
+    ncclComm_t comm = nullptr;
     // device error word of the asynchronous entry points (ac_check), and a
     // pinned word to read it back through
     uint32_t* d_err = nullptr;
@@ -384,6 +388,43 @@ ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hi
 
 }  // namespace
 
+// RCCL for the multi-process path (ac_comm_*): resolved at run time with dlopen, so the
+// library itself does not depend on it; an RCCL already in the process (torch's) is reused.
+namespace {
+struct Rccl {
+    decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+    decltype(&ncclCommInitRank) comm_init_rank = nullptr;
+    decltype(&ncclAllReduce) all_reduce = nullptr;
+    decltype(&ncclCommDestroy) comm_destroy = nullptr;
+    decltype(&ncclGetErrorString) error_string = nullptr;
+    std::string err;  // empty when usable
+};
+const Rccl& rccl() {
+    static const Rccl r = [] {
+        Rccl x;
+        void* h = nullptr;
+        for (const char* name : {"librccl.so.1", "librccl.so"})
+            if (!h) h = dlopen(name, RTLD_NOW | RTLD_NOLOAD);
+        for (const char* name : {"librccl.so.1", "librccl.so"})
+            if (!h) h = dlopen(name, RTLD_NOW | RTLD_LOCAL);
+        if (!h) {
+            const char* e = dlerror();
+            x.err = std::string("RCCL (librccl.so) could not be loaded: ") + (e ? e : "?");
+            return x;
+        }
+        x.get_unique_id = (decltype(x.get_unique_id))dlsym(h, "ncclGetUniqueId");
+        x.comm_init_rank = (decltype(x.comm_init_rank))dlsym(h, "ncclCommInitRank");
+        x.all_reduce = (decltype(x.all_reduce))dlsym(h, "ncclAllReduce");
+        x.comm_destroy = (decltype(x.comm_destroy))dlsym(h, "ncclCommDestroy");
+        x.error_string = (decltype(x.error_string))dlsym(h, "ncclGetErrorString");
+        if (!x.get_unique_id || !x.comm_init_rank || !x.all_reduce || !x.comm_destroy || !x.error_string)
+            x.err = "RCCL is missing one of ncclGetUniqueId / ncclCommInitRank / ncclAllReduce / ncclCommDestroy";
+        return x;
+    }();
+    return r;
+}
+}  // namespace
+
 extern "C" {
 
 int ac_abi_version(void) { return AC_ABI_VERSION; }
@@ -441,6 +482,7 @@ void ac_destroy(ac_ctx* ctx) {
     if (!ctx) return;
     for (ac_ctx* p : ctx->peers) ac_destroy(p);
     (void)hipSetDevice(ctx->device);
+    if (ctx->comm) (void)rccl().comm_destroy(ctx->comm);
     for (void* p : ctx->d_buf)
         if (p) (void)hipFree(p);
     if (ctx->d_stage) (void)hipFree(ctx->d_stage);
@@ -949,6 +991,50 @@ ac_status ac_check(ac_ctx* ctx, void* hip_stream) {
     AC_HIP(ctx, hipMemsetAsync(ctx->d_err, 0, sizeof(uint32_t), st));
     AC_HIP(ctx, hipStreamSynchronize(st));
     return device_error(ctx, word);
+}
+
+int ac_comm_id_bytes(void) { return (int)sizeof(ncclUniqueId); }
+
+ac_status ac_comm_unique_id(ac_ctx* ctx, void* id_out) {
+    if (!ctx || !id_out) return fail(ctx, AC_ERR_INVALID, "ctx or id_out is NULL");
+    const Rccl& r = rccl();
+    if (!r.err.empty()) return fail(ctx, AC_ERR_DEVICE, r.err);
+    AC_HIP(ctx, hipSetDevice(ctx->device));
+    ncclUniqueId id;
+    const ncclResult_t e = r.get_unique_id(&id);
+    if (e != ncclSuccess) return fail(ctx, AC_ERR_DEVICE, std::string("ncclGetUniqueId: ") + r.error_string(e));
+    std::memcpy(id_out, &id, sizeof id);
+    return AC_OK;
+}
+
+ac_status ac_comm_init(ac_ctx* ctx, int n_ranks, int rank, const void* id) {
+    if (!ctx || !id) return fail(ctx, AC_ERR_INVALID, "ctx or id is NULL");
+    if (n_ranks < 1 || rank < 0 || rank >= n_ranks) return fail(ctx, AC_ERR_INVALID, "rank outside [0, n_ranks)");
+    if (!ctx->peers.empty()) return fail(ctx, AC_ERR_INVALID, "ac_comm_init needs a single-device context");
+    if (ctx->comm) return fail(ctx, AC_ERR_INVALID, "the context already has a communicator");
+    const Rccl& r = rccl();
+    if (!r.err.empty()) return fail(ctx, AC_ERR_DEVICE, r.err);
+    AC_HIP(ctx, hipSetDevice(ctx->device));
+    ncclUniqueId u;
+    std::memcpy(&u, id, sizeof u);
+    ncclComm_t c = nullptr;
+    const ncclResult_t e = r.comm_init_rank(&c, n_ranks, u, rank);
+    if (e != ncclSuccess) return fail(ctx, AC_ERR_DEVICE, std::string("ncclCommInitRank: ") + r.error_string(e));
+    ctx->comm = c;
+    return AC_OK;
+}
+
+ac_status ac_allreduce_counts(ac_ctx* ctx, uint32_t* d_counts, uint64_t n, void* hip_stream) {
+    if (!ctx) return fail(ctx, AC_ERR_INVALID, "ctx is NULL");
+    if (!ctx->comm) return fail(ctx, AC_ERR_INVALID, "no communicator: call ac_comm_init first");
+    if (n == 0) return AC_OK;
+    if (!d_counts) return fail(ctx, AC_ERR_INVALID, "d_counts is NULL");
+    AC_HIP(ctx, hipSetDevice(ctx->device));
+    const Rccl& r = rccl();
+    const ncclResult_t e = r.all_reduce(d_counts, d_counts, (size_t)n, ncclUint32, ncclSum, ctx->comm,
+                                        (hipStream_t)hip_stream);
+    if (e != ncclSuccess) return fail(ctx, AC_ERR_DEVICE, std::string("ncclAllReduce: ") + r.error_string(e));
+    return AC_OK;
 }
 
 }  // extern "C"

@@ -322,6 +322,22 @@ def main():
                      "note": "same host-buffer steps via ac_error_count_jobs_submit + async D2H, not synchronised per "
                              "step: step i+1's packing overlaps step i's kernel (independent -mr runs)"}
 
+    # ---- the count all-reduce of N > 1 (RCCL over xGMI): the library's own communicator
+    # (ac_comm_init, id from rank 0 over the process group); if it cannot be set up, torch's
+    # RCCL process group does the same all-reduce and the line says so.
+    allreduce_by = None
+    if world > 1 and backend == "nccl":
+        try:
+            uid = [counter.comm_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            counter.comm_init(world, rank, uid[0])
+            allreduce_by = "library (ac_allreduce_counts, RCCL)"
+        except Exception as exc:  # noqa: BLE001 -- reported on the line, the run continues on torch's RCCL
+            print(f"[bench] library RCCL communicator unavailable ({exc}); using torch.distributed", file=sys.stderr)
+            allreduce_by = f"torch.distributed RCCL (library communicator failed: {exc})"
+    elif world > 1:
+        allreduce_by = f"torch.distributed {backend} on host copies (rehearsal)"
+
     # ---- the stage (value): host Dna5 buffers -> host counts ---------------------------------
     if world == 1:
         def step():
@@ -330,7 +346,10 @@ def main():
         def step():
             counter.submit_jobs(args.k, jobs, d_counts, stream=stream.cuda_stream)
             if backend == "nccl":
-                dist.all_reduce(d_counts)  # RCCL over xGMI, on the current stream
+                if allreduce_by.startswith("library"):
+                    counter.allreduce_counts(d_counts, stream=stream.cuda_stream)  # RCCL over xGMI
+                else:
+                    dist.all_reduce(d_counts)  # torch's RCCL, on the current stream
                 h_counts.copy_(d_counts, non_blocking=True)
                 stream.synchronize()
             else:
@@ -392,12 +411,12 @@ def main():
                                  + ("1 fused launch reading the pinned block (zero-copy)" if stage_path == "zero-copy"
                                     else "1 DMA in -> 1 fused launch") + " (both ends)"
                                  + (" -> RCCL all-reduce -> counts D2H" if world > 1 else
-                                    (" -> counts written to pinned host memory by the kernel"
-                                     if stage_path == "zero-copy" else " -> counts written to pinned host memory by the kernel"))),
+                                    " -> counts written to pinned host memory by the kernel")),
                        "stage_path": stage_path,
                        "parallelism": (f"{args.scaling} window shards x{world}, "
                                        f"{'RCCL' if backend == 'nccl' else backend} all-reduce of counts")
                        if world > 1 else "1 GPU"},
+            **({"allreduce": allreduce_by} if allreduce_by else {}),
         }
         if world == 1:  # each step is synchronous at N = 1: its own duration
             d = np.diff(np.array([t0] + marks)) * 1e3

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define AC_ABI_VERSION 2
+#define AC_ABI_VERSION 3
 
 typedef int32_t ac_status;
 #define AC_OK 0
@@ -257,6 +257,25 @@ ac_status ac_error_count_jobs_submit(ac_ctx* ctx, uint32_t k, const ac_job* jobs
  * set-up fault) if a launch since the last check hit one, AC_OK otherwise.
  */
 ac_status ac_check(ac_ctx* ctx, void* hip_stream);
+
+/*
+ * Multi-process data parallelism (one process per GPU): window
+ * shards are counted independently (ac_error_count_jobs_submit leaves each
+ * shard's counts in device memory) and the count vectors are summed by one RCCL
+ * all-reduce over xGMI, owned by the context.  There is no reference
+ * counterpart (errorCount runs on one host's OpenMP threads, approx_counter.cpp:547).
+ *   ac_comm_id_bytes    size of the RCCL unique id (128)
+ *   ac_comm_unique_id   a fresh id (rank 0); the caller sends it to every rank
+ *   ac_comm_init        join the n_ranks-rank communicator as `rank`
+ *                       (single-device contexts; ranks on distinct devices)
+ *   ac_allreduce_counts in-place uint32 sum of d_counts[0, n) over the ranks,
+ *                       asynchronous on hip_stream
+ * RCCL (librccl.so) is loaded at the first of these calls, not at library load.
+ */
+int ac_comm_id_bytes(void);
+ac_status ac_comm_unique_id(ac_ctx* ctx, void* id_out);
+ac_status ac_comm_init(ac_ctx* ctx, int n_ranks, int rank, const void* id);
+ac_status ac_allreduce_counts(ac_ctx* ctx, uint32_t* d_counts, uint64_t n, void* hip_stream);
 
 /*
  * How ac_error_count_jobs moves the packed inputs (no reference counterpart):

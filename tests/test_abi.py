@@ -27,7 +27,7 @@ def test_library_targets_gfx950():
 
 
 def test_abi_version():
-    assert _lib.load().ac_abi_version() == 2
+    assert _lib.load().ac_abi_version() == 3
 
 
 def test_pack_layout():
@@ -57,6 +57,16 @@ def test_null_ctx_is_rejected():
     st = L.ac_error_count(None, 16, None, 0, None, None)
     assert st == _lib.AC_ERR_INVALID
     assert b"ctx" in L.ac_last_error(None)
+
+
+def test_comm_entry_points_without_a_context():
+    """The RCCL entry points reject a NULL context before touching RCCL; the id size is
+    RCCL's 128 bytes (ncclUniqueId)."""
+    L = _lib.load()
+    assert L.ac_comm_id_bytes() == 128
+    assert L.ac_comm_unique_id(None, None) == _lib.AC_ERR_INVALID
+    assert L.ac_comm_init(None, 1, 0, None) == _lib.AC_ERR_INVALID
+    assert L.ac_allreduce_counts(None, None, 0, None) == _lib.AC_ERR_INVALID
 
 
 def _has_gpu():

@@ -236,3 +236,30 @@ def test_large_image_takes_dma_path():
         c.close()
     sub = np.r_[0:16, 500:508, 992:1000]  # every candidate group's first and last lanes, and more
     assert np.array_equal(got[sub], oracle.count_myers(16, kmers[sub], win, 16))
+
+
+def test_rccl_allreduce_single_rank(counter):
+    """The library's RCCL path (ac_comm_unique_id / ac_comm_init / ac_allreduce_counts),
+    as bench.py's N > 1 steps use it, on a one-rank communicator (this pool has one GPU
+    per box; RCCL refuses two ranks on one device): the sum over one rank is the
+    identity, so the all-reduced counts equal the oracle's; misuse is refused."""
+    import torch
+
+    with pytest.raises(ac.ApproxCounterError):  # no communicator yet
+        counter.allreduce_counts(torch.zeros(4, dtype=torch.int32, device="cuda"))
+    uid = counter.comm_unique_id()
+    assert len(uid) == 128
+    counter.comm_init(1, 0, uid)
+    with pytest.raises(ac.ApproxCounterError):  # one communicator per context
+        counter.comm_init(1, 0, uid)
+    a = cases.planted_case(41, 16, 300, 500, win_len=(100, 101), p_n=0.01)
+    b = cases.planted_case(42, 16, 200, 400, win_len=(101, 101))
+    jobs = ac.Jobs([(a[0], ac.Dna5Sample.from_windows(a[1])), (b[0], ac.Dna5Sample.from_windows(b[1]))])
+    out = torch.zeros(jobs.n_counts, dtype=torch.int32, device="cuda")
+    st = torch.cuda.current_stream()
+    counter.submit_jobs(16, jobs, out, stream=st.cuda_stream)
+    counter.allreduce_counts(out, stream=st.cuda_stream)
+    counter.check(stream=st.cuda_stream)
+    got = out.cpu().numpy().view(np.uint32).astype(np.uint64)
+    assert np.array_equal(got[:300], oracle.count_myers(16, *a))
+    assert np.array_equal(got[300:], oracle.count_myers(16, *b))
