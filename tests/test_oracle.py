@@ -43,6 +43,17 @@ def test_strict_variant_is_a_real_alternative():
     assert diff > 0
 
 
+def test_strict_levels_depend_on_context():
+    """Why `strict` is not a flag flip on the GPU's <= d NFA rows: an exact
+    occurrence reports {0, 1, 2} under M1 wherever it sits, but under strict {0, 2} when it
+    starts the window (no leading base for scheme 2's e = 1) and {0, 1, 2} otherwise."""
+    p = "ACGTTGCAAGTCCGTA"
+    km = np.array([cases.kmer_value(p)], dtype=np.uint64)
+    for w, m1, strict in (("GG" + p + "TT", 7, 7), (p + "TT", 7, 5), ("GG" + p, 7, 7), (p, 7, 5)):
+        assert oracle.count_scheme(16, km, [w], return_levels=True)[1][0][0] == m1
+        assert oracle.count_scheme(16, km, [w], strict=True, return_levels=True)[1][0][0] == strict
+
+
 def test_known_answers():
     km = "ACGTACGTTGCAAGCT"
     v = cases.kmer_value(km)
