@@ -29,7 +29,7 @@ static_assert(AC_MAX_JOBS <= AC_MAX_SEGS, "every job of ac_error_count_jobs is o
 // A synchronous jobs call is cut into up to this many parts (window ranges of
 // every job), each packed, sent and counted on its own stream, so a part's
 // packing and DMA overlap the previous part's kernel.
-#define AC_STAGE_MAX_PARTS 2
+#define AC_STAGE_MAX_PARTS 4
 
 struct ac_ctx {
     int device = 0;
@@ -1097,15 +1097,22 @@ struct JobPlan {
     bool zc_eligible = true;  // false: the image is too large for zero-copy (DMA, not measured)
 };
 
-// AC_STAGE_PARTS (1 or 2, default 1) and AC_STAGE_SPLIT (first part's share of
-// the bases, default 0.5): experiment switches of the synchronous stage.
-int stage_parts() {
-    static const int v = [] {
+// AC_STAGE_PARTS (1-4) and AC_STAGE_SPLIT (with two parts, the first part's
+// share of the bases, default 0.5): switches of the synchronous stage.
+// Without AC_STAGE_PARTS: one part, or two for calls of at least
+// STAGE_PARTS_MIN_WINDOWS windows, whose pack and DMA take milliseconds (cfg4:
+// pack 2.8 + DMA 3.6 ms before a 7.5 ms kernel): part 1 is
+// packed and sent while part 0 counts.  cfg4 step p50 12.1-12.2 ms with two
+// parts vs 13.3 with one and 13.5-13.6 with four; cfg3 (200k windows) 3.56 ms
+// with four vs 3.36 with one (profiles/r02_stage_parts_ab.log).
+constexpr uint64_t STAGE_PARTS_MIN_WINDOWS = 1ull << 18;
+int stage_parts(uint64_t total_w) {
+    static const int env = [] {
         const char* e = std::getenv("AC_STAGE_PARTS");
-        const int n = e ? std::atoi(e) : 1;  // 2 measured slower (DMA and zero-copy alike)
-        return std::max(1, std::min(AC_STAGE_MAX_PARTS, n));
+        return e ? std::max(1, std::min(AC_STAGE_MAX_PARTS, std::atoi(e))) : 0;
     }();
-    return v;
+    if (env) return env;
+    return total_w >= STAGE_PARTS_MIN_WINDOWS ? 2 : 1;
 }
 // Zero-copy stage (default; AC_STAGE_ZEROCOPY=0 = DMA in and out): the count
 // kernel reads the packed inputs straight from the pinned host block and
@@ -1170,6 +1177,53 @@ unsigned stage_host_flags() {
         return (unsigned)hipHostMallocDefault;
     }();
     return v;
+}
+
+// DMA-mode transfer of a one-part call (default, AC_STAGE_BLIT=0 turns it off):
+// a copy kernel on the compute queue reads the pinned block once over PCIe and
+// writes the device block, so the count kernel follows it on the same queue;
+// otherwise hipMemcpyAsync (the copy engine, whose completion -> kernel start
+// costs ~9 us at cfg2).  With the job-by-job pipeline below: cfg2 sync 114-118
+// vs 130-132 us, step p50 0.156-0.158 vs 0.164-0.167 ms on one loaded box
+// (profiles/r02_stage_pipe_blit_ab.log); alone it gained nothing (128 vs 130 us).
+int stage_blit() {
+    static const int v = [] {
+        const char* e = std::getenv("AC_STAGE_BLIT");
+        return e ? (std::atoi(e) != 0 ? 1 : 0) : 1;
+    }();
+    return v;
+}
+// DMA mode packs and sends job by job, so job j's inputs travel while job j + 1
+// is packed (default; AC_STAGE_PIPE=0 = pack everything, then one transfer).
+int stage_pipe() {
+    static const int v = [] {
+        const char* e = std::getenv("AC_STAGE_PIPE");
+        return e ? (std::atoi(e) != 0 ? 1 : 0) : 1;
+    }();
+    return v;
+}
+constexpr uint32_t BLIT_THREADS = 256, BLIT_UNROLL = 2;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__global__ void __launch_bounds__(BLIT_THREADS) stage_blit_kernel(const u32x4* __restrict__ src,
+                                                                  u32x4* __restrict__ dst, uint32_t n16) {
+    const uint32_t i0 = blockIdx.x * (BLIT_THREADS * BLIT_UNROLL) + threadIdx.x;
+    u32x4 v[BLIT_UNROLL];
+#pragma unroll
+    for (uint32_t u = 0; u < BLIT_UNROLL; ++u)
+        if (i0 + u * BLIT_THREADS < n16) v[u] = __builtin_nontemporal_load(src + i0 + u * BLIT_THREADS);
+#pragma unroll
+    for (uint32_t u = 0; u < BLIT_UNROLL; ++u)
+        if (i0 + u * BLIT_THREADS < n16) dst[i0 + u * BLIT_THREADS] = v[u];
+}
+// bytes: a multiple of 16 (the stage's offsets are 256-aligned)
+hipError_t stage_blit_launch(const void* src_dev, void* dst, size_t bytes, hipStream_t stream) {
+    const size_t n16 = bytes / 16;
+    if (n16 == 0) return hipSuccess;
+    if (n16 >= (1ull << 32)) return hipErrorInvalidValue;
+    const uint32_t per = BLIT_THREADS * BLIT_UNROLL;
+    const uint32_t blocks = (uint32_t)((n16 + per - 1) / per);
+    stage_blit_kernel<<<blocks, BLIT_THREADS, 0, stream>>>((const u32x4*)src_dev, (u32x4*)dst, (uint32_t)n16);
+    return hipGetLastError();
 }
 
 double stage_split() {
@@ -1278,7 +1332,7 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
     const uint32_t cpw = acamd::cands_per_wave(acamd::pack_factor(k));
     for (uint32_t j = 0; j < p.n; ++j)
         pcie_bytes += p.n_bases[j] / 8 * 3 * ((jobs[j].n_kmers + cpw - 1) / cpw);  // 2-bit codes + N bitmap
-    p.zc_eligible = pcie_bytes <= ZC_MAX_PCIE_BYTES;
+    p.zc_eligible = p.zc_eligible && pcie_bytes <= ZC_MAX_PCIE_BYTES;  // (a multi-part call is DMA-only)
     if (!p.zc_eligible && stage_zerocopy_env() < 0) p.zc = false;
     // The slot: wait until the launch that last read it has finished, grow it.
     if (d_counts) {
@@ -1328,9 +1382,31 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
     // In both modes the kernel writes the error word and the counts straight into the pinned
     // block (hd), so no copy comes back (profiles/r02_stage_dma_back_ab.log).
     char* hd = (char*)sl.hd;
-    pool.run((uint32_t)tasks.size(), pack);
-    mark(2);
-    if (!zc) AC_HIP(ctx, hipMemcpyAsync(d, h, p.off_err, hipMemcpyHostToDevice, stream));
+    // DMA mode sends the inputs [r0, r1) of the slot (copy engine or blit kernel)
+    auto transfer = [&](size_t r0, size_t r1) -> hipError_t {
+        if (r1 <= r0) return hipSuccess;
+        if (stage_blit() && part == 0 && wave_div == 0) return stage_blit_launch(hd + r0, d + r0, r1 - r0, stream);
+        return hipMemcpyAsync(d + r0, h + r0, r1 - r0, hipMemcpyHostToDevice, stream);
+    };
+    if (!zc && stage_pipe() && p.n > 1) {
+        // job by job: job j's inputs travel while job j + 1 is packed
+        uint32_t t0 = 0;
+        for (uint32_t j = 0; j < p.n; ++j) {
+            uint32_t t1 = t0;
+            while (t1 < (uint32_t)tasks.size() && tasks[t1].job == j) ++t1;
+            if (t1 > t0) {
+                const std::function<void(uint32_t)> pack_j = [&](uint32_t t) { pack(t0 + t); };
+                pool.run(t1 - t0, pack_j);
+            }
+            AC_HIP(ctx, transfer(p.off_kmers[j], j + 1 < p.n ? p.off_kmers[j + 1] : p.off_err));
+            t0 = t1;
+        }
+        mark(2);
+    } else {
+        pool.run((uint32_t)tasks.size(), pack);
+        mark(2);
+        if (!zc) AC_HIP(ctx, transfer(0, p.off_err));
+    }
     mark(3);
     ac_segment segs[AC_MAX_JOBS];
     uint64_t cbase = 0;
@@ -1365,7 +1441,8 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
 
 // Shard g of G of job windows [0, n): contiguous, balanced by bases (the rule
 // of ac_error_count's multi-device split and approx_counter_amd/shard.py).
-void shard_range(const uint32_t* length, uint32_t n, size_t G, size_t g, uint32_t* lo, uint32_t* hi) {
+// All G + 1 cut points of job windows [0, n) in one pass (shard g = [cut[g], cut[g + 1])).
+std::vector<uint32_t> shard_cuts(const uint32_t* length, uint32_t n, size_t G) {
     uint64_t total = 0;
     for (uint32_t i = 0; i < n; ++i) total += length[i];
     std::vector<uint32_t> cut(G + 1, n);
@@ -1376,8 +1453,7 @@ void shard_range(const uint32_t* length, uint32_t n, size_t G, size_t g, uint32_
         acc += length[i];
         while (c < G && acc * G >= total * c) cut[c++] = i + 1;
     }
-    *lo = cut[g];
-    *hi = cut[g + 1];
+    return cut;
 }
 
 // The two parts of a single-device call: windows [0, cut) and [cut, n), the
@@ -1420,26 +1496,41 @@ ac_status ac_error_count_jobs(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint3
     for (uint32_t j = 0; j < n_jobs; ++j) total_w += jobs[j].sample.n_windows;
     if (!ctx->peers.empty()) {
         const size_t G = ctx->peers.size() + 1;
+        std::vector<std::vector<uint32_t>> cuts;
+        for (uint32_t j = 0; j < n_jobs; ++j) cuts.push_back(shard_cuts(jobs[j].sample.length, jobs[j].sample.n_windows, G));
         for (size_t g = 0; g < G; ++g) {
             Unit u{g == 0 ? ctx : ctx->peers[g - 1], 0, nullptr, 0, JobPlan()};
             u.stream = u.c->stream;
             u.plan.n = n_jobs;
-            for (uint32_t j = 0; j < n_jobs; ++j)
-                shard_range(jobs[j].sample.length, jobs[j].sample.n_windows, G, g, &u.plan.lo[j], &u.plan.hi[j]);
+            for (uint32_t j = 0; j < n_jobs; ++j) {
+                u.plan.lo[j] = cuts[j][g];
+                u.plan.hi[j] = cuts[j][g + 1];
+            }
             units.push_back(u);
         }
     } else {
-        const int parts = total_w >= 2048 ? stage_parts() : 1;  // small calls: one launch
+        const int parts = total_w >= 2048 ? stage_parts(total_w) : 1;  // small calls: one launch
+        // every job's part boundaries, once (equal shares of the bases; two parts: AC_STAGE_SPLIT)
+        std::vector<std::vector<uint32_t>> cuts;
+        for (uint32_t j = 0; j < n_jobs; ++j) {
+            const uint32_t n = jobs[j].sample.n_windows;
+            if (parts == 1)
+                cuts.push_back({0u, n});
+            else if (parts == 2)
+                cuts.push_back({0u, part_cut(jobs[j].sample.length, n, stage_split()), n});
+            else
+                cuts.push_back(shard_cuts(jobs[j].sample.length, n, (size_t)parts));
+        }
         for (int q = 0; q < parts; ++q) {
             if (q > 0 && !ctx->part_stream[q])
                 AC_HIP(ctx, hipStreamCreateWithFlags(&ctx->part_stream[q], hipStreamNonBlocking));
             Unit u{ctx, q, q == 0 ? ctx->stream : ctx->part_stream[q], (parts > 1 && q == 0) ? 2u : 0u, JobPlan()};
             u.plan.n = n_jobs;
+            // parts are for large calls: DMA only (zero-copy would read the whole image per group)
+            u.plan.zc_eligible = parts == 1;
             for (uint32_t j = 0; j < n_jobs; ++j) {
-                const uint32_t n = jobs[j].sample.n_windows;
-                const uint32_t cut = parts > 1 ? part_cut(jobs[j].sample.length, n, stage_split()) : n;
-                u.plan.lo[j] = q == 0 ? 0 : cut;
-                u.plan.hi[j] = q == 0 ? cut : n;
+                u.plan.lo[j] = cuts[j][q];
+                u.plan.hi[j] = cuts[j][q + 1];
             }
             units.push_back(u);
         }

@@ -409,7 +409,9 @@ def main():
                        "candidates": n_c, "kmer_bp_per_step": units_job, "kmer_bp_per_rank_step": units_rank,
                        "stage": ("Dna5 host buffers -> pack (host pool, pinned) -> "
                                  + ("1 fused launch reading the pinned block (zero-copy)" if stage_path == "zero-copy"
-                                    else "1 DMA in -> 1 fused launch") + " (both ends)"
+                                    else ("per read end: pack, then a copy kernel reads it over PCIe into HBM "
+                                          "while the next end is packed (windows >= 2^18: two parts, copy "
+                                          "engine) -> 1 fused launch")) + " (both ends)"
                                  + (" -> RCCL all-reduce -> counts D2H" if world > 1 else
                                     " -> counts written to pinned host memory by the kernel")),
                        "stage_path": stage_path,
