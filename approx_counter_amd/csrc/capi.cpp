@@ -1099,20 +1099,22 @@ struct JobPlan {
 
 // AC_STAGE_PARTS (1-4) and AC_STAGE_SPLIT (with two parts, the first part's
 // share of the bases, default 0.5): switches of the synchronous stage.
-// Without AC_STAGE_PARTS: one part, or two for calls of at least
-// STAGE_PARTS_MIN_WINDOWS windows, whose pack and DMA take milliseconds (cfg4:
-// pack 2.8 + DMA 3.6 ms before a 7.5 ms kernel): part 1 is
-// packed and sent while part 0 counts.  cfg4 step p50 12.1-12.2 ms with two
-// parts vs 13.3 with one and 13.5-13.6 with four; cfg3 (200k windows) 3.56 ms
-// with four vs 3.36 with one (profiles/r02_stage_parts_ab.log).
-constexpr uint64_t STAGE_PARTS_MIN_WINDOWS = 1ull << 18;
+// Without AC_STAGE_PARTS: calls whose pack and DMA take hundreds of
+// microseconds or more are cut into parts (equal bases, one stream each), so
+// part q + 1 is packed and sent while part q counts: two parts from 2^17
+// windows, four from 2^19.  Same box, interleaved (profiles/r02_stage_parts_ab2.log):
+// cfg4 (2M windows) step p50 10.26-10.31 ms in four parts, 10.42-10.49 in three,
+// 11.27 in two (13.3 in one, r02_stage_parts_ab.log); cfg3 (200k windows)
+// 3.27-3.29 ms in two vs 3.24-3.40 one-part with the zero-copy / DMA chooser
+// and 3.42 one-part DMA.
+constexpr uint64_t STAGE_PARTS2_MIN_WINDOWS = 1ull << 17, STAGE_PARTS4_MIN_WINDOWS = 1ull << 19;
 int stage_parts(uint64_t total_w) {
     static const int env = [] {
         const char* e = std::getenv("AC_STAGE_PARTS");
         return e ? std::max(1, std::min(AC_STAGE_MAX_PARTS, std::atoi(e))) : 0;
     }();
     if (env) return env;
-    return total_w >= STAGE_PARTS_MIN_WINDOWS ? 2 : 1;
+    return total_w >= STAGE_PARTS4_MIN_WINDOWS ? 4 : total_w >= STAGE_PARTS2_MIN_WINDOWS ? 2 : 1;
 }
 // Zero-copy stage (default; AC_STAGE_ZEROCOPY=0 = DMA in and out): the count
 // kernel reads the packed inputs straight from the pinned host block and

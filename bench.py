@@ -410,8 +410,9 @@ def main():
                        "stage": ("Dna5 host buffers -> pack (host pool, pinned) -> "
                                  + ("1 fused launch reading the pinned block (zero-copy)" if stage_path == "zero-copy"
                                     else ("per read end: pack, then a copy kernel reads it over PCIe into HBM "
-                                          "while the next end is packed (windows >= 2^18: two parts, copy "
-                                          "engine) -> 1 fused launch")) + " (both ends)"
+                                          "while the next end is packed -> 1 fused launch (>= 2^17 windows: 2 parts, "
+                                          ">= 2^19: 4, each packed and sent by the copy engine while the previous "
+                                          "part counts)")) + " (both ends)"
                                  + (" -> RCCL all-reduce -> counts D2H" if world > 1 else
                                     " -> counts written to pinned host memory by the kernel")),
                        "stage_path": stage_path,
