@@ -230,8 +230,10 @@ ac_status check_layout(ac_ctx* ctx, const ac_windows& s) {
 // `sc` = the scratch set (one per concurrently running stream); `wave_cap` (0
 // = none) limits the launch to that many waves, so another launch's waves can
 // be resident beside it.
+// `no_n` (optional, per segment): the segment's image is known to hold no N.
 ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hipStream_t stream,
-                 bool zero, uint32_t* err = nullptr, int part = 0, uint64_t wave_cap = 0) {
+                 bool zero, uint32_t* err = nullptr, int part = 0, uint64_t wave_cap = 0,
+                 const bool* no_n = nullptr) {
     ac_ctx::Scratch& sc = ctx->sc[part];
     if (ac_status st = check_k(ctx, k)) return st;
     if (n > AC_MAX_SEGS) return fail(ctx, AC_ERR_INVALID, "too many segments in one launch (max 4)");
@@ -289,6 +291,7 @@ ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hi
         d.kmers = s.kmers;
         d.codes = s.sample.codes;
         d.nmask = s.sample.nmask;
+        d.has_n = (no_n && no_n[i]) ? 0u : 1u;
         d.start = s.sample.start;
         d.length = s.sample.length;
         d.n_bases = s.sample.n_bases;
@@ -1268,6 +1271,7 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
     struct Task {
         uint32_t job, w0, w1;
         uint64_t bases;  // image bases the range occupies, then its first image base
+        uint64_t span;   // image bases the range occupies
     };
     uint64_t total_w = 0;
     for (uint32_t j = 0; j < p.n; ++j)
@@ -1277,7 +1281,7 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
     for (uint32_t j = 0; j < p.n; ++j) {
         if (!jobs[j].n_kmers) continue;  // nothing to count: its windows are not needed
         for (uint64_t w = p.lo[j]; w < p.hi[j]; w += per)
-            tasks.push_back({j, (uint32_t)w, (uint32_t)std::min<uint64_t>(p.hi[j], w + per), 0});
+            tasks.push_back({j, (uint32_t)w, (uint32_t)std::min<uint64_t>(p.hi[j], w + per), 0, 0});
     }
     const std::function<void(uint32_t)> span_of = [&](uint32_t t) {
         Task& x = tasks[t];
@@ -1304,6 +1308,7 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
     uint64_t acc[AC_MAX_JOBS] = {};
     for (Task& x : tasks) {
         const uint64_t b = x.bases;
+        x.span = b;
         x.bases = acc[x.job];
         acc[x.job] += b;
     }
@@ -1311,16 +1316,17 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
     for (uint32_t j = 0; j < p.n; ++j) {
         const uint32_t nw = jobs[j].n_kmers ? p.hi[j] - p.lo[j] : 0;
         p.n_bases[j] = std::max<uint64_t>(32, acc[j]);
+        // the N bitmap last: a job without N is sent without it (job by job, below)
         p.off_kmers[j] = off;
         off = align256(off + sizeof(uint64_t) * jobs[j].n_kmers);
         p.off_codes[j] = off;
         off = align256(off + sizeof(uint32_t) * (p.n_bases[j] / 16));
-        p.off_nmask[j] = off;
-        off = align256(off + sizeof(uint32_t) * (p.n_bases[j] / 32));
         p.off_start[j] = off;
         off = align256(off + sizeof(uint64_t) * nw);
         p.off_len[j] = off;
         off = align256(off + sizeof(uint32_t) * nw);
+        p.off_nmask[j] = off;
+        off = align256(off + sizeof(uint32_t) * (p.n_bases[j] / 32));
     }
     p.off_err = off;
     off = align256(off + sizeof(uint32_t));
@@ -1372,13 +1378,24 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
     }
     *(uint32_t*)(h + p.off_err) = 0u;
     mark(1);
+    // per task: did its windows hold an N (its N-bitmap words, or-ed after packing; still in cache)
+    std::vector<uint8_t> task_n(tasks.size(), 0);
     const std::function<void(uint32_t)> pack = [&](uint32_t t) {
         const Task& x = tasks[t];
         const ac_dna5_windows& w = jobs[x.job].sample;
         const uint32_t j = x.job, r = x.w0 - p.lo[j];
-        acamd::pack_dna5_range(w.bases, w.offset, w.length, x.w0, x.w1, x.bases, (uint32_t*)(h + p.off_codes[j]),
-                               (uint32_t*)(h + p.off_nmask[j]), (uint64_t*)(h + p.off_start[j]) + r,
-                               (uint32_t*)(h + p.off_len[j]) + r);
+        uint32_t* nm = (uint32_t*)(h + p.off_nmask[j]);
+        acamd::pack_dna5_range(w.bases, w.offset, w.length, x.w0, x.w1, x.bases, (uint32_t*)(h + p.off_codes[j]), nm,
+                               (uint64_t*)(h + p.off_start[j]) + r, (uint32_t*)(h + p.off_len[j]) + r);
+        uint32_t any = 0;
+        for (uint64_t i = x.bases / 32, e = (x.bases + x.span) / 32; i < e; ++i) any |= nm[i];
+        task_n[t] = any != 0u;
+    };
+    bool no_n[AC_MAX_JOBS] = {};
+    auto job_no_n = [&](uint32_t j) {
+        for (size_t t = 0; t < tasks.size(); ++t)
+            if (tasks[t].job == j && task_n[t]) return false;
+        return true;
     };
     char* d = zc ? (char*)sl.hd : (char*)sl.d;
     // In both modes the kernel writes the error word and the counts straight into the pinned
@@ -1400,12 +1417,14 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
                 const std::function<void(uint32_t)> pack_j = [&](uint32_t t) { pack(t0 + t); };
                 pool.run(t1 - t0, pack_j);
             }
-            AC_HIP(ctx, transfer(p.off_kmers[j], j + 1 < p.n ? p.off_kmers[j + 1] : p.off_err));
+            no_n[j] = job_no_n(j);
+            AC_HIP(ctx, transfer(p.off_kmers[j], no_n[j] ? p.off_nmask[j] : j + 1 < p.n ? p.off_kmers[j + 1] : p.off_err));
             t0 = t1;
         }
         mark(2);
     } else {
         pool.run((uint32_t)tasks.size(), pack);
+        for (uint32_t j = 0; j < p.n; ++j) no_n[j] = job_no_n(j);
         mark(2);
         if (!zc) AC_HIP(ctx, transfer(0, p.off_err));
     }
@@ -1432,7 +1451,7 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
         cap = ctx->resident[P] / wave_div;
     }
     if (ac_status st = launch(ctx, k, segs, p.n, stream, true, d_counts ? nullptr : (uint32_t*)(hd + p.off_err), part,
-                              cap))
+                              cap, no_n))
         return st;
     mark(4);
     mark(5);

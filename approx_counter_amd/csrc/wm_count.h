@@ -40,6 +40,7 @@ struct SegDev {
     uint32_t subq;        // sub-queues per candidate group (proportional to n_windows; a multiple of AC_WAVES_PER_BLOCK)
     uint32_t acc_begin;   // this segment's first slot in LaunchArgs::acc (groups x cands_per_wave slots)
     uint32_t ticket_begin;  // this segment's first group ticket in LaunchArgs::tickets
+    uint32_t has_n;       // 0: the image holds no N (its N bitmap is not read; every word reads as 0)
 };
 
 struct LaunchArgs {

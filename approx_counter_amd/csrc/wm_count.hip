@@ -296,7 +296,8 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
     // fetch in a waterfall loop)
     const uint32_t* codes_p = sg.codes;
     const uint32_t* nmask_p = sg.nmask;
-    uint32_t code_bytes = (uint32_t)(sg.n_bases >> 2), nmask_bytes = (uint32_t)(sg.n_bases >> 3);
+    // (an N-free image: a zero-sized N-bitmap descriptor, whose loads all return 0 without a memory access)
+    uint32_t code_bytes = (uint32_t)(sg.n_bases >> 2), nmask_bytes = sg.has_n ? (uint32_t)(sg.n_bases >> 3) : 0u;
     asm volatile("" : "+s"(codes_p), "+s"(nmask_p), "+s"(code_bytes), "+s"(nmask_bytes));
     Image im;
     im.codes = __builtin_amdgcn_make_buffer_rsrc((void*)codes_p, 0, (int)code_bytes, 0x00020000);

@@ -77,6 +77,27 @@ def test_dna5_bytes_above_4_are_n(counter):
     assert np.array_equal(got, exp) and got[0] == 2 * len(wins)
 
 
+def test_single_n_anywhere_is_seen(counter):
+    """A job is sent and counted without its N bitmap only when none of its windows holds
+    an N: a single N in the first, a middle or the last window (a different pool task each)
+    must still count as a mismatch; an N-free job fused beside it is counted N-free."""
+    rng = np.random.default_rng(41)
+    n, L = 6000, 100
+    base = rng.integers(0, 4, size=(n, L), dtype=np.uint8)
+    pick = base[17, 30:46]
+    kmers = np.array([sum(int(b) << (2 * (15 - i)) for i, b in enumerate(pick))], dtype=np.uint64)
+    clean = [w for w in base]
+    exp_clean = oracle.count_myers(16, kmers, clean, 16)
+    for where in (17, n // 2, n - 1):
+        wins = base.copy()
+        wins[where, 30 + 7 if where == 17 else L - 1] = 4
+        got = counter.count_jobs(16, [(kmers, [w for w in wins]), (kmers, clean)])
+        assert np.array_equal(got[0], oracle.count_myers(16, kmers, [w for w in wins], 16))
+        assert np.array_equal(got[1], exp_clean)
+        if where == 17:  # the N sits inside the k-mer's exact occurrence: one level fewer there
+            assert got[0][0] < exp_clean[0]
+
+
 def test_jobs_equal_image_path_and_repeat(counter):
     """Calls alternating between the two staging slots, growing and shrinking."""
     for trial, (n_k, n_w, wl) in enumerate([(500, 2000, (100, 101)), (37, 50, (0, 300)), (1000, 5000, (150, 151)),
