@@ -231,9 +231,11 @@ ac_status check_layout(ac_ctx* ctx, const ac_windows& s) {
 // = none) limits the launch to that many waves, so another launch's waves can
 // be resident beside it.
 // `no_n` (optional, per segment): the segment's image is known to hold no N.
+// `ulen` (optional, per segment): AC_NO_ULEN, or all windows have this length
+// and sit back to back at ceil32(ulen)-base strides (start / length unread).
 ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hipStream_t stream,
                  bool zero, uint32_t* err = nullptr, int part = 0, uint64_t wave_cap = 0,
-                 const bool* no_n = nullptr) {
+                 const bool* no_n = nullptr, const uint32_t* ulen = nullptr) {
     ac_ctx::Scratch& sc = ctx->sc[part];
     if (ac_status st = check_k(ctx, k)) return st;
     if (n > AC_MAX_SEGS) return fail(ctx, AC_ERR_INVALID, "too many segments in one launch (max 4)");
@@ -292,6 +294,7 @@ ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hi
         d.codes = s.sample.codes;
         d.nmask = s.sample.nmask;
         d.has_n = (no_n && no_n[i]) ? 0u : 1u;
+        d.ulen = ulen ? ulen[i] : AC_NO_ULEN;
         d.start = s.sample.start;
         d.length = s.sample.length;
         d.n_bases = s.sample.n_bases;
@@ -1207,6 +1210,15 @@ int stage_pipe() {
     }();
     return v;
 }
+// Equal-length windows counted with arithmetic descriptors (default;
+// AC_STAGE_ULEN=0 sends and reads the descriptors, A/B)
+int stage_ulen() {
+    static const int v = [] {
+        const char* e = std::getenv("AC_STAGE_ULEN");
+        return e ? (std::atoi(e) != 0 ? 1 : 0) : 1;
+    }();
+    return v;
+}
 constexpr uint32_t BLIT_THREADS = 256, BLIT_UNROLL = 2;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 __global__ void __launch_bounds__(BLIT_THREADS) stage_blit_kernel(const u32x4* __restrict__ src,
@@ -1272,6 +1284,7 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
         uint32_t job, w0, w1;
         uint64_t bases;  // image bases the range occupies, then its first image base
         uint64_t span;   // image bases the range occupies
+        uint32_t min_len, max_len;  // window lengths in the range
     };
     uint64_t total_w = 0;
     for (uint32_t j = 0; j < p.n; ++j)
@@ -1281,14 +1294,21 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
     for (uint32_t j = 0; j < p.n; ++j) {
         if (!jobs[j].n_kmers) continue;  // nothing to count: its windows are not needed
         for (uint64_t w = p.lo[j]; w < p.hi[j]; w += per)
-            tasks.push_back({j, (uint32_t)w, (uint32_t)std::min<uint64_t>(p.hi[j], w + per), 0, 0});
+            tasks.push_back({j, (uint32_t)w, (uint32_t)std::min<uint64_t>(p.hi[j], w + per), 0, 0, ~0u, 0u});
     }
     const std::function<void(uint32_t)> span_of = [&](uint32_t t) {
         Task& x = tasks[t];
         const uint32_t* len = jobs[x.job].sample.length;
         uint64_t b = 0;
-        for (uint32_t w = x.w0; w < x.w1; ++w) b += image_span(len[w]);
+        uint32_t lo = ~0u, hi = 0u;
+        for (uint32_t w = x.w0; w < x.w1; ++w) {
+            b += image_span(len[w]);
+            lo = std::min(lo, len[w]);
+            hi = std::max(hi, len[w]);
+        }
         x.bases = b;
+        x.min_len = lo;
+        x.max_len = hi;
     };
     double tt = g_trace.on ? now_us() : 0.0;
     auto mark = [&](int i) {
@@ -1316,17 +1336,18 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
     for (uint32_t j = 0; j < p.n; ++j) {
         const uint32_t nw = jobs[j].n_kmers ? p.hi[j] - p.lo[j] : 0;
         p.n_bases[j] = std::max<uint64_t>(32, acc[j]);
-        // the N bitmap last: a job without N is sent without it (job by job, below)
+        // the N bitmap, then the window descriptors: a job without N / with equal windows is
+        // sent without them (job by job, below)
         p.off_kmers[j] = off;
         off = align256(off + sizeof(uint64_t) * jobs[j].n_kmers);
         p.off_codes[j] = off;
         off = align256(off + sizeof(uint32_t) * (p.n_bases[j] / 16));
+        p.off_nmask[j] = off;
+        off = align256(off + sizeof(uint32_t) * (p.n_bases[j] / 32));
         p.off_start[j] = off;
         off = align256(off + sizeof(uint64_t) * nw);
         p.off_len[j] = off;
         off = align256(off + sizeof(uint32_t) * nw);
-        p.off_nmask[j] = off;
-        off = align256(off + sizeof(uint32_t) * (p.n_bases[j] / 32));
     }
     p.off_err = off;
     off = align256(off + sizeof(uint32_t));
@@ -1397,6 +1418,17 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
             if (tasks[t].job == j && task_n[t]) return false;
         return true;
     };
+    // equal windows (the common case: every start window sl bases, every end window sl + 1)
+    uint32_t ulen[AC_MAX_JOBS];
+    for (uint32_t j = 0; j < p.n; ++j) {
+        uint32_t lo = ~0u, hi = 0u;
+        for (const Task& x : tasks)
+            if (x.job == j) {
+                lo = std::min(lo, x.min_len);
+                hi = std::max(hi, x.max_len);
+            }
+        ulen[j] = (lo == hi && stage_ulen()) ? lo : AC_NO_ULEN;
+    }
     char* d = zc ? (char*)sl.hd : (char*)sl.d;
     // In both modes the kernel writes the error word and the counts straight into the pinned
     // block (hd), so no copy comes back (profiles/r02_stage_dma_back_ab.log).
@@ -1418,7 +1450,8 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
                 pool.run(t1 - t0, pack_j);
             }
             no_n[j] = job_no_n(j);
-            AC_HIP(ctx, transfer(p.off_kmers[j], no_n[j] ? p.off_nmask[j] : j + 1 < p.n ? p.off_kmers[j + 1] : p.off_err));
+            AC_HIP(ctx, transfer(p.off_kmers[j], no_n[j] ? p.off_nmask[j] : p.off_start[j]));
+            if (ulen[j] == AC_NO_ULEN) AC_HIP(ctx, transfer(p.off_start[j], j + 1 < p.n ? p.off_kmers[j + 1] : p.off_err));
             t0 = t1;
         }
         mark(2);
@@ -1451,7 +1484,7 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
         cap = ctx->resident[P] / wave_div;
     }
     if (ac_status st = launch(ctx, k, segs, p.n, stream, true, d_counts ? nullptr : (uint32_t*)(hd + p.off_err), part,
-                              cap, no_n))
+                              cap, no_n, ulen))
         return st;
     mark(4);
     mark(5);

@@ -21,6 +21,7 @@
 // its set-up broken (the ~Eq table not at LDS address 0) and skipped its work.
 #define AC_DEVERR_WINDOW 1u
 #define AC_DEVERR_SETUP 2u
+#define AC_NO_ULEN 0xffffffffu
 
 namespace acamd {
 
@@ -41,6 +42,8 @@ struct SegDev {
     uint32_t acc_begin;   // this segment's first slot in LaunchArgs::acc (groups x cands_per_wave slots)
     uint32_t ticket_begin;  // this segment's first group ticket in LaunchArgs::tickets
     uint32_t has_n;       // 0: the image holds no N (its N bitmap is not read; every word reads as 0)
+    uint32_t ulen;        // AC_NO_ULEN, or every window has this length and window w starts at base
+                          // w * ceil32(ulen) (start / length are not read)
 };
 
 struct LaunchArgs {

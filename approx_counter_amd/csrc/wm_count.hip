@@ -310,6 +310,18 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
     // lgkmcnt and so would be waited for by the NFA blocks' LDS waits)
     uint32_t* g_queue = a.queue + ((uint64_t)a.bank * a.qstride + sg.queue_begin + g * sg.subq) * AC_QUEUE_LINE;
     asm volatile("" : "+s"(g_start), "+s"(g_length), "+s"(g_nbases));
+    // Equal windows packed back to back (the host-buffer stage's image): descriptors by arithmetic.
+    uint32_t ulen = sg.ulen;
+    asm volatile("" : "+s"(ulen));
+    const uint32_t ustride = ulen == AC_NO_ULEN ? 0u : (ulen + 31u) & ~31u;
+    auto desc = [&](uint32_t ww, uint64_t& base_out, uint32_t& len_out) __attribute__((always_inline)) {
+        if (ulen != AC_NO_ULEN) {
+            base_out = (uint64_t)ww * ustride;
+            len_out = ulen;
+        } else {
+            load_desc(g_start, g_length, ww, base_out, len_out);
+        }
+    };
     const uint32_t m = a.m;
     // An occurrence with <= 2 edits spans >= m - 2 bases: none ends in a window's
     // first m - 3 bases, whose hit accumulation the first block skips (12 of them).
@@ -438,7 +450,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
     Fetch nf = {0u, 0u};
     const uint32_t lane_off = (lane < 16u ? lane : (lane - 16u) & 7u) << 2;  // this lane's word of a segment, in bytes
     if (item < n_items) {
-        load_desc(g_start, g_length, w, nbase, nlen);
+        desc(w, nbase, nlen);
         if (fetchable(nbase, nlen)) tid_fetch(nf, im, nbase, lane, lane_off);
     }
 
@@ -480,7 +492,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
         const bool last = wn >= item_end;  // the item's last window: claim the next item
         uint32_t nitem = n_items;
         if (!last) {
-            load_desc(g_start, g_length, wn, nbase, nlen);
+            desc(wn, nbase, nlen);
         } else {
             pending = dequeue_issue();
         }
@@ -510,7 +522,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
         if (last) {
             nitem = __builtin_amdgcn_readfirstlane(item_of(jc_waves + __builtin_amdgcn_readfirstlane(pending)));
             if (nitem < n_items) {
-                load_desc(g_start, g_length, nitem * chunk, nbase, nlen);
+                desc(nitem * chunk, nbase, nlen);
             }
         } else if (fetchable(nbase, nlen)) {
             tid_fetch(nf, im, nbase, lane, lane_off);
@@ -556,7 +568,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
             if (item >= n_items && S > 1) {
                 item = __builtin_amdgcn_readfirstlane(steal());
                 if (item < n_items) {
-                    load_desc(g_start, g_length, item * chunk, nbase, nlen);
+                    desc(item * chunk, nbase, nlen);
                     if (fetchable(nbase, nlen))
                         tid_fetch(nf, im, nbase, lane, lane_off);
                 }
