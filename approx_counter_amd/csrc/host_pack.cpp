@@ -48,37 +48,38 @@ WorkPool::~WorkPool() {
     for (auto& t : threads_) t.join();
 }
 
-void WorkPool::drain() {
-    const uint32_t n = n_tasks_;
+void WorkPool::drain(uint32_t gen) {
+    const Job& job = jobs_[gen & 1u];
     for (;;) {
-        const uint32_t i = next_.fetch_add(1, std::memory_order_relaxed);
-        if (i >= n) break;
-        (*fn_)(i);
-        done_.fetch_add(1, std::memory_order_release);
+        uint64_t s = state_.load(std::memory_order_acquire);
+        if ((uint32_t)(s >> 32) != gen) return;  // the job is over (a later one is published)
+        const uint32_t i = (uint32_t)s;
+        const std::function<void(uint32_t)>* fn = job.fn.load(std::memory_order_relaxed);
+        const uint32_t n = job.n.load(std::memory_order_relaxed);
+        if (i >= n) return;
+        if (!state_.compare_exchange_weak(s, s + 1, std::memory_order_acq_rel, std::memory_order_relaxed)) continue;
+        (*fn)(i);
+        jobs_[gen & 1u].done.fetch_add(1, std::memory_order_release);
     }
 }
 
 void WorkPool::worker() {
-    uint64_t seen = 0;
+    uint32_t seen = 0;
     for (;;) {
-        // Wait for the next job: spin for spin_ns_, then sleep.  gen_ changes
+        // Wait for the next job: spin for spin_ns_, then sleep.  pub_ changes
         // under m_, so a sleeper cannot miss it.
         const int64_t t0 = now_ns();
         uint32_t polls = 0;
-        while (gen_.load(std::memory_order_acquire) == seen && !stop_.load(std::memory_order_relaxed)) {
+        while (pub_.load(std::memory_order_acquire) == seen && !stop_.load(std::memory_order_relaxed)) {
             cpu_relax();
             if ((++polls & 255u) == 0 && now_ns() - t0 > spin_ns_) {
                 std::unique_lock<std::mutex> lk(m_);
-                cv_.wait(lk, [&] { return gen_.load(std::memory_order_relaxed) != seen || stop_.load(); });
+                cv_.wait(lk, [&] { return pub_.load(std::memory_order_relaxed) != seen || stop_.load(); });
             }
         }
         if (stop_.load()) return;
-        seen = gen_.load(std::memory_order_acquire);
-        drain();
-        // run() returns only once every worker has left drain() for this job,
-        // so no worker can still be reading fn_ / n_tasks_ when the next job
-        // replaces them.
-        acked_.fetch_add(1, std::memory_order_release);
+        seen = pub_.load(std::memory_order_acquire);
+        drain(seen);
     }
 }
 
@@ -88,24 +89,19 @@ void WorkPool::run(uint32_t n, const std::function<void(uint32_t)>& fn) {
         for (uint32_t i = 0; i < n; ++i) fn(i);
         return;
     }
-    fn_ = &fn;
-    n_tasks_ = n;
-    next_.store(0, std::memory_order_relaxed);
-    done_.store(0, std::memory_order_relaxed);
-    acked_.store(0, std::memory_order_relaxed);
+    const uint32_t g = ++gen_;
+    Job& job = jobs_[g & 1u];  // its previous job (g - 2) finished before run(g - 1) started
+    job.fn.store(&fn, std::memory_order_relaxed);
+    job.n.store(n, std::memory_order_relaxed);
+    job.done.store(0, std::memory_order_relaxed);
+    state_.store((uint64_t)g << 32, std::memory_order_release);
     {
         std::lock_guard<std::mutex> l2(m_);
-        gen_.fetch_add(1, std::memory_order_release);
+        pub_.store(g, std::memory_order_release);
     }
     cv_.notify_all();
-    drain();
-    while (done_.load(std::memory_order_acquire) < n) cpu_relax();
-    const uint32_t nw = (uint32_t)threads_.size();
-    uint32_t polls = 0;
-    while (acked_.load(std::memory_order_acquire) < nw) {
-        cpu_relax();
-        if ((++polls & 1023u) == 0) std::this_thread::yield();  // a worker that was asleep is still waking
-    }
+    drain(g);
+    while (job.done.load(std::memory_order_acquire) < n) cpu_relax();
 }
 
 namespace {

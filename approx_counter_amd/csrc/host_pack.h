@@ -34,19 +34,28 @@ public:
 
 private:
     void worker();
-    void drain();
+    void drain(uint32_t gen);
 
+    // A job is published as state_ = gen << 32 | next task; a participant
+    // claims task i by a CAS of state_ from (gen, i) to (gen, i + 1), having
+    // read the job's fn / n from slot gen & 1 before it: state_ only grows, so
+    // a successful CAS proves the slot still held that job.  run() returns once
+    // the job's tasks are done, without waiting for workers that never got to
+    // it (a descheduled spinning worker used to hold every call up).
+    struct Job {
+        std::atomic<const std::function<void(uint32_t)>*> fn{nullptr};
+        std::atomic<uint32_t> n{0};
+        std::atomic<uint32_t> done{0};
+    };
     std::vector<std::thread> threads_;
     std::mutex run_m_;
     std::mutex m_;
     std::condition_variable cv_;
-    std::atomic<uint64_t> gen_{0};
-    std::atomic<uint32_t> next_{0};
-    std::atomic<uint32_t> done_{0};
-    std::atomic<uint32_t> acked_{0};
+    std::atomic<uint64_t> state_{0};
+    std::atomic<uint32_t> pub_{0};  // last published gen (sleepers wait for it to change, under m_)
+    uint32_t gen_ = 0;               // run()'s own counter (under run_m_)
+    Job jobs_[2];
     std::atomic<bool> stop_{false};
-    const std::function<void(uint32_t)>* fn_ = nullptr;
-    uint32_t n_tasks_ = 0;
     int64_t spin_ns_ = 0;
 };
 
