@@ -1284,7 +1284,7 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
         uint32_t job, w0, w1;
         uint64_t bases;  // image bases the range occupies, then its first image base
         uint64_t span;   // image bases the range occupies
-        uint32_t min_len, max_len;  // window lengths in the range
+        uint32_t first_len, len_diff;  // the range's first window length; OR of (length ^ first_len)
     };
     uint64_t total_w = 0;
     for (uint32_t j = 0; j < p.n; ++j)
@@ -1294,21 +1294,20 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
     for (uint32_t j = 0; j < p.n; ++j) {
         if (!jobs[j].n_kmers) continue;  // nothing to count: its windows are not needed
         for (uint64_t w = p.lo[j]; w < p.hi[j]; w += per)
-            tasks.push_back({j, (uint32_t)w, (uint32_t)std::min<uint64_t>(p.hi[j], w + per), 0, 0, ~0u, 0u});
+            tasks.push_back({j, (uint32_t)w, (uint32_t)std::min<uint64_t>(p.hi[j], w + per), 0, 0, 0u, 0u});
     }
     const std::function<void(uint32_t)> span_of = [&](uint32_t t) {
         Task& x = tasks[t];
         const uint32_t* len = jobs[x.job].sample.length;
         uint64_t b = 0;
-        uint32_t lo = ~0u, hi = 0u;
-        for (uint32_t w = x.w0; w < x.w1; ++w) {
-            b += image_span(len[w]);
-            lo = std::min(lo, len[w]);
-            hi = std::max(hi, len[w]);
-        }
+        for (uint32_t w = x.w0; w < x.w1; ++w) b += image_span(len[w]);
+        // (a separate OR-reduction: folded into the loop above, min / max stopped it vectorising: +7 us at cfg2)
+        const uint32_t f = x.w1 > x.w0 ? len[x.w0] : 0u;
+        uint32_t diff = 0;
+        for (uint32_t w = x.w0; w < x.w1; ++w) diff |= len[w] ^ f;
         x.bases = b;
-        x.min_len = lo;
-        x.max_len = hi;
+        x.first_len = f;
+        x.len_diff = diff;
     };
     double tt = g_trace.on ? now_us() : 0.0;
     auto mark = [&](int i) {
@@ -1421,13 +1420,15 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
     // equal windows (the common case: every start window sl bases, every end window sl + 1)
     uint32_t ulen[AC_MAX_JOBS];
     for (uint32_t j = 0; j < p.n; ++j) {
-        uint32_t lo = ~0u, hi = 0u;
+        bool any = false, equal = true;
+        uint32_t l0 = 0;
         for (const Task& x : tasks)
             if (x.job == j) {
-                lo = std::min(lo, x.min_len);
-                hi = std::max(hi, x.max_len);
+                if (!any) l0 = x.first_len;
+                any = true;
+                equal = equal && x.len_diff == 0u && x.first_len == l0;
             }
-        ulen[j] = (lo == hi && stage_ulen()) ? lo : AC_NO_ULEN;
+        ulen[j] = (any && equal && stage_ulen()) ? l0 : AC_NO_ULEN;
     }
     char* d = zc ? (char*)sl.hd : (char*)sl.d;
     // In both modes the kernel writes the error word and the counts straight into the pinned
@@ -1440,20 +1441,38 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
         return hipMemcpyAsync(d + r0, h + r0, r1 - r0, hipMemcpyHostToDevice, stream);
     };
     if (!zc && stage_pipe() && p.n > 1) {
-        // job by job: job j's inputs travel while job j + 1 is packed
+        // job by job: job j's inputs travel while job j + 1 is packed.  One pool job for all
+        // tasks (they are in job order); the caller packs job j's share, waits for its last
+        // task, sends it, then helps with job j + 1 while the workers carry on.
+        std::atomic<uint32_t> left[AC_MAX_JOBS];
+        for (uint32_t j = 0; j < AC_MAX_JOBS; ++j) left[j].store(0, std::memory_order_relaxed);
+        for (const Task& x : tasks) left[x.job].fetch_add(1, std::memory_order_relaxed);
+        const std::function<void(uint32_t)> pack_counted = [&](uint32_t t) {
+            pack(t);
+            left[tasks[t].job].fetch_sub(1, std::memory_order_release);
+        };
+        pool.begin((uint32_t)tasks.size(), pack_counted);
         uint32_t t0 = 0;
         for (uint32_t j = 0; j < p.n; ++j) {
             uint32_t t1 = t0;
             while (t1 < (uint32_t)tasks.size() && tasks[t1].job == j) ++t1;
-            if (t1 > t0) {
-                const std::function<void(uint32_t)> pack_j = [&](uint32_t t) { pack(t0 + t); };
-                pool.run(t1 - t0, pack_j);
-            }
+            pool.help(t1);
+            while (left[j].load(std::memory_order_acquire) != 0u) __builtin_ia32_pause();
             no_n[j] = job_no_n(j);
-            AC_HIP(ctx, transfer(p.off_kmers[j], no_n[j] ? p.off_nmask[j] : p.off_start[j]));
-            if (ulen[j] == AC_NO_ULEN) AC_HIP(ctx, transfer(p.off_start[j], j + 1 < p.n ? p.off_kmers[j + 1] : p.off_err));
+            if (const hipError_t e = transfer(p.off_kmers[j], no_n[j] ? p.off_nmask[j] : p.off_start[j]); e != hipSuccess) {
+                pool.finish();
+                return hip_fail(ctx, e, "stage transfer");
+            }
+            if (ulen[j] == AC_NO_ULEN) {
+                const hipError_t e = transfer(p.off_start[j], j + 1 < p.n ? p.off_kmers[j + 1] : p.off_err);
+                if (e != hipSuccess) {
+                    pool.finish();
+                    return hip_fail(ctx, e, "stage transfer");
+                }
+            }
             t0 = t1;
         }
+        pool.finish();
         mark(2);
     } else {
         pool.run((uint32_t)tasks.size(), pack);

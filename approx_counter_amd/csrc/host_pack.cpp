@@ -48,7 +48,7 @@ WorkPool::~WorkPool() {
     for (auto& t : threads_) t.join();
 }
 
-void WorkPool::drain(uint32_t gen) {
+void WorkPool::drain(uint32_t gen, uint32_t upto) {
     const Job& job = jobs_[gen & 1u];
     for (;;) {
         uint64_t s = state_.load(std::memory_order_acquire);
@@ -56,7 +56,7 @@ void WorkPool::drain(uint32_t gen) {
         const uint32_t i = (uint32_t)s;
         const std::function<void(uint32_t)>* fn = job.fn.load(std::memory_order_relaxed);
         const uint32_t n = job.n.load(std::memory_order_relaxed);
-        if (i >= n) return;
+        if (i >= n || i >= upto) return;
         if (!state_.compare_exchange_weak(s, s + 1, std::memory_order_acq_rel, std::memory_order_relaxed)) continue;
         (*fn)(i);
         jobs_[gen & 1u].done.fetch_add(1, std::memory_order_release);
@@ -84,9 +84,17 @@ void WorkPool::worker() {
 }
 
 void WorkPool::run(uint32_t n, const std::function<void(uint32_t)>& fn) {
-    std::lock_guard<std::mutex> lk(run_m_);
-    if (threads_.empty() || n <= 1) {
-        for (uint32_t i = 0; i < n; ++i) fn(i);
+    begin(n, fn);
+    finish();
+}
+
+void WorkPool::begin(uint32_t n, const std::function<void(uint32_t)>& fn) {
+    held_ = std::unique_lock<std::mutex>(run_m_);
+    n_ = n;
+    serial_ = threads_.empty() || n <= 1;
+    if (serial_) {
+        serial_fn_ = &fn;
+        serial_next_ = 0;
         return;
     }
     const uint32_t g = ++gen_;
@@ -100,8 +108,24 @@ void WorkPool::run(uint32_t n, const std::function<void(uint32_t)>& fn) {
         pub_.store(g, std::memory_order_release);
     }
     cv_.notify_all();
-    drain(g);
-    while (job.done.load(std::memory_order_acquire) < n) cpu_relax();
+}
+
+void WorkPool::help(uint32_t upto) {
+    if (serial_) {
+        for (; serial_next_ < std::min(upto, n_); ++serial_next_) (*serial_fn_)(serial_next_);
+        return;
+    }
+    drain(gen_, upto);
+}
+
+void WorkPool::finish() {
+    if (serial_) {
+        help(n_);
+    } else {
+        drain(gen_);
+        while (jobs_[gen_ & 1u].done.load(std::memory_order_acquire) < n_) cpu_relax();
+    }
+    held_.unlock();
 }
 
 namespace {

@@ -31,10 +31,17 @@ public:
     // fn(i) for every i in [0, n); returns when all have run.  One run() at a
     // time (serialised by a mutex); fn must not call run() itself.
     void run(uint32_t n, const std::function<void(uint32_t)>& fn);
+    // The same in steps, so the caller can act on a prefix of the tasks while
+    // the workers go on with the rest: begin() publishes the job (and holds
+    // the pool until finish()), help(upto) makes the caller run unclaimed tasks
+    // below `upto`, finish() runs what is left and waits for every task.
+    void begin(uint32_t n, const std::function<void(uint32_t)>& fn);
+    void help(uint32_t upto);
+    void finish();
 
 private:
     void worker();
-    void drain(uint32_t gen);
+    void drain(uint32_t gen, uint32_t upto = ~0u);
 
     // A job is published as state_ = gen << 32 | next task; a participant
     // claims task i by a CAS of state_ from (gen, i) to (gen, i + 1), having
@@ -54,6 +61,10 @@ private:
     std::atomic<uint64_t> state_{0};
     std::atomic<uint32_t> pub_{0};  // last published gen (sleepers wait for it to change, under m_)
     uint32_t gen_ = 0;               // run()'s own counter (under run_m_)
+    std::unique_lock<std::mutex> held_;  // run_m_ between begin() and finish()
+    bool serial_ = false;            // begin() without workers (or <= 1 task): the caller runs the tasks
+    uint32_t serial_next_ = 0, n_ = 0;
+    const std::function<void(uint32_t)>* serial_fn_ = nullptr;
     Job jobs_[2];
     std::atomic<bool> stop_{false};
     int64_t spin_ns_ = 0;

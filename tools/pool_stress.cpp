@@ -1,5 +1,5 @@
 // Stress test of the host work pool (approx_counter_amd/csrc/host_pack.cpp), CPU only:
-// many back-to-back run() calls of varying sizes, every task must run exactly once per
+// many back-to-back run() / begin-help-finish calls of varying sizes, every task must run exactly once per
 // call, with the workers' spin time short enough that they also sleep and wake.
 // Built and run by tests/test_host_pool.py; exit status 0 = every check passed.
 #include <atomic>
@@ -19,7 +19,14 @@ int main(int argc, char** argv) {
         const uint32_t n = (uint32_t)((c * 2654435761u) % 257u);  // 0..256 tasks, 0 and 1 included
         for (uint32_t i = 0; i < n; ++i) hits[i].store(0, std::memory_order_relaxed);
         const std::function<void(uint32_t)> fn = [&](uint32_t i) { hits[i].fetch_add(1, std::memory_order_relaxed); };
-        pool.run(n, fn);
+        if (c % 3 == 0) {
+            pool.run(n, fn);
+        } else {  // the stepwise form, as the host-buffer stage uses it: help with prefixes, then finish
+            pool.begin(n, fn);
+            pool.help(n / 3);
+            pool.help(n / 2);
+            pool.finish();
+        }
         for (uint32_t i = 0; i < n; ++i)
             if (hits[i].load(std::memory_order_relaxed) != 1) {
                 std::fprintf(stderr, "call %d: task %u ran %u times (n = %u)\n", c, i, hits[i].load(), n);
