@@ -223,8 +223,10 @@ typedef struct ac_job {
  * synchronous call, host buffers in and out: jobs[j].counts[i] = M1 count of
  * jobs[j].kmers[i] over jobs[j].sample.  The whole stage runs here: the Dna5
  * windows are packed to 2-bit codes + N bitmap by the host worker pool
- * straight into a pinned staging block, sent in one DMA, counted by ONE fused
- * kernel launch over all jobs, and the counts come back in one DMA.  On an
+ * straight into a pinned staging block, read by the kernel over PCIe or sent
+ * into device memory job by job (ac_stage_mode), counted by ONE fused kernel
+ * launch over all jobs (calls of >= 2^17 windows: 2-4 parts, each launched
+ * once it is sent), and the kernel writes the counts into the pinned block.  On an
  * ac_create_multi context every job's windows are split into contiguous shards
  * balanced by bases, one per device, and the shard counts are summed.
  * Replaces the index build (537-541), the OpenMP search loop (547-599) and
@@ -279,8 +281,11 @@ ac_status ac_allreduce_counts(ac_ctx* ctx, uint32_t* d_counts, uint64_t n, void*
 
 /*
  * How ac_error_count_jobs moves the packed inputs (no reference counterpart):
- * 1 = zero-copy (the kernel reads the pinned staging block over PCIe), 0 = one
- * DMA in (either way the kernel writes the counts into the pinned block), -1 =
+ * 1 = zero-copy (the kernel reads the pinned staging block over PCIe), 0 = the
+ * DMA path: each job copied into device memory as soon as it is packed, without
+ * its N bitmap when it holds no N and without window descriptors when its
+ * windows have one length (either way the kernel writes the counts into the
+ * pinned block), -1 =
  * not decided yet.  Unless AC_STAGE_ZEROCOPY=1/0 forces one: a call whose
  * image x candidate groups exceeds 256 MB always takes the DMA (zero-copy may
  * read the image over PCIe once per group) and then reports 0; for smaller
