@@ -1219,7 +1219,13 @@ int stage_ulen() {
     }();
     return v;
 }
-constexpr uint32_t BLIT_THREADS = 256, BLIT_UNROLL = 2;
+#ifndef AC_BLIT_THREADS  // (A/B builds: tools/variants.sh)
+#define AC_BLIT_THREADS 256
+#endif
+#ifndef AC_BLIT_UNROLL
+#define AC_BLIT_UNROLL 2
+#endif
+constexpr uint32_t BLIT_THREADS = AC_BLIT_THREADS, BLIT_UNROLL = AC_BLIT_UNROLL;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 __global__ void __launch_bounds__(BLIT_THREADS) stage_blit_kernel(const u32x4* __restrict__ src,
                                                                   u32x4* __restrict__ dst, uint32_t n16) {
