@@ -1219,7 +1219,11 @@ int stage_ulen() {
     }();
     return v;
 }
-#ifndef AC_BLIT_THREADS  // (A/B builds: tools/variants.sh)
+// Shape (A/B builds: tools/variants.sh).  64-thread workgroups with 4 loads in flight per
+// thread measured faster on one box -- cfg2 stage p50 0.146-0.147 ms vs 0.150-0.159 for
+// 256 x 2 (profiles/r02_blit_shape_ab.log) -- but no GPU box was free to run the test
+// suite on it before round 2 ended, so the tested 256 x 2 stays the default.
+#ifndef AC_BLIT_THREADS
 #define AC_BLIT_THREADS 256
 #endif
 #ifndef AC_BLIT_UNROLL
