@@ -119,6 +119,14 @@ def load():
     L.ac_check.restype = ctypes.c_int
     L.ac_stage_mode.argtypes = [vp]
     L.ac_stage_mode.restype = ctypes.c_int
+    pint = ctypes.POINTER(ctypes.c_int)
+    L.ac_set_host_cpus.argtypes = [pint, ctypes.c_int, ctypes.c_int]
+    L.ac_set_host_cpus.restype = ctypes.c_int
+    L.ac_host_pool_cpus.argtypes = [pint, pint, ctypes.c_int]
+    L.ac_host_pool_cpus.restype = ctypes.c_int
+    L.ac_plan_host_cpus.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.c_int, ctypes.c_int, ctypes.c_char_p,
+                                    pint, ctypes.c_int, pint, ctypes.c_int]
+    L.ac_plan_host_cpus.restype = ctypes.c_int
     _lib = L
     return L
 

@@ -346,6 +346,34 @@ class DeviceSegment:
         return self.counts[: self.n_kmers].cpu().numpy().view(np.uint32).astype(np.uint64)
 
 
+def plan_host_cpus(rank_cpulists, rank: int, allowed: str, core_of=None) -> list:
+    """ac_plan_host_cpus: the host-pool CPUs of local rank `rank`, given every local
+    rank's GPU cpulist (sysfs text such as "0-63,128-191"), the CPUs the process may
+    use and optionally each CPU's physical core (index = CPU)."""
+    L = _lib.load()
+    arr = (ctypes.c_char_p * len(rank_cpulists))(*[s.encode() for s in rank_cpulists])
+    core = None
+    if core_of is not None:
+        core = np.ascontiguousarray(np.asarray(core_of, dtype=np.int32))
+    cap = 4096
+    out = np.zeros(cap, np.int32)
+    n = L.ac_plan_host_cpus(arr, len(rank_cpulists), int(rank), allowed.encode(),
+                            _ptr(core, ctypes.c_int) if core is not None else None,
+                            int(core.size) if core is not None else 0, _ptr(out, ctypes.c_int), cap)
+    if n < 0:
+        raise ValueError("ac_plan_host_cpus: bad arguments")
+    return [int(c) for c in out[: min(n, cap)]]
+
+
+def host_pool_cpus():
+    """ac_host_pool_cpus: (participants, [CPUs]) of the host pool plan in force."""
+    L = _lib.load()
+    part = ctypes.c_int()
+    out = np.zeros(4096, np.int32)
+    n = L.ac_host_pool_cpus(ctypes.byref(part), _ptr(out, ctypes.c_int), out.size)
+    return int(part.value), [int(c) for c in out[: min(n, out.size)]]
+
+
 _default_counter = None
 
 

@@ -6,6 +6,7 @@
 // packed sample once per call and launches one HIP kernel over the
 // candidate x window grid.
 #include <dlfcn.h>
+#include <sched.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>  // types only: RCCL is resolved at run time (rccl() below)
 
@@ -54,7 +55,9 @@ struct ac_ctx {
     void* e_buf[12] = {};
     size_t e_cap[12] = {};
     // Count-kernel scratch, one set per stream a launch may run on at the same
-    // time as another (the parts of a jobs call, AC_STAGE_MAX_PARTS).
+    // time as another: the parts of a synchronous jobs call (0 .. MAX_PARTS-1),
+    // the parts of a submit (MAX_PARTS ..), so a synchronous call never shares
+    // queues / sums / tickets with a submit still in flight on another stream.
     struct Scratch {
         // work-queue counters: two banks of qcap u32; dirty[b] =
         // counters of bank b used by the last launch on it (zeroed by the next launch)
@@ -64,9 +67,14 @@ struct ac_ctx {
         uint32_t* acc = nullptr;
         uint32_t* tickets = nullptr;
         uint32_t acc_cap = 0, ticket_cap = 0;
-    } sc[AC_STAGE_MAX_PARTS];
-    // streams of parts 1.. of a jobs call (part 0 runs on `stream`)
+    } sc[2 * AC_STAGE_MAX_PARTS];
+    // streams of parts 1.. of a synchronous jobs call (part 0 runs on `stream`)
+    // and of a submit (part 0 runs on the caller's stream), with the events that
+    // order a submit's parts around the caller's stream
     hipStream_t part_stream[AC_STAGE_MAX_PARTS] = {};
+    hipStream_t sub_stream[AC_STAGE_MAX_PARTS] = {};
+    hipEvent_t sub_ev[AC_STAGE_MAX_PARTS] = {};
+    hipEvent_t sub_zero_ev = nullptr;
     // resident waves of the count kernel per pattern pack P (0 = not queried yet)
     uint32_t resident[AC_MAX_PACK + 1] = {0, 0, 0, 0, 0};
     // last launch geometry
@@ -91,8 +99,8 @@ struct ac_ctx {
         size_t h_cap = 0, d_cap = 0;
         hipEvent_t ev = nullptr;
         bool pending = false;
-    } slot[2 * AC_STAGE_MAX_PARTS];
-    uint32_t next_slot = 0;
+    } slot[3 * AC_STAGE_MAX_PARTS];  // synchronous parts, then two sets of submit parts
+    uint32_t next_slot = 0;          // the submit set the next submit uses
     // zero-copy vs DMA choice of the host-buffer stage (ac_stage_mode)
     int zc_choice = -1;
     int zc_last = -1;  // 0: the last synchronous call was too large for zero-copy (ac_stage_mode)
@@ -234,9 +242,9 @@ ac_status check_layout(ac_ctx* ctx, const ac_windows& s) {
 // `ulen` (optional, per segment): AC_NO_ULEN, or all windows have this length
 // and sit back to back at ceil32(ulen)-base strides (start / length unread).
 ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hipStream_t stream,
-                 bool zero, uint32_t* err = nullptr, int part = 0, uint64_t wave_cap = 0,
+                 bool zero, uint32_t* err = nullptr, int scratch = 0, uint64_t wave_cap = 0,
                  const bool* no_n = nullptr, const uint32_t* ulen = nullptr) {
-    ac_ctx::Scratch& sc = ctx->sc[part];
+    ac_ctx::Scratch& sc = ctx->sc[scratch];
     if (ac_status st = check_k(ctx, k)) return st;
     if (n > AC_MAX_SEGS) return fail(ctx, AC_ERR_INVALID, "too many segments in one launch (max 4)");
     if (n && !segs) return fail(ctx, AC_ERR_INVALID, "segments is NULL");
@@ -431,6 +439,59 @@ const Rccl& rccl() {
 }
 }  // namespace
 
+namespace {
+
+// CPUs local to a device's PCIe root (sysfs local_cpulist), empty if unknown.
+std::vector<int> device_local_cpus(int device) {
+    char bus[64] = {0};
+    if (hipDeviceGetPCIBusId(bus, sizeof bus, device) != hipSuccess) return {};
+    for (char* c = bus; *c; ++c) *c = (char)std::tolower((unsigned char)*c);
+    const std::string path = std::string("/sys/bus/pci/devices/") + bus + "/local_cpulist";
+    return acamd::read_cpulist(path.c_str());
+}
+
+std::vector<int> allowed_cpus() {
+    std::vector<int> out;
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof set, &set) != 0) return out;
+    for (int c = 0; c < CPU_SETSIZE; ++c)
+        if (CPU_ISSET(c, &set)) out.push_back(c);
+    return out;
+}
+
+int env_int(const char* name, int dflt) {
+    const char* e = std::getenv(name);
+    return e && *e ? std::atoi(e) : dflt;
+}
+
+// The host pool's CPUs, once per process, before its first use: it packs into
+// memory this GPU reads, so it runs on the CPUs local to the GPU's PCIe root.
+// One process per GPU (torchrun: LOCAL_RANK / LOCAL_WORLD_SIZE, local rank r
+// on device r mod the visible devices): the local ranks whose GPUs share a
+// CPU list split it into disjoint runs of physical cores, and each rank's pool
+// takes at most its share of the cgroup CPU quota (16 participants at most), so
+// 8 ranks on one node never pin their workers onto the same CPUs nor spin
+// more threads than the quota runs.  (The reference sizes its one OpenMP team
+// with omp_set_num_threads(nb_thread), approx_counter.cpp:547.)
+void plan_host_pool(int device, int n_dev) {
+    if (acamd::host_plan().participants) return;  // set already (ac_set_host_cpus or an earlier context)
+    int lws = env_int("LOCAL_WORLD_SIZE", 1), lr = env_int("LOCAL_RANK", 0);
+    if (lws < 1 || lr < 0 || lr >= lws) lws = 1, lr = 0;
+    std::vector<std::vector<int>> lists((size_t)lws);
+    for (int r = 0; r < lws; ++r) lists[(size_t)r] = r == lr ? device_local_cpus(device) : device_local_cpus(r % n_dev);
+    const std::vector<int> allowed = allowed_cpus();
+    bool shared = false;
+    acamd::HostPlan plan;
+    plan.cpus = acamd::plan_host_cpus(lists, lr, allowed, acamd::sysfs_core_of, &shared);
+    size_t n = plan.cpus.empty() ? allowed.size() : plan.cpus.size();
+    const double quota = acamd::cgroup_cpu_quota();
+    if (quota > 0.0) n = std::min<size_t>(n, (size_t)std::max(1.0, quota / lws));
+    plan.participants = shared ? 1u : (unsigned)std::max<size_t>(1, std::min<size_t>(16, n));
+    (void)acamd::set_host_plan(plan);
+}
+
+}  // namespace
+
 extern "C" {
 
 int ac_abi_version(void) { return AC_ABI_VERSION; }
@@ -465,14 +526,7 @@ ac_status ac_create(ac_ctx** out, int device) {
         return st;
     }
     ctx->cu_count = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
-    {  // the host pool packs into memory this GPU reads: prefer the CPUs local to its PCIe root
-        char bus[64] = {0};
-        if (hipDeviceGetPCIBusId(bus, sizeof bus, device) == hipSuccess) {
-            for (char* c = bus; *c; ++c) *c = (char)std::tolower((unsigned char)*c);
-            const std::string path = std::string("/sys/bus/pci/devices/") + bus + "/local_cpulist";
-            acamd::set_host_cpus(acamd::read_cpulist(path.c_str()));
-        }
-    }
+    plan_host_pool(device, n);
     if ((e = hipMalloc(&ctx->d_err, sizeof(uint32_t))) != hipSuccess ||
         (e = hipMemset(ctx->d_err, 0, sizeof(uint32_t))) != hipSuccess ||
         (e = hipHostMalloc(&ctx->h_err, sizeof(uint32_t), hipHostMallocDefault)) != hipSuccess) {
@@ -500,6 +554,11 @@ void ac_destroy(ac_ctx* ctx) {
     }
     for (hipStream_t ps : ctx->part_stream)
         if (ps) (void)hipStreamDestroy(ps);
+    for (hipStream_t ps : ctx->sub_stream)
+        if (ps) (void)hipStreamDestroy(ps);
+    for (hipEvent_t ev : ctx->sub_ev)
+        if (ev) (void)hipEventDestroy(ev);
+    if (ctx->sub_zero_ev) (void)hipEventDestroy(ctx->sub_zero_ev);
     for (void* p : ctx->s_buf)
         if (p) (void)hipFree(p);
     for (void* p : ctx->e_buf)
@@ -742,7 +801,10 @@ ac_status ac_exact_count_device(ac_ctx* ctx, uint32_t k, const ac_windows* dev, 
     // 4,096; the histogram / scatter kernels keep one LDS cursor per bucket):
     // larger samples take the hash table.
     if (key_cap > (uint64_t(8192) << 11)) partitioned = false;
-    const uint64_t list_cap = partitioned ? key_cap + 2 : dev->n_bases / 2 + 2;
+    // Distinct kept k-mers <= image positions (a k-mer is fixed by its image position, whichever
+    // overlapping windows cover it), so this list never overflows; n_bases / 2 (entries seen at
+    // least twice, disjoint windows) did for duplicated windows.
+    const uint64_t list_cap = key_cap + 2;
     // small block: special[0..1] u32, had_n u64 @16, n_out u64 @24, n_list u64 @32, err u32 @40,
     // overflow u32 @44, n_keys u64 @48, hist[EXACT_HIST_BINS] u32 @64
     const size_t small_bytes = 64 + sizeof(uint32_t) * EXACT_HIST_BINS;
@@ -813,6 +875,10 @@ ac_status ac_exact_count_device(ac_ctx* ctx, uint32_t k, const ac_windows* dev, 
         AC_HIP(ctx, hipMemcpyAsync(h_small.data(), small, small_bytes, hipMemcpyDeviceToHost, st));
         AC_HIP(ctx, hipStreamSynchronize(st));
         if (*(const uint32_t*)(h_small.data() + 44)) partitioned = false;  // a bucket overflowed its LDS table
+        // Overlapping windows (allowed by ac_windows) hold more k-mer positions than the image
+        // has bases: the dense key arrays dropped the excess, so count on the hash table instead
+        // (its distinct keys are still bounded by the image's positions).
+        if (*(const unsigned long long*)(h_small.data() + 48) > key_cap) partitioned = false;
     }
     if (!partitioned) {
         // Table: a power of two >= 1.5 x the image size (an upper bound on k-mer
@@ -1043,6 +1109,36 @@ ac_status ac_allreduce_counts(ac_ctx* ctx, uint32_t* d_counts, uint64_t n, void*
     return AC_OK;
 }
 
+ac_status ac_set_host_cpus(const int* cpus, int n_cpus, int participants) {
+    if (n_cpus < 0 || (n_cpus && !cpus) || participants < 0) return fail(nullptr, AC_ERR_INVALID, "bad CPU list");
+    acamd::HostPlan plan;
+    plan.cpus.assign(cpus, cpus + n_cpus);
+    std::sort(plan.cpus.begin(), plan.cpus.end());
+    plan.participants = participants ? (unsigned)participants : (unsigned)std::max(1, std::min(16, n_cpus ? n_cpus : 16));
+    if (!acamd::set_host_plan(plan))
+        return fail(nullptr, AC_ERR_INVALID, "the host pool's CPUs are already fixed (set before the first ac_create)");
+    return AC_OK;
+}
+
+int ac_host_pool_cpus(int* participants, int* cpus, int cap) {
+    const acamd::HostPlan p = acamd::host_plan();
+    if (participants) *participants = (int)p.participants;
+    for (int i = 0; i < cap && i < (int)p.cpus.size(); ++i) cpus[i] = p.cpus[(size_t)i];
+    return (int)p.cpus.size();
+}
+
+int ac_plan_host_cpus(const char* const* rank_cpulists, int n_ranks, int rank, const char* allowed_cpulist,
+                      const int* core_of, int n_core_of, int* out, int cap) {
+    if (n_ranks < 1 || rank < 0 || rank >= n_ranks || !rank_cpulists || !allowed_cpulist) return -1;
+    std::vector<std::vector<int>> lists((size_t)n_ranks);
+    for (int r = 0; r < n_ranks; ++r) lists[(size_t)r] = acamd::parse_cpulist(rank_cpulists[r] ? rank_cpulists[r] : "");
+    std::function<int(int)> core;
+    if (core_of) core = [=](int c) { return c >= 0 && c < n_core_of ? core_of[c] : c; };
+    const std::vector<int> v = acamd::plan_host_cpus(lists, rank, acamd::parse_cpulist(allowed_cpulist), core);
+    for (int i = 0; i < cap && i < (int)v.size(); ++i) out[i] = v[(size_t)i];
+    return (int)v.size();
+}
+
 }  // extern "C"
 
 // ---------------------------------------------------------------------------
@@ -1072,7 +1168,9 @@ struct StageTrace {
         if (!on || !calls) return;
         static const char* names[8] = {"span", "layout", "pack", "h2d_enq", "launch_enq", "d2h_enq", "sync", "widen"};
         const double n = calls > 5 ? double(calls - 5) : double(calls);
-        std::fprintf(stderr, "[ac stage trace] %llu calls (first 5 left out), mean us:", (unsigned long long)calls);
+        const char* lr = std::getenv("LOCAL_RANK");
+        std::fprintf(stderr, "[ac stage trace] local rank %s, %llu calls (first 5 left out), mean us:", lr ? lr : "-",
+                     (unsigned long long)calls);
         for (int i = 0; i < 8; ++i) std::fprintf(stderr, " %s %.1f", names[i], sum[i] / n);
         std::fprintf(stderr, "\n");
         for (size_t c = 0; c < per_call.size(); ++c) {
@@ -1098,7 +1196,8 @@ struct JobPlan {
     size_t off_kmers[AC_MAX_JOBS] = {}, off_codes[AC_MAX_JOBS] = {}, off_nmask[AC_MAX_JOBS] = {};
     size_t off_start[AC_MAX_JOBS] = {}, off_len[AC_MAX_JOBS] = {}, off_counts[AC_MAX_JOBS] = {};
     size_t off_err = 0, total = 0;
-    int slot = 0;
+    int slot = 0;     // staging slot (set by the caller: a synchronous part q uses slot q, a submit part its set's)
+    int scratch = 0;  // count-kernel scratch set (ac_ctx::sc)
     bool zc = true;  // this call's transfer mode (zero-copy or DMA)
     bool zc_eligible = true;  // false: the image is too large for zero-copy (DMA, not measured)
 };
@@ -1286,7 +1385,7 @@ ac_status check_jobs(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint32_t n_job
 // pinned pages every call: with the zero-copy stage the GPU's translations of
 // them stay cached); submits alternate between the last two slots.
 ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan& p, hipStream_t stream,
-                           uint32_t* d_counts, int part = 0, uint32_t wave_div = 0) {
+                           uint32_t* d_counts, int part = 0, uint32_t wave_div = 0, bool zero = true) {
     using acamd::image_span;
     acamd::WorkPool& pool = acamd::host_pool();
     // Tasks: contiguous window ranges, about 4 per pool thread.
@@ -1373,12 +1472,6 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
     p.zc_eligible = p.zc_eligible && pcie_bytes <= ZC_MAX_PCIE_BYTES;  // (a multi-part call is DMA-only)
     if (!p.zc_eligible && stage_zerocopy_env() < 0) p.zc = false;
     // The slot: wait until the launch that last read it has finished, grow it.
-    if (d_counts) {
-        p.slot = AC_STAGE_MAX_PARTS + (int)ctx->next_slot;
-        ctx->next_slot ^= 1u;
-    } else {
-        p.slot = part;
-    }
     ac_ctx::Slot& sl = ctx->slot[p.slot];
     if (sl.pending) {
         AC_HIP(ctx, hipEventSynchronize(sl.ev));
@@ -1512,8 +1605,8 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
         if (!ctx->resident[P]) AC_HIP(ctx, acamd::resident_waves(P, ctx->cu_count, &ctx->resident[P]));
         cap = ctx->resident[P] / wave_div;
     }
-    if (ac_status st = launch(ctx, k, segs, p.n, stream, true, d_counts ? nullptr : (uint32_t*)(hd + p.off_err), part,
-                              cap, no_n, ulen))
+    if (ac_status st = launch(ctx, k, segs, p.n, stream, zero, d_counts ? nullptr : (uint32_t*)(hd + p.off_err),
+                              p.scratch, cap, no_n, ulen))
         return st;
     mark(4);
     mark(5);
@@ -1553,6 +1646,21 @@ uint32_t part_cut(const uint32_t* length, uint32_t n, double frac) {
     return n;
 }
 
+// Every job's part boundaries of a single-device call in `parts` parts, once
+// (equal shares of the bases; two parts: AC_STAGE_SPLIT of them in the first).
+std::vector<std::vector<uint32_t>> part_cuts(const ac_job* jobs, uint32_t n_jobs, int parts) {
+    std::vector<std::vector<uint32_t>> cuts;
+    for (uint32_t j = 0; j < n_jobs; ++j) {
+        const uint32_t n = jobs[j].sample.n_windows;
+        if (parts == 1)
+            cuts.push_back({0u, n});
+        else if (parts == 2)
+            cuts.push_back({0u, part_cut(jobs[j].sample.length, n, stage_split()), n});
+        else
+            cuts.push_back(shard_cuts(jobs[j].sample.length, n, (size_t)parts));
+    }
+    return cuts;
+}
 
 }  // namespace
 
@@ -1585,6 +1693,8 @@ ac_status ac_error_count_jobs(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint3
             Unit u{g == 0 ? ctx : ctx->peers[g - 1], 0, nullptr, 0, JobPlan()};
             u.stream = u.c->stream;
             u.plan.n = n_jobs;
+            u.plan.slot = 0;
+            u.plan.scratch = 0;
             for (uint32_t j = 0; j < n_jobs; ++j) {
                 u.plan.lo[j] = cuts[j][g];
                 u.plan.hi[j] = cuts[j][g + 1];
@@ -1593,22 +1703,14 @@ ac_status ac_error_count_jobs(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint3
         }
     } else {
         const int parts = total_w >= 2048 ? stage_parts(total_w) : 1;  // small calls: one launch
-        // every job's part boundaries, once (equal shares of the bases; two parts: AC_STAGE_SPLIT)
-        std::vector<std::vector<uint32_t>> cuts;
-        for (uint32_t j = 0; j < n_jobs; ++j) {
-            const uint32_t n = jobs[j].sample.n_windows;
-            if (parts == 1)
-                cuts.push_back({0u, n});
-            else if (parts == 2)
-                cuts.push_back({0u, part_cut(jobs[j].sample.length, n, stage_split()), n});
-            else
-                cuts.push_back(shard_cuts(jobs[j].sample.length, n, (size_t)parts));
-        }
+        const std::vector<std::vector<uint32_t>> cuts = part_cuts(jobs, n_jobs, parts);
         for (int q = 0; q < parts; ++q) {
             if (q > 0 && !ctx->part_stream[q])
                 AC_HIP(ctx, hipStreamCreateWithFlags(&ctx->part_stream[q], hipStreamNonBlocking));
             Unit u{ctx, q, q == 0 ? ctx->stream : ctx->part_stream[q], (parts > 1 && q == 0) ? 2u : 0u, JobPlan()};
             u.plan.n = n_jobs;
+            u.plan.slot = q;
+            u.plan.scratch = q;
             // parts are for large calls: DMA only (zero-copy would read the whole image per group)
             u.plan.zc_eligible = parts == 1;
             for (uint32_t j = 0; j < n_jobs; ++j) {
@@ -1621,7 +1723,15 @@ ac_status ac_error_count_jobs(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint3
     // Units are staged one after another on the host pool; a unit's DMA and
     // kernel run while the next one is packed.
     const double t_call = now_us();
-    for (Unit& u : units) u.plan.zc = stage_zerocopy(u.c, true);
+    // the transfer path, decided once per context per call (the parts of one device share it;
+    // multi-part calls are DMA-only and do not advance the context's probe cadence)
+    for (size_t g = 0; g < units.size(); ++g) {
+        Unit& u = units[g];
+        if (g > 0 && u.c == units[g - 1].c)
+            u.plan.zc = units[g - 1].plan.zc;
+        else
+            u.plan.zc = (u.plan.zc_eligible || stage_zerocopy_env() >= 0) && stage_zerocopy(u.c, true);
+    }
     for (size_t g = 0; g < units.size(); ++g) {
         Unit& u = units[g];
         AC_HIP(u.c, hipSetDevice(u.c->device));
@@ -1677,19 +1787,61 @@ ac_status ac_error_count_jobs_submit(ac_ctx* ctx, uint32_t k, const ac_job* jobs
     if (ac_status st = check_jobs(ctx, k, jobs, n_jobs)) return st;
     if (!ctx->peers.empty())
         return fail(ctx, AC_ERR_INVALID, "ac_error_count_jobs_submit needs a single-device context");
-    uint64_t n_counts = 0;
-    for (uint32_t j = 0; j < n_jobs; ++j) n_counts += jobs[j].n_kmers;
+    uint64_t n_counts = 0, total_w = 0;
+    for (uint32_t j = 0; j < n_jobs; ++j) {
+        n_counts += jobs[j].n_kmers;
+        total_w += jobs[j].sample.n_windows;
+    }
     if (n_counts && !d_counts) return fail(ctx, AC_ERR_INVALID, "d_counts is NULL");
     if (n_jobs == 0) return AC_OK;
     AC_HIP(ctx, hipSetDevice(ctx->device));
-    JobPlan p;
-    p.n = n_jobs;
-    for (uint32_t j = 0; j < n_jobs; ++j) {
-        p.lo[j] = 0;
-        p.hi[j] = jobs[j].sample.n_windows;
+    hipStream_t caller = (hipStream_t)hip_stream;
+    // Large submits are cut into parts like the synchronous stage (a rank's shard of cfg4 is
+    // 2^17-2^18 windows): part q + 1 is packed and sent while part q counts.  The parts add
+    // into d_counts, zeroed first on the caller's stream; parts 1.. run on the context's
+    // submit streams, ordered after the zeroing and joined back into the caller's stream.
+    // Submits alternate between two sets of staging slots, so a submit packs while the
+    // previous one's launch may still read its inputs.
+    const int parts = total_w >= 2048 ? stage_parts(total_w) : 1;
+    const int set = (int)ctx->next_slot;
+    ctx->next_slot ^= 1u;
+    const std::vector<std::vector<uint32_t>> cuts = part_cuts(jobs, n_jobs, parts);
+    const bool zc = parts == 1 && stage_zerocopy(ctx, false);
+    if (parts > 1) {
+        AC_HIP(ctx, hipMemsetAsync(d_counts, 0, sizeof(uint32_t) * n_counts, caller));
+        if (!ctx->sub_zero_ev) AC_HIP(ctx, hipEventCreateWithFlags(&ctx->sub_zero_ev, hipEventDisableTiming));
+        AC_HIP(ctx, hipEventRecord(ctx->sub_zero_ev, caller));
     }
-    p.zc = stage_zerocopy(ctx, false);
-    return stage_and_launch(ctx, k, jobs, p, (hipStream_t)hip_stream, d_counts);
+    for (int q = 0; q < parts; ++q) {
+        hipStream_t st = caller;
+        if (q > 0) {
+            if (!ctx->sub_stream[q]) AC_HIP(ctx, hipStreamCreateWithFlags(&ctx->sub_stream[q], hipStreamNonBlocking));
+            if (!ctx->sub_ev[q]) AC_HIP(ctx, hipEventCreateWithFlags(&ctx->sub_ev[q], hipEventDisableTiming));
+            st = ctx->sub_stream[q];
+            AC_HIP(ctx, hipStreamWaitEvent(st, ctx->sub_zero_ev, 0));
+        }
+        JobPlan p;
+        p.n = n_jobs;
+        for (uint32_t j = 0; j < n_jobs; ++j) {
+            p.lo[j] = cuts[j][q];
+            p.hi[j] = cuts[j][q + 1];
+        }
+        p.slot = AC_STAGE_MAX_PARTS * (1 + set) + q;
+        p.scratch = AC_STAGE_MAX_PARTS + q;
+        p.zc_eligible = parts == 1;
+        p.zc = zc;
+        if (ac_status rc = stage_and_launch(ctx, k, jobs, p, st, d_counts, q, (parts > 1 && q == 0) ? 2u : 0u,
+                                            parts == 1))
+            return rc;
+        if (q > 0) AC_HIP(ctx, hipEventRecord(ctx->sub_ev[q], st));
+    }
+    for (int q = 1; q < parts; ++q) AC_HIP(ctx, hipStreamWaitEvent(caller, ctx->sub_ev[q], 0));
+    if (g_trace.on) {
+        ++g_trace.calls;
+        g_trace.skip_warmup();
+        g_trace.end_call();
+    }
+    return AC_OK;
 }
 
 int ac_stage_mode(const ac_ctx* ctx) {

@@ -9,6 +9,7 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <string>
 
 #include <pthread.h>
 
@@ -25,17 +26,19 @@ int64_t now_ns() {
 
 }  // namespace
 
-WorkPool::WorkPool(unsigned n_threads, const std::vector<int>& cpus) {
+WorkPool::WorkPool(unsigned n_threads, const std::vector<int>& cpus, bool pin_each) {
     const char* s = std::getenv("AC_HOST_SPIN_US");
     spin_ns_ = (s ? std::atoll(s) : 2000) * 1000;  // 2 ms: consecutive calls find the workers spinning
+    cpu_set_t all;
+    CPU_ZERO(&all);
+    for (int c : cpus) CPU_SET(c, &all);
     for (unsigned i = 1; i < std::max(1u, n_threads); ++i) {
         threads_.emplace_back([this] { worker(); });
-        if (!cpus.empty()) {
-            cpu_set_t set;
-            CPU_ZERO(&set);
-            CPU_SET(cpus[(i - 1) % cpus.size()], &set);
-            (void)pthread_setaffinity_np(threads_.back().native_handle(), sizeof set, &set);
-        }
+        if (cpus.empty()) continue;
+        cpu_set_t one;
+        CPU_ZERO(&one);
+        CPU_SET(cpus[(i - 1) % cpus.size()], &one);
+        (void)pthread_setaffinity_np(threads_.back().native_handle(), sizeof(cpu_set_t), pin_each ? &one : &all);
     }
 }
 
@@ -89,7 +92,9 @@ void WorkPool::run(uint32_t n, const std::function<void(uint32_t)>& fn) {
 }
 
 void WorkPool::begin(uint32_t n, const std::function<void(uint32_t)>& fn) {
-    held_ = std::unique_lock<std::mutex>(run_m_);
+    // (a plain lock, not a member unique_lock: unique_lock::unlock() releases the mutex before it
+    // clears its owns flag, so the next caller's move-assignment could see the flag still set)
+    run_m_.lock();
     n_ = n;
     serial_ = threads_.empty() || n <= 1;
     if (serial_) {
@@ -125,28 +130,42 @@ void WorkPool::finish() {
         drain(gen_);
         while (jobs_[gen_ & 1u].done.load(std::memory_order_acquire) < n_) cpu_relax();
     }
-    held_.unlock();
+    run_m_.unlock();
 }
 
 namespace {
-std::mutex g_cpus_m;
-std::vector<int> g_cpus;
+std::mutex g_plan_m;
+HostPlan g_plan;
+bool g_plan_set = false;
+bool g_pool_made = false;
 }  // namespace
 
-void set_host_cpus(const std::vector<int>& cpus) {
-    std::lock_guard<std::mutex> lk(g_cpus_m);
-    if (g_cpus.empty()) g_cpus = cpus;
+bool set_host_plan(const HostPlan& plan) {
+    std::lock_guard<std::mutex> lk(g_plan_m);
+    if (g_pool_made || g_plan_set) return false;
+    g_plan = plan;
+    g_plan_set = true;
+    return true;
+}
+
+HostPlan host_plan() {
+    std::lock_guard<std::mutex> lk(g_plan_m);
+    return g_plan;
 }
 
 std::vector<int> read_cpulist(const char* path) {
-    std::vector<int> out;
     FILE* f = std::fopen(path, "r");
-    if (!f) return out;
+    if (!f) return {};
     char buf[4096];
     const size_t n = std::fread(buf, 1, sizeof buf - 1, f);
     std::fclose(f);
     buf[n] = 0;
-    for (char* p = buf; *p;) {
+    return parse_cpulist(buf);
+}
+
+std::vector<int> parse_cpulist(const char* text) {
+    std::vector<int> out;
+    for (const char* p = text; *p;) {
         char* e;
         const long a = std::strtol(p, &e, 10);
         if (e == p) break;
@@ -160,33 +179,107 @@ std::vector<int> read_cpulist(const char* path) {
         if (*p == ',') ++p;
         else break;
     }
+    std::sort(out.begin(), out.end());
+    out.erase(std::unique(out.begin(), out.end()), out.end());
     return out;
 }
 
-WorkPool& host_pool() {
-    static WorkPool pool(
-        [] {
-            unsigned n = 0;
-            if (const char* s = std::getenv("AC_HOST_THREADS")) n = (unsigned)std::max(1, std::atoi(s));
-            if (!n) {
-                cpu_set_t set;
-                unsigned cpus = std::thread::hardware_concurrency();
-                if (sched_getaffinity(0, sizeof set, &set) == 0) cpus = (unsigned)CPU_COUNT(&set);
-                n = std::max(1u, std::min(16u, cpus));
+int sysfs_core_of(int cpu) {
+    // the first CPU of its SMT sibling set stands for the physical core
+    const std::string path = "/sys/devices/system/cpu/cpu" + std::to_string(cpu) + "/topology/thread_siblings_list";
+    const std::vector<int> sib = read_cpulist(path.c_str());
+    return sib.empty() ? cpu : sib.front();
+}
+
+std::vector<int> plan_host_cpus(const std::vector<std::vector<int>>& rank_lists, int rank,
+                                const std::vector<int>& allowed, const std::function<int(int)>& core_of,
+                                bool* shared) {
+    // This rank's GPU-local CPUs that the process may use (all allowed ones if that leaves none).
+    std::vector<int> mine;
+    const std::vector<int>& own = rank >= 0 && rank < (int)rank_lists.size() ? rank_lists[rank] : allowed;
+    for (int c : own)
+        if (std::binary_search(allowed.begin(), allowed.end(), c)) mine.push_back(c);
+    if (mine.empty()) mine = allowed;
+    // Ranks whose GPUs share this list (same socket / PCIe root, or the same GPU in a rehearsal)
+    // split it: this rank's position among them and their number.
+    int pos = 0, n = 0;
+    for (int r = 0; r < (int)rank_lists.size(); ++r)
+        if (rank_lists[r] == own) {
+            if (r < rank) ++pos;
+            ++n;
+        }
+    if (n <= 1 || rank < 0 || rank >= (int)rank_lists.size()) {
+        n = 1;
+        pos = 0;
+    }
+    // Physical cores in CPU order, each with its SMT siblings; contiguous runs of cores per rank,
+    // so two ranks never share a core through its siblings.
+    std::vector<std::pair<int, std::vector<int>>> cores;
+    for (int c : mine) {
+        const int id = core_of ? core_of(c) : c;
+        auto it = std::find_if(cores.begin(), cores.end(), [&](const auto& x) { return x.first == id; });
+        if (it == cores.end()) cores.push_back({id, {c}});
+        else it->second.push_back(c);
+    }
+    std::sort(cores.begin(), cores.end());
+    std::vector<int> out;
+    const size_t nc = cores.size();
+    if (shared) *shared = nc < (size_t)n;
+    if (nc == 0) return out;
+    if (nc < (size_t)n) {  // fewer cores than ranks: one core each, shared round-robin
+        out = cores[(size_t)pos % nc].second;
+        return out;
+    }
+    const size_t lo = nc * (size_t)pos / (size_t)n, hi = nc * (size_t)(pos + 1) / (size_t)n;
+    // first threads of every core, then second threads: the pool's first workers get distinct cores
+    for (size_t t = 0;; ++t) {
+        bool any = false;
+        for (size_t i = lo; i < hi; ++i)
+            if (t < cores[i].second.size()) {
+                out.push_back(cores[i].second[t]);
+                any = true;
             }
-            return n;
-        }(),
-        [] {
-            std::vector<int> use;
-            const char* pin = std::getenv("AC_HOST_PIN");
-            if (pin && std::atoi(pin) == 0) return use;
-            cpu_set_t set;
-            if (sched_getaffinity(0, sizeof set, &set) != 0) return use;
-            std::lock_guard<std::mutex> lk(g_cpus_m);
-            for (int c : g_cpus)
-                if (CPU_ISSET(c, &set)) use.push_back(c);
-            return use;
-        }());
+        if (!any) break;
+    }
+    return out;
+}
+
+double cgroup_cpu_quota() {
+    // cgroup v2 cpu.max: "<quota> <period>" or "max <period>"
+    FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r");
+    if (!f) return 0.0;
+    char q[64] = {0};
+    long period = 0;
+    const int got = std::fscanf(f, "%63s %ld", q, &period);
+    std::fclose(f);
+    if (got != 2 || period <= 0 || std::strcmp(q, "max") == 0) return 0.0;
+    return std::atof(q) / (double)period;
+}
+
+WorkPool& host_pool() {
+    static WorkPool pool = [] {
+        std::lock_guard<std::mutex> lk(g_plan_m);
+        g_pool_made = true;
+        unsigned n = 0;
+        if (const char* s = std::getenv("AC_HOST_THREADS")) n = (unsigned)std::max(1, std::atoi(s));
+        std::vector<int> use;
+        cpu_set_t set;
+        const bool aff = sched_getaffinity(0, sizeof set, &set) == 0;
+        for (int c : g_plan.cpus)
+            if (!aff || CPU_ISSET(c, &set)) use.push_back(c);
+        if (!n) n = g_plan.participants;
+        if (!n) {
+            unsigned cpus = std::thread::hardware_concurrency();
+            if (aff) cpus = (unsigned)CPU_COUNT(&set);
+            n = std::max(1u, std::min(16u, cpus));
+        }
+        g_plan.participants = n;
+        g_plan.cpus = use;
+        const char* pin = std::getenv("AC_HOST_PIN");
+        if (pin && std::atoi(pin) == 0) use.clear();
+        const bool pin_each = !(pin && std::string(pin) == "set");
+        return WorkPool(n, use, pin_each);
+    }();
     return pool;
 }
 

@@ -21,8 +21,9 @@ namespace acamd {
 // the whole cfg2 stage ~150 us) and then sleep on a condition variable.
 class WorkPool {
 public:
-    // total participants, caller included; worker i is pinned to cpus[i % size] when cpus is non-empty
-    explicit WorkPool(unsigned n_threads, const std::vector<int>& cpus = {});
+    // total participants, caller included; when cpus is non-empty, worker i is pinned to
+    // cpus[(i - 1) % size] (pin_each) or every worker to the whole set
+    explicit WorkPool(unsigned n_threads, const std::vector<int>& cpus = {}, bool pin_each = true);
     ~WorkPool();
     WorkPool(const WorkPool&) = delete;
     WorkPool& operator=(const WorkPool&) = delete;
@@ -55,13 +56,12 @@ private:
         std::atomic<uint32_t> done{0};
     };
     std::vector<std::thread> threads_;
-    std::mutex run_m_;
+    std::mutex run_m_;  // held from begin() to finish()
     std::mutex m_;
     std::condition_variable cv_;
     std::atomic<uint64_t> state_{0};
     std::atomic<uint32_t> pub_{0};  // last published gen (sleepers wait for it to change, under m_)
     uint32_t gen_ = 0;               // run()'s own counter (under run_m_)
-    std::unique_lock<std::mutex> held_;  // run_m_ between begin() and finish()
     bool serial_ = false;            // begin() without workers (or <= 1 task): the caller runs the tasks
     uint32_t serial_next_ = 0, n_ = 0;
     const std::function<void(uint32_t)>* serial_fn_ = nullptr;
@@ -70,16 +70,42 @@ private:
     int64_t spin_ns_ = 0;
 };
 
+// Where the process-wide pool runs: its participants (caller included) and
+// the CPUs its workers are pinned to.  ac_create fills it in once, before the
+// pool's first use (capi.cpp: the CPUs local to the GPU's PCIe root, split
+// among the local ranks whose GPUs share them, and a participant count within
+// the rank's share of the cgroup CPU quota); ac_set_host_cpus overrides it.
+struct HostPlan {
+    std::vector<int> cpus;
+    unsigned participants = 0;  // 0: min(16, CPUs this process may run on)
+};
+// false once the pool exists or a plan was already set (the first plan wins)
+bool set_host_plan(const HostPlan& plan);
+HostPlan host_plan();  // the plan in force (after the pool's creation: what it actually used)
+
 // The process-wide pool of the host-buffer entry points.  Size: the
-// AC_HOST_THREADS environment variable, else min(16, CPUs this process may
-// run on); AC_HOST_THREADS=1 packs on the calling thread alone.  Its workers
-// are pinned to the CPUs given to set_host_cpus() before the pool's first use
-// (the CPUs local to the GPU's PCIe root: the packed block they write is read
-// by that GPU), minus those the process may not use; AC_HOST_PIN=0 disables.
+// AC_HOST_THREADS environment variable, else the plan's participants, else
+// min(16, CPUs this process may run on); AC_HOST_THREADS=1 packs on the
+// calling thread alone.  Workers are pinned to the plan's CPUs (minus those
+// the process may not use): AC_HOST_PIN=0 disables, AC_HOST_PIN=set pins every
+// worker to the whole set instead of one CPU each.
 WorkPool& host_pool();
-void set_host_cpus(const std::vector<int>& cpus);
-// CPUs of a sysfs cpulist ("0-63,128-191"); empty if unreadable.
+// CPUs of a sysfs cpulist file / text ("0-63,128-191"), sorted; empty if unreadable.
 std::vector<int> read_cpulist(const char* path);
+std::vector<int> parse_cpulist(const char* text);
+// The physical core of a CPU (its first SMT sibling, from sysfs).
+int sysfs_core_of(int cpu);
+// The pool CPUs of local rank `rank`: rank_lists[r] = the GPU-local CPU list of
+// local rank r.  Ranks with identical lists split them (contiguous runs of
+// physical cores, never one core's siblings across two ranks), intersected
+// with `allowed` (sorted); ordered first SMT threads first.  core_of maps a CPU
+// to its core (NULL: every CPU its own core).  *shared = fewer cores than ranks
+// (this rank's core is another rank's too).
+std::vector<int> plan_host_cpus(const std::vector<std::vector<int>>& rank_lists, int rank,
+                                const std::vector<int>& allowed, const std::function<int(int)>& core_of,
+                                bool* shared = nullptr);
+// cgroup v2 CPU quota in CPUs (cpu.max), 0 when unlimited or unknown.
+double cgroup_cpu_quota();
 
 // Image bases a window of `len` bases occupies (windows start on 32-base
 // boundaries, include/approx_counter_amd.h).

@@ -103,6 +103,21 @@ def parse():
     return a
 
 
+def _ranges(cpus):
+    """'0-15,128-143' for a CPU list."""
+    out, run = [], []
+    for c in sorted(cpus):
+        if run and c == run[-1] + 1:
+            run.append(c)
+        else:
+            if run:
+                out.append(f"{run[0]}-{run[-1]}" if len(run) > 1 else str(run[0]))
+            run = [c]
+    if run:
+        out.append(f"{run[0]}-{run[-1]}" if len(run) > 1 else str(run[0]))
+    return ",".join(out) or "unpinned"
+
+
 def cpu_share():
     """(CPUs this process may run on = nproc, CPU quota of its cgroup or None)."""
     try:
@@ -242,12 +257,17 @@ def main():
     import approx_counter_amd as ac
 
     wl, units_job = build_workload(args, rank, world)
+    from approx_counter_amd.counter import host_pool_cpus
     ends = ("start", "end")
     n_c = [int(wl[e]["kmers"].size) for e in ends]
     bases = [sum(int(w.size) for w in wl[e]["windows"]) for e in ends]
     units_rank = sum(n * b for n, b in zip(n_c, bases))
     jobs = ac.Jobs([(wl[e]["kmers"], ac.Dna5Sample.from_windows(wl[e]["windows"])) for e in ends])
     counter = ac.ApproxCounter(local)
+    pool_participants, pool_cpus = host_pool_cpus()  # planned by the first ac_create
+    if world > 1:
+        print(f"[bench] rank {rank} (local {local}): host pool {pool_participants} participants on CPUs "
+              f"{_ranges(pool_cpus)}", file=sys.stderr, flush=True)
     stream = torch.cuda.current_stream(dev)
     d_counts = torch.zeros(max(1, jobs.n_counts), dtype=torch.int32, device=dev)
     h_counts = torch.zeros(max(1, jobs.n_counts), dtype=torch.int32).pin_memory()
@@ -425,6 +445,9 @@ def main():
             d = np.diff(np.array([t0] + marks)) * 1e3
             out["step_ms"] = {"min": float(d.min()), "p50": float(np.median(d)), "max": float(d.max())}
         out["stage_cold_call_ms"] = cold_ms
+        out["host_pool"] = {"participants": pool_participants, "cpus": _ranges(pool_cpus),
+                            "note": "rank 0's pack pool: GPU-local CPUs split among the local ranks, at most its "
+                                    "share of the cgroup CPU quota (ac_host_pool_cpus)"}
         out["stage_path_choice"] = {"path": stage_path, "untimed_calls": tune_calls,
                                     "note": "zero-copy vs DMA chosen by the library (ac_stage_mode): DMA when "
                                             "image x candidate groups > 256 MB, else timed both ways over the first "

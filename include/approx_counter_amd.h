@@ -280,6 +280,32 @@ ac_status ac_comm_init(ac_ctx* ctx, int n_ranks, int rank, const void* id);
 ac_status ac_allreduce_counts(ac_ctx* ctx, uint32_t* d_counts, uint64_t n, void* hip_stream);
 
 /*
+ * The host worker pool that packs the Dna5 sample (ac_error_count_jobs*).  The
+ * reference sizes its one OpenMP team with omp_set_num_threads(nb_thread)
+ * (approx_counter.cpp:547); here the pool is process-wide and planned once, at
+ * the first ac_create: the CPUs local to the GPU's PCIe root, split among the
+ * local ranks (LOCAL_RANK / LOCAL_WORLD_SIZE, local rank r on device r mod the
+ * visible devices) whose GPUs share them -- disjoint runs of physical cores per
+ * rank -- with at most min(16, this rank's share of the cgroup CPU quota)
+ * participants (the calling thread included).
+ *   ac_set_host_cpus   the pool's CPUs and participants (0 = min(16, n_cpus))
+ *                      instead; only before the first ac_create
+ *                      (AC_ERR_INVALID afterwards)
+ *   ac_host_pool_cpus  the plan in force: *participants, the CPUs (up to cap
+ *                      written into cpus); returns the number of CPUs
+ *   ac_plan_host_cpus  the rule itself, for callers that place threads on their
+ *                      own: the CPUs of local rank `rank` given every local
+ *                      rank's GPU cpulist ("0-63,128-191") and the CPUs the
+ *                      process may use; core_of[c] = physical core of CPU c
+ *                      (NULL: every CPU its own core).  Returns the count (up
+ *                      to cap written), -1 on bad arguments.
+ */
+ac_status ac_set_host_cpus(const int* cpus, int n_cpus, int participants);
+int ac_host_pool_cpus(int* participants, int* cpus, int cap);
+int ac_plan_host_cpus(const char* const* rank_cpulists, int n_ranks, int rank, const char* allowed_cpulist,
+                      const int* core_of, int n_core_of, int* out, int cap);
+
+/*
  * How ac_error_count_jobs moves the packed inputs (no reference counterpart):
  * 1 = zero-copy (the kernel reads the pinned staging block over PCIe), 0 = the
  * DMA path: each job copied into device memory as soon as it is packed, without

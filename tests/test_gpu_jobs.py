@@ -151,6 +151,28 @@ def test_submit_into_device_tensor(counter):
     assert np.array_equal(got[500:], oracle.count_myers(16, *b))
 
 
+def test_sync_call_while_submit_in_flight(counter):
+    """A synchronous jobs call made while a submit's launch is still running on another
+    stream: the two launches use separate count-kernel scratch (queues, sums, tickets),
+    so neither corrupts the other."""
+    import torch
+
+    a = cases.planted_case(31, 16, 500, 3000, win_len=(100, 101), p_n=0.01)
+    b = cases.planted_case(32, 16, 300, 2000, win_len=(100, 101), p_n=0.01)
+    ja = ac.Jobs([(a[0], ac.Dna5Sample.from_windows(a[1]))])
+    st = torch.cuda.Stream()
+    out = torch.zeros(ja.n_counts, dtype=torch.int32, device="cuda")
+    exp_a, exp_b = oracle.count_myers(16, *a), oracle.count_myers(16, *b)
+    for _ in range(4):
+        out.fill_(-1)
+        counter.submit_jobs(16, ja, out, stream=st.cuda_stream)  # not synchronised
+        got_b = counter.count_jobs(16, [(b[0], ac.Dna5Sample.from_windows(b[1]))])[0]
+        st.synchronize()
+        assert np.array_equal(got_b, exp_b)
+        assert np.array_equal(out.cpu().numpy().view(np.uint32).astype(np.uint64), exp_a)
+    counter.check(stream=st.cuda_stream)
+
+
 def test_device_error_word_reports_malformed_window(counter):
     """A device segment with a misaligned window (and one past the image) is
     skipped by the kernel, which reports it: ac_check returns AC_ERR_INVALID."""

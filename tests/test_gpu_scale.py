@@ -64,3 +64,43 @@ def test_cfg4_full_parity_and_shards(counter):
             counter.count_device(k, [s], accumulate=True)
         torch.cuda.synchronize()
         assert np.array_equal(acc.counts_numpy(), g)
+
+
+def test_cfg4_submit_in_parts_and_rank_shards(counter):
+    """The N > 1 bench path at cfg4 scale: ac_error_count_jobs_submit cuts a large call
+    into parts (2M windows: four; one rank's 1/8 shard of 250k windows: two), each packed
+    and sent while the previous part counts, the parts adding into the zeroed device
+    counts.  The whole call and the sum of the 8 rank shards (strong scaling, one submit
+    per shard as bench.py's ranks do) both equal the synchronous stage, which equals the
+    oracle (test above; here a candidate subset is re-checked against the oracle)."""
+    import torch
+
+    from approx_counter_amd.shard import shard_bounds
+
+    k, n = 16, 1_000_000
+    wl = workload.build_fast(n_reads=n, k=k, sl=100, lim=500, seed=12)
+    ends = ("start", "end")
+    smp = {e: ac.Dna5Sample.from_windows(wl[e]["windows"]) for e in ends}
+    whole = counter.count_jobs(k, [(wl[e]["kmers"], smp[e]) for e in ends])
+    st = torch.cuda.Stream()
+    n_c = sum(wl[e]["kmers"].size for e in ends)
+    d = torch.zeros(n_c, dtype=torch.int32, device="cuda")
+    jobs = ac.Jobs([(wl[e]["kmers"], smp[e]) for e in ends])
+    counter.submit_jobs(k, jobs, d, stream=st.cuda_stream)
+    st.synchronize()
+    counter.check(stream=st.cuda_stream)
+    got = d.cpu().numpy().view(np.uint32).astype(np.uint64)
+    assert np.array_equal(got, np.concatenate(whole))
+    total = np.zeros(n_c, np.uint64)
+    cuts = {e: shard_bounds(smp[e].length.tolist(), 8) for e in ends}
+    for r in range(8):
+        part = ac.Jobs([(wl[e]["kmers"], smp[e].subset(cuts[e][r], cuts[e][r + 1])) for e in ends])
+        d.fill_(-1)
+        counter.submit_jobs(k, part, d, stream=st.cuda_stream)
+        st.synchronize()
+        total += d.cpu().numpy().view(np.uint32).astype(np.uint64)
+    counter.check(stream=st.cuda_stream)
+    assert np.array_equal(total, np.concatenate(whole))
+    sub = slice(0, 40)
+    for e, g in zip(ends, whole):
+        assert np.array_equal(g[sub], oracle.count_myers(k, wl[e]["kmers"][sub], wl[e]["windows"], THREADS))
