@@ -43,6 +43,10 @@ class ACJob(ctypes.Structure):
     _fields_ = [("kmers", p64), ("n_kmers", ctypes.c_uint32), ("sample", ACDna5Windows), ("counts", p64)]
 
 
+class ACSampleJob(ctypes.Structure):
+    _fields_ = [("kmers", p64), ("n_kmers", ctypes.c_uint32), ("sample", ACWindows), ("counts", p64)]
+
+
 class ApproxCounterError(RuntimeError):
     def __init__(self, status: int, message: str):
         super().__init__(f"[ac_status {status}] {message}")
@@ -106,6 +110,11 @@ def load():
         fn.restype = ctypes.c_int
     L.ac_error_count_sample.argtypes = [vp, ctypes.c_uint32, p64, ctypes.c_uint32, ctypes.POINTER(ACWindows), p64]
     L.ac_error_count_sample.restype = ctypes.c_int
+    L.ac_sample_upload_slot.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ACWindows), ctypes.POINTER(ACWindows)]
+    L.ac_sample_upload_slot.restype = ctypes.c_int
+    for fn in (L.ac_error_count_samples, L.ac_error_count_images):
+        fn.argtypes = [vp, ctypes.c_uint32, ctypes.POINTER(ACSampleJob), ctypes.c_uint32]
+        fn.restype = ctypes.c_int
     L.ac_create_multi.argtypes = [ctypes.POINTER(vp), ctypes.c_int]
     L.ac_create_multi.restype = ctypes.c_int
     L.ac_count.argtypes = [vp, ctypes.c_uint32, p64, ctypes.c_uint32, p32, p32, p64,

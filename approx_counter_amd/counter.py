@@ -15,7 +15,7 @@ import ctypes
 import numpy as np
 
 from . import _lib
-from ._lib import ACDna5Windows, ACJob, ACSegment, ACWindows, check
+from ._lib import ACDna5Windows, ACJob, ACSampleJob, ACSegment, ACWindows, check
 
 _DNA5 = np.full(256, 4, dtype=np.uint8)
 for _c, _v in ((b"A", 0), (b"C", 1), (b"G", 2), (b"T", 3), (b"U", 3)):
@@ -235,6 +235,34 @@ class ApproxCounter:
                                                 ctypes.c_void_p(stream or 0))
         if st:
             check(st, self._h)
+
+    def _sample_jobs(self, fn, k, parts):
+        keep, arr = [], []
+        for km, ws in parts:
+            km = np.ascontiguousarray(np.asarray(km, dtype=np.uint64))
+            c = np.zeros(max(km.size, 1), dtype=np.uint64)
+            keep.append((km, c))
+            arr.append(ACSampleJob(_ptr(km if km.size else np.zeros(1, np.uint64), ctypes.c_uint64), int(km.size), ws,
+                                   _ptr(c, ctypes.c_uint64)))
+        a = (ACSampleJob * len(arr))(*arr)
+        check(fn(self._h, int(k), a, len(arr)), self._h)
+        return [c[: km.size] for km, c in keep]
+
+    def count_images(self, k: int, parts) -> list:
+        """ac_error_count_images: host images [(kmers, PackedSample), ...] (up to 4 jobs) in one
+        fused launch per device (sharded over the devices of an n_gpus context)."""
+        return self._sample_jobs(self._L.ac_error_count_images, k, [(km, smp.as_struct()) for km, smp in parts])
+
+    def upload_sample(self, sample: PackedSample, slot: int = 0) -> ACWindows:
+        """ac_sample_upload_slot: the device copy of a host image (valid until the slot's next upload)."""
+        dev = ACWindows()
+        hw = sample.as_struct()
+        check(self._L.ac_sample_upload_slot(self._h, int(slot), ctypes.byref(hw), ctypes.byref(dev)), self._h)
+        return dev
+
+    def count_samples(self, k: int, parts) -> list:
+        """ac_error_count_samples: [(kmers, device sample from upload_sample), ...], one fused launch."""
+        return self._sample_jobs(self._L.ac_error_count_samples, k, parts)
 
     def stage_mode(self) -> int:
         """ac_stage_mode: 1 zero-copy, 0 DMA, -1 not decided yet (count_jobs probes both first)."""

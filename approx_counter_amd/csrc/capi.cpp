@@ -101,9 +101,11 @@ struct ac_ctx {
         bool pending = false;
     } slot[3 * AC_STAGE_MAX_PARTS];  // synchronous parts, then two sets of submit parts
     uint32_t next_slot = 0;          // the submit set the next submit uses
+    uint32_t gen = 0;                // generation of the last early-launch call (never 0 once used)
+    uint32_t early_flip = 0;         // early-launch calls alternate between staging slots 0 and 1
     // zero-copy vs DMA choice of the host-buffer stage (ac_stage_mode)
     int zc_choice = -1;
-    int zc_last = -1;  // 0: the last synchronous call was too large for zero-copy (ac_stage_mode)
+    int zc_last = -1;  // 0: the last synchronous call was too large for zero-copy, 2: it was an early launch (ac_stage_mode)
     uint32_t zc_probe = 0, zc_calls = 0;
     std::vector<double> zc_us[2];
 };
@@ -158,6 +160,8 @@ ac_status ensure(ac_ctx* ctx, int slot, size_t bytes) { return grow(ctx, &ctx->d
 // Asynchronous on ctx->stream; the block is reused by the next call, so callers
 // synchronise the stream before returning.  `extra` bytes after the arrays are
 // reserved (the counts' way back).
+inline size_t align256(size_t x) { return (x + 255) / 256 * 256; }
+
 size_t staged_bytes(int n, const size_t* sz) {
     size_t total = 0;
     for (int i = 0; i < n; ++i) total += (sz[i] + 255) / 256 * 256;
@@ -218,6 +222,8 @@ inline bool window_ok(uint64_t start, uint32_t length, uint64_t n_bases) {
 
 // Status for a device error word read back after a launch (wm_count.h).
 ac_status device_error(ac_ctx* ctx, uint32_t word) {
+    if (word & AC_DEVERR_STAGE)
+        return fail(ctx, AC_ERR_INTERNAL, "early launch: the kernel timed out waiting for the host's packed inputs");
     if (word & AC_DEVERR_SETUP)
         return fail(ctx, AC_ERR_INTERNAL, "count kernel set-up fault (~Eq table not at LDS 0): its work was skipped");
     if (word & AC_DEVERR_WINDOW)
@@ -241,9 +247,20 @@ ac_status check_layout(ac_ctx* ctx, const ac_windows& s) {
 // `no_n` (optional, per segment): the segment's image is known to hold no N.
 // `ulen` (optional, per segment): AC_NO_ULEN, or all windows have this length
 // and sit back to back at ceil32(ulen)-base strides (start / length unread).
+// Staged launch (the early-launch stage): the kernel copies each
+// segment's region from src (the pinned block) to dst once the host flags it in
+// host_hdr, and reports its completion there.
+struct StageLaunch {
+    uint32_t gen = 0;
+    uint32_t* host_hdr = nullptr;
+    const uint8_t* src[AC_MAX_SEGS] = {};
+    uint8_t* dst[AC_MAX_SEGS] = {};
+    uint32_t chunks[AC_MAX_SEGS] = {};
+};
+
 ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hipStream_t stream,
                  bool zero, uint32_t* err = nullptr, int scratch = 0, uint64_t wave_cap = 0,
-                 const bool* no_n = nullptr, const uint32_t* ulen = nullptr) {
+                 const bool* no_n = nullptr, const uint32_t* ulen = nullptr, const StageLaunch* stage = nullptr) {
     ac_ctx::Scratch& sc = ctx->sc[scratch];
     if (ac_status st = check_k(ctx, k)) return st;
     if (n > AC_MAX_SEGS) return fail(ctx, AC_ERR_INVALID, "too many segments in one launch (max 4)");
@@ -307,6 +324,11 @@ ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hi
         d.length = s.sample.length;
         d.n_bases = s.sample.n_bases;
         d.counts = s.counts;
+        if (stage) {
+            d.stage_src = stage->src[i];
+            d.stage_dst = stage->dst[i];
+            d.stage_chunks = stage->chunks[i];
+        }
         d.n_kmers = s.n_kmers;
         d.n_windows = s.sample.n_windows;
         d.groups = std::max<uint32_t>(1, (s.n_kmers + cpw - 1) / cpw);
@@ -368,11 +390,13 @@ ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hi
     a.err = err ? err : ctx->d_err;
     const uint32_t n_counters = qbegin;
     if (n_counters) wave = std::max<uint64_t>(resident, n_counters);
-    if (n_counters > sc.qcap) {
+    // a staged launch's device words follow its sub-queue counters in the bank (zeroed with them)
+    const uint32_t used = n_counters + (stage ? AC_STAGE_LINES : 0u);
+    if (used > sc.qcap) {
         if (sc.queue) AC_HIP(ctx, hipFree(sc.queue));
         sc.queue = nullptr;
         sc.qcap = 0;
-        const uint32_t cap = std::max<uint32_t>(n_counters, 1024);
+        const uint32_t cap = std::max<uint32_t>(used, 1024);
         const size_t bytes = sizeof(uint32_t) * AC_QUEUE_LINE * 2 * (size_t)cap;
         AC_HIP(ctx, hipMalloc(&sc.queue, bytes));
         AC_HIP(ctx, hipMemsetAsync(sc.queue, 0, bytes, stream));
@@ -385,6 +409,14 @@ ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hi
     a.bank = sc.bank;
     a.zero_count = sc.dirty[sc.bank ^ 1u];
     a.n_queues = std::max<uint32_t>(1, n_counters);
+    if (stage) {
+        a.staged = 1;
+        a.gen = stage->gen;
+        a.host_hdr = stage->host_hdr;
+        a.stage = sc.queue + ((uint64_t)sc.bank * sc.qcap + n_counters) * AC_QUEUE_LINE;
+        a.err = a.stage + AC_STAGE_L_ERR * AC_QUEUE_LINE;
+        a.total_groups = groups_total;
+    }
     // Live segments' queue_begin values are increasing; the kernel picks the
     // last live segment whose queue_begin <= its sub-queue.
     a.total_waves = wave;
@@ -393,7 +425,7 @@ ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hi
     ctx->last_groups = groups_total;
     AC_HIP(ctx, acamd::launch_wm2_count(a, stream));
     if (wave) {  // the launch dequeued from `bank` and zeroed the other one
-        sc.dirty[sc.bank] = n_counters;
+        sc.dirty[sc.bank] = used;
         sc.dirty[sc.bank ^ 1u] = 0;
         sc.bank ^= 1u;
     }
@@ -593,103 +625,133 @@ ac_status ac_error_count_device_accumulate(ac_ctx* ctx, uint32_t k, const ac_seg
 
 namespace {
 
-ac_status error_count_one(ac_ctx* ctx, uint32_t k, const uint64_t* kmers, uint32_t n_kmers,
-                          const ac_windows* sample, uint64_t* counts) {
+// errorCount (approx_counter.cpp:531-601) for up to AC_MAX_JOBS host images on
+// one device, ONE fused launch: every job's k-mers and image go up through the
+// pinned staging block (h2d_staged), the counts and the device error word come
+// back in one copy.  jobs[j].sample holds host pointers.
+ac_status count_images_one(ac_ctx* ctx, uint32_t k, const ac_sample_job* jobs, uint32_t n) {
     if (!ctx) return fail(nullptr, AC_ERR_INVALID, "ctx is NULL");
     if (ac_status st = check_k(ctx, k)) return st;
-    if (n_kmers == 0) return AC_OK;
-    if (!kmers || !counts || !sample) return fail(ctx, AC_ERR_INVALID, "NULL argument");
-    const ac_windows& s = *sample;
-    if (s.n_bases % 32 || s.n_bases >= AC_MAX_IMAGE_BASES)
-        return fail(ctx, AC_ERR_INVALID, "sample n_bases must be a multiple of 32 below 2^34");
-    if (s.n_windows && (!s.codes || !s.nmask || !s.start || !s.length))
-        return fail(ctx, AC_ERR_INVALID, "sample has a NULL array");
-    if (ac_status st = check_layout(ctx, s)) return st;
+    if (n > AC_MAX_JOBS) return fail(ctx, AC_ERR_INVALID, "too many jobs in one call (max 4)");
+    uint64_t total_k = 0;
+    for (uint32_t j = 0; j < n; ++j) {
+        const ac_sample_job& b = jobs[j];
+        if (b.n_kmers && (!b.kmers || !b.counts)) return fail(ctx, AC_ERR_INVALID, "NULL argument");
+        if (ac_status st = check_sample(ctx, &b.sample)) return st;
+        if (ac_status st = check_layout(ctx, b.sample)) return st;
+        total_k += b.n_kmers;
+    }
+    if (total_k == 0) return AC_OK;
     AC_HIP(ctx, hipSetDevice(ctx->device));
-    // Device block: kmers | codes | nmask | start | length | err | counts,
-    // each 256-B aligned, filled through the pinned staging block
-    // (h2d_staged; the device error word goes up as a zero with the inputs).
+    // Device block: per job kmers | codes | nmask | start | length, then err | counts of every
+    // job, each 256-B aligned (the staging offsets; the error word goes up as a zero).
     static const uint32_t zero_word = 0;
-    const size_t sz[7] = {sizeof(uint64_t) * n_kmers, sizeof(uint32_t) * (s.n_bases / 16),
-                          sizeof(uint32_t) * (s.n_bases / 32), sizeof(uint64_t) * s.n_windows,
-                          sizeof(uint32_t) * s.n_windows, sizeof(uint32_t), sizeof(uint32_t) * n_kmers};
-    const void* src[6] = {kmers, s.codes, s.nmask, s.start, s.length, &zero_word};
-    size_t off[8];
-    off[0] = 0;
-    for (int i = 0; i < 7; ++i) off[i + 1] = (off[i] + sz[i] + 255) / 256 * 256;
-    if (ac_status rc = grow(ctx, &ctx->d_stage, &ctx->d_stage_cap, off[7])) return rc;
+    std::vector<const void*> src;
+    std::vector<size_t> sz;
+    for (uint32_t j = 0; j < n; ++j) {
+        const ac_windows& w = jobs[j].sample;
+        src.insert(src.end(), {jobs[j].kmers, w.codes, w.nmask, w.start, w.length});
+        sz.insert(sz.end(), {sizeof(uint64_t) * jobs[j].n_kmers, sizeof(uint32_t) * (w.n_bases / 16),
+                             sizeof(uint32_t) * (w.n_bases / 32), sizeof(uint64_t) * w.n_windows,
+                             sizeof(uint32_t) * w.n_windows});
+    }
+    src.push_back(&zero_word);
+    sz.push_back(sizeof(uint32_t));
+    const size_t in_bytes = staged_bytes((int)sz.size(), sz.data());
+    size_t back = 0;
+    for (uint32_t j = 0; j < n; ++j) back += align256(sizeof(uint32_t) * jobs[j].n_kmers);
+    if (ac_status rc = grow(ctx, &ctx->d_stage, &ctx->d_stage_cap, in_bytes + back)) return rc;
     char* d = (char*)ctx->d_stage;
-    // the error word and the counts come back into the staging block
-    if (ac_status rc = h2d_staged(ctx, 6, src, sz, d, (sz[6] + 255) / 256 * 256)) return rc;
+    if (ac_status rc = h2d_staged(ctx, (int)sz.size(), src.data(), sz.data(), d, back)) return rc;
     char* h = (char*)ctx->h_stage;
+    const size_t off_err = in_bytes - align256(sizeof(uint32_t));
+    ac_segment seg[AC_MAX_JOBS];
+    size_t off = 0, coff = in_bytes;
+    size_t c_off[AC_MAX_JOBS];
+    for (uint32_t j = 0; j < n; ++j) {
+        const ac_windows& w = jobs[j].sample;
+        size_t o[5];
+        for (int i = 0; i < 5; ++i) {
+            o[i] = off;
+            off += align256(sz[5 * j + i]);
+        }
+        seg[j].kmers = (const uint64_t*)(d + o[0]);
+        seg[j].n_kmers = jobs[j].n_kmers;
+        seg[j].sample = ac_windows{(const uint32_t*)(d + o[1]), (const uint32_t*)(d + o[2]), (const uint64_t*)(d + o[3]),
+                                   (const uint32_t*)(d + o[4]), w.n_windows, w.n_bases};
+        seg[j].counts = (uint32_t*)(d + coff);
+        c_off[j] = coff;
+        coff += align256(sizeof(uint32_t) * jobs[j].n_kmers);
+    }
     hipStream_t st = ctx->stream;
-    ac_segment seg;
-    seg.kmers = (const uint64_t*)(d + off[0]);
-    seg.n_kmers = n_kmers;
-    seg.sample.codes = (const uint32_t*)(d + off[1]);
-    seg.sample.nmask = (const uint32_t*)(d + off[2]);
-    seg.sample.start = (const uint64_t*)(d + off[3]);
-    seg.sample.length = (const uint32_t*)(d + off[4]);
-    seg.sample.n_windows = s.n_windows;
-    seg.sample.n_bases = s.n_bases;
-    seg.counts = (uint32_t*)(d + off[6]);
-    if (ac_status rc = launch(ctx, k, &seg, 1, st, true, (uint32_t*)(d + off[5]))) return rc;
-    AC_HIP(ctx, hipMemcpyAsync(h + off[5], d + off[5], off[6] - off[5] + sz[6], hipMemcpyDeviceToHost, st));
+    if (ac_status rc = launch(ctx, k, seg, n, st, true, (uint32_t*)(d + off_err))) return rc;
+    AC_HIP(ctx, hipMemcpyAsync(h + off_err, d + off_err, coff - off_err, hipMemcpyDeviceToHost, st));
     AC_HIP(ctx, hipStreamSynchronize(st));
-    if (ac_status rc = device_error(ctx, *(const uint32_t*)(h + off[5]))) return rc;
-    const uint32_t* hc = (const uint32_t*)(h + off[6]);
-    for (uint32_t i = 0; i < n_kmers; ++i) counts[i] = hc[i];
+    if (ac_status rc = device_error(ctx, *(const uint32_t*)(h + off_err))) return rc;
+    for (uint32_t j = 0; j < n; ++j) {
+        const uint32_t* hc = (const uint32_t*)(h + c_off[j]);
+        for (uint32_t i = 0; i < jobs[j].n_kmers; ++i) jobs[j].counts[i] = hc[i];
+    }
     return AC_OK;
 }
 
-}  // namespace
-
-extern "C" {
-
-ac_status ac_error_count(ac_ctx* ctx, uint32_t k, const uint64_t* kmers, uint32_t n_kmers,
-                         const ac_windows* sample, uint64_t* counts) {
-    if (!ctx || ctx->peers.empty()) return error_count_one(ctx, k, kmers, n_kmers, sample, counts);
+// The same over an ac_create_multi context: every job's windows cut into one
+// contiguous shard per device (balanced by bases), each device counting its
+// shards of all jobs in one fused launch, the shard counts summed on the host.
+ac_status count_images(ac_ctx* ctx, uint32_t k, const ac_sample_job* jobs, uint32_t n) {
+    if (!ctx || ctx->peers.empty()) return count_images_one(ctx, k, jobs, n);
     if (ac_status st = check_k(ctx, k)) return st;
-    if (n_kmers == 0) return AC_OK;
-    if (!kmers || !counts || !sample) return fail(ctx, AC_ERR_INVALID, "NULL argument");
-    if (ac_status st = check_sample(ctx, sample)) return st;
-    const ac_windows& s = *sample;
-    if (ac_status st = check_layout(ctx, s)) return st;
-    // Shards: contiguous window ranges balanced by bases; shard g is a slice of
-    // the image (codes/nmask from its first window's start), starts rebased.
+    if (n > AC_MAX_JOBS) return fail(ctx, AC_ERR_INVALID, "too many jobs in one call (max 4)");
+    for (uint32_t j = 0; j < n; ++j) {
+        if (jobs[j].n_kmers && (!jobs[j].kmers || !jobs[j].counts)) return fail(ctx, AC_ERR_INVALID, "NULL argument");
+        if (ac_status st = check_sample(ctx, &jobs[j].sample)) return st;
+        if (ac_status st = check_layout(ctx, jobs[j].sample)) return st;
+    }
     const size_t G = ctx->peers.size() + 1;
-    uint64_t total = 0;
-    for (uint32_t i = 0; i < s.n_windows; ++i) total += s.length[i];
-    std::vector<uint32_t> cut(G + 1, s.n_windows);
-    cut[0] = 0;
-    {
+    // shard g of job j: windows [cut[j][g], cut[j][g + 1]), a slice of the image from its
+    // lowest start to its highest end (windows may come in any order and overlap;
+    // window_ok guarantees start + length <= n_bases, so nothing here wraps)
+    std::vector<std::vector<uint32_t>> cut(n);
+    for (uint32_t j = 0; j < n; ++j) {
+        const ac_windows& s = jobs[j].sample;
+        uint64_t total = 0;
+        for (uint32_t i = 0; i < s.n_windows; ++i) total += s.length[i];
+        cut[j].assign(G + 1, s.n_windows);
+        cut[j][0] = 0;
         uint64_t acc = 0;
         size_t g = 1;
         for (uint32_t i = 0; i < s.n_windows && g < G; ++i) {
             acc += s.length[i];
-            while (g < G && acc * G >= total * g) cut[g++] = i + 1;
+            while (g < G && acc * G >= total * g) cut[j][g++] = i + 1;
         }
     }
-    std::vector<std::vector<uint64_t>> part(G, std::vector<uint64_t>(n_kmers, 0));
+    std::vector<std::vector<std::vector<uint64_t>>> part(G, std::vector<std::vector<uint64_t>>(n));
     std::vector<ac_status> rc(G, AC_OK);
     auto run = [&](size_t g) {
         ac_ctx* c = g == 0 ? ctx : ctx->peers[g - 1];
-        const uint32_t lo = cut[g], hi = cut[g + 1];
-        if (hi == lo) return;
-        // The shard's slice of the image spans its lowest start to its highest
-        // end: windows may come in any order and overlap (window_ok above
-        // guarantees start + length <= n_bases, so nothing here wraps).
-        uint64_t b0 = s.start[lo], b1 = 0;
-        for (uint32_t i = lo; i < hi; ++i) {
-            b0 = std::min<uint64_t>(b0, s.start[i]);
-            b1 = std::max<uint64_t>(b1, s.start[i] + s.length[i]);
+        ac_sample_job sj[AC_MAX_JOBS];
+        std::vector<std::vector<uint64_t>> st(n);
+        uint32_t m = 0;
+        for (uint32_t j = 0; j < n; ++j) {
+            const ac_windows& s = jobs[j].sample;
+            const uint32_t lo = cut[j][g], hi = cut[j][g + 1];
+            part[g][j].assign(jobs[j].n_kmers, 0);
+            if (hi == lo || !jobs[j].n_kmers) continue;
+            uint64_t b0 = s.start[lo], b1 = 0;
+            for (uint32_t i = lo; i < hi; ++i) {
+                b0 = std::min<uint64_t>(b0, s.start[i]);
+                b1 = std::max<uint64_t>(b1, s.start[i] + s.length[i]);
+            }
+            b1 = std::max<uint64_t>(b0 + 32, (b1 + 31) / 32 * 32);  // empty windows still count (k = 2: d = 2)
+            if (b1 > s.n_bases) b1 = s.n_bases;  // b0 + 32 <= n_bases: b0 is a 32-aligned start < n_bases or 0
+            st[j].resize(hi - lo);
+            for (uint32_t i = lo; i < hi; ++i) st[j][i - lo] = s.start[i] - b0;
+            sj[m++] = ac_sample_job{jobs[j].kmers, jobs[j].n_kmers,
+                                    ac_windows{s.codes + b0 / 16, s.nmask + b0 / 32, st[j].data(), s.length + lo, hi - lo,
+                                               b1 - b0},
+                                    part[g][j].data()};
         }
-        b1 = std::max<uint64_t>(b0 + 32, (b1 + 31) / 32 * 32);  // empty windows still count (k = 2: d = 2)
-        if (b1 > s.n_bases) b1 = s.n_bases;  // b0 + 32 <= n_bases: b0 is a 32-aligned start < n_bases or 0
-        std::vector<uint64_t> st(hi - lo);
-        for (uint32_t i = lo; i < hi; ++i) st[i - lo] = s.start[i] - b0;
-        const ac_windows w{s.codes + b0 / 16, s.nmask + b0 / 32, st.data(), s.length + lo, hi - lo, b1 - b0};
-        rc[g] = error_count_one(c, k, kmers, n_kmers, &w, part[g].data());
+        if (m) rc[g] = count_images_one(c, k, sj, m);
     };
     std::vector<std::thread> th;
     for (size_t g = 1; g < G; ++g) th.emplace_back(run, g);
@@ -700,12 +762,32 @@ ac_status ac_error_count(ac_ctx* ctx, uint32_t k, const uint64_t* kmers, uint32_
             ac_ctx* c = g == 0 ? ctx : ctx->peers[g - 1];
             return fail(ctx, rc[g], "shard " + std::to_string(g) + ": " + c->err);
         }
-    for (uint32_t i = 0; i < n_kmers; ++i) {
-        uint64_t v = 0;
-        for (size_t g = 0; g < G; ++g) v += part[g][i];
-        counts[i] = v;
-    }
+    for (uint32_t j = 0; j < n; ++j)
+        for (uint32_t i = 0; i < jobs[j].n_kmers; ++i) {
+            uint64_t v = 0;
+            for (size_t g = 0; g < G; ++g) v += part[g][j][i];
+            jobs[j].counts[i] = v;
+        }
     return AC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+ac_status ac_error_count(ac_ctx* ctx, uint32_t k, const uint64_t* kmers, uint32_t n_kmers,
+                         const ac_windows* sample, uint64_t* counts) {
+    if (!ctx) return fail(nullptr, AC_ERR_INVALID, "ctx is NULL");
+    if (ac_status st = check_k(ctx, k)) return st;
+    if (n_kmers == 0) return AC_OK;
+    if (!kmers || !counts || !sample) return fail(ctx, AC_ERR_INVALID, "NULL argument");
+    const ac_sample_job job{kmers, n_kmers, *sample, counts};
+    return count_images(ctx, k, &job, 1);
+}
+
+ac_status ac_error_count_images(ac_ctx* ctx, uint32_t k, const ac_sample_job* jobs, uint32_t n_jobs) {
+    if (n_jobs && !jobs) return fail(ctx, AC_ERR_INVALID, "jobs is NULL");
+    return count_images(ctx, k, jobs, n_jobs);
 }
 
 ac_status ac_create_multi(ac_ctx** out, int n_gpus) {
@@ -748,19 +830,20 @@ ac_status ac_count(ac_ctx* ctx, uint32_t k, const uint64_t* kmers, uint32_t n_km
     return ac_error_count(ctx, k, kmers, n_kmers, &w, counts_out);
 }
 
-ac_status ac_sample_upload(ac_ctx* ctx, const ac_windows* host, ac_windows* dev) {
+ac_status ac_sample_upload_slot(ac_ctx* ctx, int slot, const ac_windows* host, ac_windows* dev) {
     if (!ctx || !dev) return fail(ctx, AC_ERR_INVALID, "ctx or dev is NULL");
+    if (slot < 0 || slot >= AC_MAX_JOBS) return fail(ctx, AC_ERR_INVALID, "upload slot outside [0, AC_MAX_JOBS)");
     if (ac_status st = check_sample(ctx, host)) return st;
     if (ac_status st = check_layout(ctx, *host)) return st;  // on the host copy
     AC_HIP(ctx, hipSetDevice(ctx->device));
     const size_t sz[4] = {sizeof(uint32_t) * (host->n_bases / 16), sizeof(uint32_t) * (host->n_bases / 32),
                           sizeof(uint64_t) * host->n_windows, sizeof(uint32_t) * host->n_windows};
     const void* src[4] = {host->codes, host->nmask, host->start, host->length};
-    // one device block (s_buf[0]) holding the four arrays at the staging offsets
-    if (ac_status st = grow(ctx, &ctx->s_buf[0], &ctx->s_cap[0], staged_bytes(4, sz))) return st;
-    if (ac_status st = h2d_staged(ctx, 4, src, sz, ctx->s_buf[0])) return st;
+    // one device block (s_buf[slot]) holding the four arrays at the staging offsets
+    if (ac_status st = grow(ctx, &ctx->s_buf[slot], &ctx->s_cap[slot], staged_bytes(4, sz))) return st;
+    if (ac_status st = h2d_staged(ctx, 4, src, sz, ctx->s_buf[slot])) return st;
     AC_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    const char* blk = (const char*)ctx->s_buf[0];
+    const char* blk = (const char*)ctx->s_buf[slot];
     size_t off = 0;
     const void* at[4];
     for (int i = 0; i < 4; ++i) {
@@ -774,6 +857,10 @@ ac_status ac_sample_upload(ac_ctx* ctx, const ac_windows* host, ac_windows* dev)
     dev->n_windows = host->n_windows;
     dev->n_bases = host->n_bases;
     return AC_OK;
+}
+
+ac_status ac_sample_upload(ac_ctx* ctx, const ac_windows* host, ac_windows* dev) {
+    return ac_sample_upload_slot(ctx, 0, host, dev);
 }
 
 ac_status ac_exact_count_device(ac_ctx* ctx, uint32_t k, const ac_windows* dev, float lc_threshold,
@@ -996,29 +1083,52 @@ ac_status ac_exact_count(ac_ctx* ctx, uint32_t k, const ac_windows* host, float 
                                  counts_out, capacity, n_out, n_distinct, had_n);
 }
 
+ac_status ac_error_count_samples(ac_ctx* ctx, uint32_t k, const ac_sample_job* jobs, uint32_t n_jobs) {
+    if (!ctx) return fail(nullptr, AC_ERR_INVALID, "ctx is NULL");
+    if (ac_status st = check_k(ctx, k)) return st;
+    if (n_jobs > AC_MAX_JOBS) return fail(ctx, AC_ERR_INVALID, "too many jobs in one call (max 4)");
+    if (n_jobs && !jobs) return fail(ctx, AC_ERR_INVALID, "jobs is NULL");
+    uint64_t total = 0;
+    for (uint32_t j = 0; j < n_jobs; ++j) {
+        if (jobs[j].n_kmers && (!jobs[j].kmers || !jobs[j].counts)) return fail(ctx, AC_ERR_INVALID, "NULL argument");
+        if (ac_status st = check_sample(ctx, &jobs[j].sample)) return st;
+        total += jobs[j].n_kmers;
+    }
+    if (total == 0) return AC_OK;
+    AC_HIP(ctx, hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    // every job's k-mers in one upload (d_buf[0]); uint32 counts in d_buf[5], one D2H
+    std::vector<uint64_t> km;
+    km.reserve(total);
+    for (uint32_t j = 0; j < n_jobs; ++j) km.insert(km.end(), jobs[j].kmers, jobs[j].kmers + jobs[j].n_kmers);
+    if (ac_status s2 = ensure(ctx, 0, sizeof(uint64_t) * total)) return s2;
+    if (ac_status s2 = ensure(ctx, 5, sizeof(uint32_t) * total)) return s2;
+    AC_HIP(ctx, hipMemcpyAsync(ctx->d_buf[0], km.data(), sizeof(uint64_t) * total, hipMemcpyHostToDevice, st));
+    ac_segment seg[AC_MAX_JOBS];
+    uint64_t base = 0;
+    for (uint32_t j = 0; j < n_jobs; ++j) {
+        seg[j].kmers = (const uint64_t*)ctx->d_buf[0] + base;
+        seg[j].n_kmers = jobs[j].n_kmers;
+        seg[j].sample = jobs[j].sample;
+        seg[j].counts = (uint32_t*)ctx->d_buf[5] + base;
+        base += jobs[j].n_kmers;
+    }
+    if (ac_status rc = launch(ctx, k, seg, n_jobs, st, true)) return rc;
+    ctx->h_counts.resize(total);
+    AC_HIP(ctx, hipMemcpyAsync(ctx->h_counts.data(), ctx->d_buf[5], sizeof(uint32_t) * total, hipMemcpyDeviceToHost, st));
+    if (ac_status rc = ac_check(ctx, st)) return rc;  // synchronises the stream
+    base = 0;
+    for (uint32_t j = 0; j < n_jobs; ++j)
+        for (uint32_t i = 0; i < jobs[j].n_kmers; ++i) jobs[j].counts[i] = ctx->h_counts[base++];
+    return AC_OK;
+}
+
 ac_status ac_error_count_sample(ac_ctx* ctx, uint32_t k, const uint64_t* kmers, uint32_t n_kmers,
                                 const ac_windows* dev, uint64_t* counts) {
     if (!ctx) return fail(nullptr, AC_ERR_INVALID, "ctx is NULL");
-    if (ac_status st = check_k(ctx, k)) return st;
-    if (n_kmers == 0) return AC_OK;
-    if (!kmers || !counts) return fail(ctx, AC_ERR_INVALID, "NULL argument");
-    if (ac_status st = check_sample(ctx, dev)) return st;
-    AC_HIP(ctx, hipSetDevice(ctx->device));
-    hipStream_t st = ctx->stream;
-    if (ac_status s2 = ensure(ctx, 0, sizeof(uint64_t) * n_kmers)) return s2;
-    if (ac_status s2 = ensure(ctx, 5, sizeof(uint32_t) * n_kmers)) return s2;
-    AC_HIP(ctx, hipMemcpyAsync(ctx->d_buf[0], kmers, sizeof(uint64_t) * n_kmers, hipMemcpyHostToDevice, st));
-    ac_segment seg;
-    seg.kmers = (const uint64_t*)ctx->d_buf[0];
-    seg.n_kmers = n_kmers;
-    seg.sample = *dev;
-    seg.counts = (uint32_t*)ctx->d_buf[5];
-    if (ac_status rc = launch(ctx, k, &seg, 1, st, true)) return rc;
-    ctx->h_counts.resize(n_kmers);
-    AC_HIP(ctx, hipMemcpyAsync(ctx->h_counts.data(), ctx->d_buf[5], sizeof(uint32_t) * n_kmers, hipMemcpyDeviceToHost, st));
-    if (ac_status rc = ac_check(ctx, st)) return rc;  // synchronises the stream
-    for (uint32_t i = 0; i < n_kmers; ++i) counts[i] = ctx->h_counts[i];
-    return AC_OK;
+    if (!dev) return fail(ctx, AC_ERR_INVALID, "NULL argument");
+    const ac_sample_job job{kmers, n_kmers, *dev, counts};
+    return ac_error_count_samples(ctx, k, &job, 1);
 }
 
 ac_status ac_last_launch(const ac_ctx* ctx, uint64_t* waves, uint32_t* windows_per_wave, uint32_t* groups) {
@@ -1145,8 +1255,6 @@ int ac_plan_host_cpus(const char* const* rank_cpulists, int n_ranks, int rank, c
 // ac_error_count_jobs: the whole errorCount stage from Dna5 host buffers.
 namespace {
 
-inline size_t align256(size_t x) { return (x + 255) / 256 * 256; }
-
 // AC_STAGE_TRACE=1: per-phase host timings of the jobs stage, summed over the
 // calls and printed to stderr at exit (a measurement aid; no effect otherwise).
 struct StageTrace {
@@ -1195,7 +1303,9 @@ struct JobPlan {
     uint64_t n_bases[AC_MAX_JOBS] = {};
     size_t off_kmers[AC_MAX_JOBS] = {}, off_codes[AC_MAX_JOBS] = {}, off_nmask[AC_MAX_JOBS] = {};
     size_t off_start[AC_MAX_JOBS] = {}, off_len[AC_MAX_JOBS] = {}, off_counts[AC_MAX_JOBS] = {};
-    size_t off_err = 0, total = 0;
+    size_t off_err = 0, off_hdr = 0, total = 0;
+    bool early = false;  // the early-launch stage (the kernel stages its own inputs, host-polled completion)
+    uint32_t gen = 0;    // its generation (the header flags and completion word carry it)
     int slot = 0;     // staging slot (set by the caller: a synchronous part q uses slot q, a submit part its set's)
     int scratch = 0;  // count-kernel scratch set (ac_ctx::sc)
     bool zc = true;  // this call's transfer mode (zero-copy or DMA)
@@ -1361,6 +1471,42 @@ double stage_split() {
     return v;
 }
 
+// The early-launch stage for one-part synchronous calls (default; AC_STAGE_EARLY=0 = the
+// pack -> transfer -> launch order of round 2, 2 = the first job sent ahead of the launch by
+// the copy kernel, the others staged by the count kernel).
+int stage_early() {
+    static const int v = [] {
+        const char* e = std::getenv("AC_STAGE_EARLY");
+        return e ? std::max(0, std::min(2, std::atoi(e))) : 0;
+    }();
+    return v;
+}
+
+// Some job has candidates and windows (a launch with work, so a completion word to wait for).
+bool live_work(const ac_job* jobs, uint32_t n_jobs) {
+    for (uint32_t j = 0; j < n_jobs; ++j)
+        if (jobs[j].n_kmers && jobs[j].sample.n_windows) return true;
+    return false;
+}
+
+// Spin until an early launch's completion word reads `gen`.  The kernel's own waits are
+// bounded (AC_STAGE_TIMEOUT_TICKS), so the stream always completes; if it has completed
+// without the word, the launch failed.
+ac_status wait_early(ac_ctx* ctx, const uint32_t* done, uint32_t gen, hipStream_t stream) {
+    uint32_t spins = 0;
+    while (__atomic_load_n(done, __ATOMIC_ACQUIRE) != gen) {
+        __builtin_ia32_pause();
+        if ((++spins & 1023u) == 0u) {
+            const hipError_t q = hipStreamQuery(stream);
+            if (q == hipErrorNotReady) continue;
+            if (q != hipSuccess) return hip_fail(ctx, q, "early launch");
+            if (__atomic_load_n(done, __ATOMIC_ACQUIRE) == gen) break;
+            return fail(ctx, AC_ERR_INTERNAL, "early launch finished without writing its completion word");
+        }
+    }
+    return AC_OK;
+}
+
 ac_status check_jobs(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint32_t n_jobs) {
     if (!ctx) return fail(nullptr, AC_ERR_INVALID, "ctx is NULL");
     if (ac_status st = check_k(ctx, k)) return st;
@@ -1463,6 +1609,8 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
         p.off_counts[j] = off;
         off = align256(off + sizeof(uint32_t) * jobs[j].n_kmers);
     }
+    p.off_hdr = off;  // the early launch's header lines (AC_HDR_LINES of them, 128 B each)
+    off = align256(off + sizeof(uint32_t) * AC_QUEUE_LINE * AC_HDR_LINES);
     p.total = off;
     // Zero-copy's worst case moves the image over PCIe once per candidate group (ZC_MAX_PCIE_BYTES).
     uint64_t pcie_bytes = 0;
@@ -1471,6 +1619,7 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
         pcie_bytes += p.n_bases[j] / 8 * 3 * ((jobs[j].n_kmers + cpw - 1) / cpw);  // 2-bit codes + N bitmap
     p.zc_eligible = p.zc_eligible && pcie_bytes <= ZC_MAX_PCIE_BYTES;  // (a multi-part call is DMA-only)
     if (!p.zc_eligible && stage_zerocopy_env() < 0) p.zc = false;
+    if (p.early) p.zc = false;
     // The slot: wait until the launch that last read it has finished, grow it.
     ac_ctx::Slot& sl = ctx->slot[p.slot];
     if (sl.pending) {
@@ -1500,6 +1649,10 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
         }
     }
     *(uint32_t*)(h + p.off_err) = 0u;
+    // early launch: flags and the completion word cleared before the launch (the slot's last
+    // launch has finished: its event was waited for above)
+    uint32_t* hdr = (uint32_t*)(h + p.off_hdr);
+    if (p.early) std::memset(hdr, 0, sizeof(uint32_t) * AC_QUEUE_LINE * AC_HDR_LINES);
     mark(1);
     // per task: did its windows hold an N (its N-bitmap words, or-ed after packing; still in cache)
     std::vector<uint8_t> task_n(tasks.size(), 0);
@@ -1537,6 +1690,95 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
     // In both modes the kernel writes the error word and the counts straight into the pinned
     // block (hd), so no copy comes back (profiles/r02_stage_dma_back_ab.log).
     char* hd = (char*)sl.hd;
+    auto make_segs = [&](ac_segment* segs) {
+        uint64_t cbase = 0;
+        for (uint32_t j = 0; j < p.n; ++j) {
+            ac_segment& g = segs[j];
+            const uint32_t nw = jobs[j].n_kmers ? p.hi[j] - p.lo[j] : 0;
+            g.kmers = (const uint64_t*)(d + p.off_kmers[j]);
+            g.n_kmers = jobs[j].n_kmers;
+            g.sample = ac_windows{(const uint32_t*)(d + p.off_codes[j]), (const uint32_t*)(d + p.off_nmask[j]),
+                                  (const uint64_t*)(d + p.off_start[j]), (const uint32_t*)(d + p.off_len[j]), nw,
+                                  p.n_bases[j]};
+            g.counts = d_counts ? d_counts + cbase : (uint32_t*)(hd + p.off_counts[j]);
+            cbase += jobs[j].n_kmers;
+        }
+    };
+    if (p.early) {
+        // Early launch: the count kernel is launched before the later jobs are
+        // packed; the pool packs job by job and the host flags each job in the header as soon
+        // as it is complete; the kernel copies a flagged job's region into device memory itself
+        // and counts it while the next job is still being packed.  The region of job j: k-mers,
+        // codes, then the N bitmap unless the job holds no N, and the window descriptors unless
+        // its windows have one length.  The first `pre` jobs (AC_STAGE_EARLY=2: the first) are
+        // sent before the launch by the copy kernel instead, stream-ordered ahead of it.
+        const uint32_t pre = (stage_early() == 2 && p.n > 1) ? 1u : 0u;
+        size_t region[AC_MAX_JOBS] = {};
+        StageLaunch stg;
+        if (++ctx->gen == 0) ++ctx->gen;
+        p.gen = stg.gen = ctx->gen;
+        stg.host_hdr = (uint32_t*)(hd + p.off_hdr);
+        for (uint32_t j = 0; j < p.n; ++j) {
+            const size_t end = ulen[j] != AC_NO_ULEN ? p.off_start[j] : (j + 1 < p.n ? p.off_kmers[j + 1] : p.off_err);
+            region[j] = end - p.off_kmers[j];
+            stg.src[j] = (const uint8_t*)(hd + p.off_kmers[j]);
+            stg.dst[j] = (uint8_t*)(d + p.off_kmers[j]);
+            stg.chunks[j] = j < pre ? 0u : (uint32_t)((region[j] + AC_STAGE_CHUNK - 1) / AC_STAGE_CHUNK);
+        }
+        auto go = [&]() -> ac_status {
+            ac_segment segs[AC_MAX_JOBS];
+            make_segs(segs);
+            if (ac_status st = launch(ctx, k, segs, p.n, stream, zero, nullptr, p.scratch, 0, no_n, ulen, &stg))
+                return st;
+            AC_HIP(ctx, hipEventRecord(sl.ev, stream));
+            sl.pending = true;
+            mark(4);
+            return AC_OK;
+        };
+        if (pre == 0)
+            if (ac_status st = go()) return st;
+        std::atomic<uint32_t> left[AC_MAX_JOBS];
+        for (uint32_t j = 0; j < AC_MAX_JOBS; ++j) left[j].store(0, std::memory_order_relaxed);
+        for (const Task& x : tasks) left[x.job].fetch_add(1, std::memory_order_relaxed);
+        const std::function<void(uint32_t)> pack_counted = [&](uint32_t t) {
+            pack(t);
+            left[tasks[t].job].fetch_sub(1, std::memory_order_release);
+        };
+        pool.begin((uint32_t)tasks.size(), pack_counted);
+        uint32_t t0 = 0;
+        for (uint32_t j = 0; j < p.n; ++j) {
+            uint32_t t1 = t0;
+            while (t1 < (uint32_t)tasks.size() && tasks[t1].job == j) ++t1;
+            pool.help(t1);
+            while (left[j].load(std::memory_order_acquire) != 0u) __builtin_ia32_pause();
+            const bool nn = job_no_n(j);
+            const size_t bytes = nn && ulen[j] != AC_NO_ULEN ? p.off_nmask[j] - p.off_kmers[j] : region[j];
+            if (j < pre) {  // sent ahead of the launch, which follows it on the stream
+                no_n[j] = nn;
+                hipError_t e = stage_blit_launch(hd + p.off_kmers[j], d + p.off_kmers[j], bytes, stream);
+                ac_status st = e == hipSuccess ? AC_OK : hip_fail(ctx, e, "stage transfer");
+                if (st == AC_OK && j + 1 == pre) st = go();
+                if (st != AC_OK) {
+                    pool.finish();
+                    return st;
+                }
+            } else {
+                uint32_t* line = hdr + j * AC_QUEUE_LINE;
+                line[AC_HDR_BYTES] = (uint32_t)bytes;
+                line[AC_HDR_HAS_N] = nn ? 0u : 1u;
+                line[AC_HDR_ABORT] = 0u;
+                // (test hook: AC_STAGE_TEST_UNFLAGGED=1 leaves the last job unflagged, so the kernel's bounded
+                // wait runs out and the call must fail cleanly: tests/test_gpu_jobs.py)
+                static const bool unflag = std::getenv("AC_STAGE_TEST_UNFLAGGED") != nullptr;
+                if (!(unflag && j + 1 == p.n))
+                    __atomic_store_n(&line[AC_HDR_FLAG], p.gen, __ATOMIC_RELEASE);  // the kernel's waves may go
+            }
+            t0 = t1;
+        }
+        pool.finish();
+        mark(2);
+        return AC_OK;
+    }
     // DMA mode sends the inputs [r0, r1) of the slot (copy engine or blit kernel)
     auto transfer = [&](size_t r0, size_t r1) -> hipError_t {
         if (r1 <= r0) return hipSuccess;
@@ -1585,18 +1827,7 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
     }
     mark(3);
     ac_segment segs[AC_MAX_JOBS];
-    uint64_t cbase = 0;
-    for (uint32_t j = 0; j < p.n; ++j) {
-        ac_segment& g = segs[j];
-        const uint32_t nw = jobs[j].n_kmers ? p.hi[j] - p.lo[j] : 0;
-        g.kmers = (const uint64_t*)(d + p.off_kmers[j]);
-        g.n_kmers = jobs[j].n_kmers;
-        g.sample = ac_windows{(const uint32_t*)(d + p.off_codes[j]), (const uint32_t*)(d + p.off_nmask[j]),
-                              (const uint64_t*)(d + p.off_start[j]), (const uint32_t*)(d + p.off_len[j]), nw,
-                              p.n_bases[j]};
-        g.counts = d_counts ? d_counts + cbase : (uint32_t*)(hd + p.off_counts[j]);
-        cbase += jobs[j].n_kmers;
-    }
+    make_segs(segs);
     // the synchronous path reads the error word back with the counts; a
     // submit reports through the context's word (ac_check)
     uint64_t cap = 0;
@@ -1713,6 +1944,14 @@ ac_status ac_error_count_jobs(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint3
             u.plan.scratch = q;
             // parts are for large calls: DMA only (zero-copy would read the whole image per group)
             u.plan.zc_eligible = parts == 1;
+            if (parts == 1 && stage_early() && live_work(jobs, n_jobs)) {
+                // one part: the early-launch stage (alternating slots 0 / 1, so a call never waits for
+                // the previous call's launch to retire before it packs)
+                u.plan.early = true;
+                u.plan.zc_eligible = false;
+                u.plan.slot = (int)ctx->early_flip;
+                ctx->early_flip ^= 1u;
+            }
             for (uint32_t j = 0; j < n_jobs; ++j) {
                 u.plan.lo[j] = cuts[j][q];
                 u.plan.hi[j] = cuts[j][q + 1];
@@ -1745,17 +1984,28 @@ ac_status ac_error_count_jobs(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint3
     for (size_t g = 0; g < units.size(); ++g) {
         Unit& u = units[g];
         AC_HIP(u.c, hipSetDevice(u.c->device));
-        AC_HIP(u.c, hipStreamSynchronize(u.stream));
+        ac_ctx::Slot& sl = u.c->slot[u.plan.slot];
+        const char* h = (const char*)sl.h;
+        uint32_t err_word;
+        if (u.plan.early) {
+            // the kernel's last workgroup writes the completion word after every count: poll it
+            // instead of waiting for the stream (the launch's event is waited for when the slot is
+            // next used)
+            const uint32_t* res = (const uint32_t*)(h + u.plan.off_hdr) + AC_MAX_SEGS * AC_QUEUE_LINE;
+            if (ac_status st = wait_early(u.c, res + AC_HDR_DONE, u.plan.gen, u.stream)) return st;
+            err_word = __atomic_load_n(res + AC_HDR_ERR, __ATOMIC_ACQUIRE);
+        } else {
+            AC_HIP(u.c, hipStreamSynchronize(u.stream));
+            sl.pending = false;
+            err_word = *(const uint32_t*)(h + u.plan.off_err);
+        }
         if (g_trace.on && g + 1 == units.size()) {
             const double t = now_us();
             g_trace.sum[6] += t - t_sync;
             g_trace.cur[6] += t - t_sync;
             t_sync = t;
         }
-        ac_ctx::Slot& sl = u.c->slot[u.plan.slot];
-        sl.pending = false;
-        const char* h = (const char*)sl.h;
-        if (ac_status st = device_error(u.c, *(const uint32_t*)(h + u.plan.off_err))) {
+        if (ac_status st = device_error(u.c, err_word)) {
             if (first_err == AC_OK)
                 first_err = u.c != ctx ? fail(ctx, st, "shard " + std::to_string(g) + ": " + u.c->err) : st;
             continue;
@@ -1770,7 +2020,7 @@ ac_status ac_error_count_jobs(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint3
         for (size_t g = 0; g < units.size(); ++g)  // once per context (parts of one device share it)
             if ((g == 0 || units[g].c != units[g - 1].c) && units[g].plan.zc_eligible)
                 stage_zerocopy_record(units[g].c, units[g].plan.zc, us);
-        units[0].c->zc_last = units[0].plan.zc_eligible ? -1 : 0;
+        units[0].c->zc_last = units[0].plan.early ? 2 : units[0].plan.zc_eligible ? -1 : 0;
     }
     if (g_trace.on) {
         g_trace.sum[7] += now_us() - t_sync;
@@ -1847,6 +2097,7 @@ ac_status ac_error_count_jobs_submit(ac_ctx* ctx, uint32_t k, const ac_job* jobs
 int ac_stage_mode(const ac_ctx* ctx) {
     if (!ctx) return -1;
     if (stage_zerocopy_env() >= 0) return stage_zerocopy_env();
+    if (ctx->zc_last == 2) return 2;  // the last call took the early-launch stage
     if (ctx->zc_last == 0) return 0;  // the last call's image is DMA-only
     return ctx->zc_choice;
 }

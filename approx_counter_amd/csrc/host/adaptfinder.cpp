@@ -194,25 +194,12 @@ ac_windows view(const PackedImage& p) {
 
 // The device context: -g N opens N shards (device g mod the visible devices,
 // ac_create_multi); the exact count and the one-GPU approximate count use the
-// first device, the sharded count goes through ac_error_count.
+// first device, the sharded count goes through ac_error_count_images.
 struct Devices {
     ac_ctx* ctx = nullptr;
     uint64_t shards = 1;
     ~Devices() { ac_destroy(ctx); }
 };
-
-// errorCount (approx_counter.cpp:531-601) through the C ABI on a host image.
-pair_vector error_count(Devices& dev, const PackedImage& img, const pair_vector& first_n, uint32_t k) {
-    pair_vector out(first_n.size());
-    if (first_n.empty()) return out;
-    std::vector<uint64_t> kmers(first_n.size()), counts(first_n.size());
-    for (size_t i = 0; i < first_n.size(); ++i) kmers[i] = first_n[i].first;
-    const ac_windows w = view(img);
-    if (ac_error_count(dev.ctx, k, kmers.data(), (uint32_t)kmers.size(), &w, counts.data()) != AC_OK)
-        throw std::runtime_error(ac_last_error(dev.ctx));
-    for (size_t i = 0; i < kmers.size(); ++i) out[i] = {kmers[i], counts[i]};
-    return out;
-}
 
 // --dump-sample: u64 n_windows, u64 n_bases, start[n] u64, length[n] u32,
 // codes[n_bases/16] u32, nmask[n_bases/32] u32 (little endian).
@@ -372,6 +359,17 @@ int main(int argc, char const** argv) {
 
     std::mt19937 rng(seed_str.empty() ? std::random_device{}() : (uint32_t)std::strtoull(seed_str.c_str(), nullptr, 10));
 
+    // One run samples both read ends, counts each end's k-mers exactly, then counts both
+    // ends approximately in ONE fused launch (errorCount, approx_counter.cpp:922, for the
+    // two iterations of the loop at 858-953, whose inputs are independent), and ranks and
+    // exports each end.  Output files and their contents are the reference's; only the
+    // order of the progress messages differs.
+    struct End {
+        std::string which;
+        PackedImage img;
+        ac_windows dsample{};
+        pair_vector first_n;
+    };
     for (uint64_t run = 0; run < nb_of_runs; ++run) {
         const std::string run_suffix = "_" + std::to_string(run);
         if (nb_of_runs > 1 && v > 0) std::cout << "Starting run number " << run + 1 << std::endl;
@@ -382,21 +380,63 @@ int main(int argc, char const** argv) {
         }
         bool bottom = false;
         tab_level += 1;
+        std::vector<End> pending;
+        // the approximate count of the pending ends, then their ranking and export
+        auto flush = [&]() -> bool {
+            if (pending.empty()) return true;
+            std::vector<std::vector<uint64_t>> km(pending.size()), ct(pending.size());
+            std::vector<ac_sample_job> jobs(pending.size());
+            for (size_t e = 0; e < pending.size(); ++e) {
+                if (mr_v > 0) print("Approximate k-mer count (" + pending[e].which + ")", tab_level);
+                for (const auto& x : pending[e].first_n) km[e].push_back(x.first);
+                ct[e].assign(km[e].size(), 0);
+                jobs[e] = ac_sample_job{km[e].data(), (uint32_t)km[e].size(), ac_windows{}, ct[e].data()};
+            }
+            try {
+                devices();
+                const bool on_device = !host_exact && dev.shards == 1;  // the samples uploaded for the exact count
+                for (size_t e = 0; e < pending.size(); ++e)
+                    jobs[e].sample = on_device ? pending[e].dsample : view(pending[e].img);
+                const ac_status st =
+                    on_device ? ac_error_count_samples(dev.ctx, (uint32_t)k, jobs.data(), (uint32_t)jobs.size())
+                              : ac_error_count_images(dev.ctx, (uint32_t)k, jobs.data(), (uint32_t)jobs.size());
+                if (st != AC_OK) throw std::runtime_error(ac_last_error(dev.ctx));
+            } catch (const std::exception& e) {
+                std::cerr << error_pref << "approximate count failed: " << e.what() << std::endl;
+                return false;
+            }
+            for (size_t e = 0; e < pending.size(); ++e) {
+                pair_vector error_counter(km[e].size());
+                for (size_t i = 0; i < km[e].size(); ++i) error_counter[i] = {km[e][i], ct[e][i]};
+                pair_vector sorted_error_count = get_most_frequent(std::move(error_counter), limit, (uint32_t)k);
+                if (mr_v > 0) print("Exporting approximate count", tab_level);
+                const std::string path = output + run_suffix + "." + pending[e].which;
+                if (!export_counter(sorted_error_count, (uint32_t)k, path)) {
+                    std::cerr << error_pref + "Failed to export approximate k-mer count" << std::endl;
+                    std::cerr << "Path: " << path << std::endl;
+                    return false;
+                }
+                if (mr_v > 0) print("Done", tab_level);
+            }
+            pending.clear();
+            return true;
+        };
         for (const std::string which_end : {"start", "end"}) {
             if (v > 0) print("Working on sequence " + which_end + ".", tab_level - 1);
             if (mr_v > 0) print("Sampling", tab_level);
             if (mr_v > 0) print(bottom ? "Sampling the ends of reads" : "Sampling the start of reads", 1);
+            End cur;
+            cur.which = which_end;
             SeqSet sample;
-            PackedImage img;
             if (host_exact) {
                 sample = sample_sequences(seqs, sn, sl, bottom, rng);
-                img = pack_sample(sample, 0, sample.size());
+                cur.img = pack_sample(sample, 0, sample.size());
             } else {
-                img = sample_windows(store, sn, bottom, rng);
+                cur.img = sample_windows(store, sn, bottom, rng);
             }
-            if (mr_v > 0) print("Sampled " + std::to_string(img.size()) + " sequences", 1);
+            if (mr_v > 0) print("Sampled " + std::to_string(cur.img.size()) + " sequences", 1);
             if (!dump_sample.empty()) {
-                if (!write_image(img, dump_sample + run_suffix + "." + which_end)) {
+                if (!write_image(cur.img, dump_sample + run_suffix + "." + which_end)) {
                     std::cerr << error_pref << "could not write " << dump_sample + run_suffix + "." + which_end << "\n";
                     return 1;
                 }
@@ -406,21 +446,19 @@ int main(int argc, char const** argv) {
             }
             if (mr_v > 0) print("Exact k-mer count", tab_level);
             uint64_t had_n = 0, n_found = 0;
-            pair_vector first_n;
-            ac_windows dsample{};
             if (host_exact) {  // the reference's host stages (approx_counter.cpp:874-899)
                 pair_vector count = count_kmers(sample, (uint32_t)k, lc, forbidden, &had_n);
                 n_found = count.size();
-                first_n = solid_km != 0 ? get_solid_kmers(std::move(count), solid_km, (uint32_t)k)
-                                        : get_most_frequent(std::move(count), limit, (uint32_t)k);
-            } else {  // the same on GPU 0; the uploaded sample also serves the approximate count
+                cur.first_n = solid_km != 0 ? get_solid_kmers(std::move(count), solid_km, (uint32_t)k)
+                                            : get_most_frequent(std::move(count), limit, (uint32_t)k);
+            } else {  // the same on GPU 0; the upload (one slot per end) also serves the approximate count
                 try {
                     devices();
-                    const ac_windows hw = view(img);
-                    if (ac_sample_upload(dev.ctx, &hw, &dsample) != AC_OK)
+                    const ac_windows hw = view(cur.img);
+                    if (ac_sample_upload_slot(dev.ctx, (int)pending.size(), &hw, &cur.dsample) != AC_OK)
                         throw std::runtime_error(ac_last_error(dev.ctx));
-                    first_n = exact_count_gpu(dev.ctx, dsample, (uint32_t)k, lc, forbidden, limit, solid_km,
-                                              &n_found, &had_n);
+                    cur.first_n = exact_count_gpu(dev.ctx, cur.dsample, (uint32_t)k, lc, forbidden, limit, solid_km,
+                                                  &n_found, &had_n);
                 } catch (const std::exception& e) {
                     std::cerr << error_pref << "exact count failed: " << e.what() << std::endl;
                     return 1;
@@ -433,42 +471,17 @@ int main(int argc, char const** argv) {
             }
             if (mr_v > 0) print("Number of kmer found: " + std::to_string(n_found), tab_level);
             if (mr_v > 0) print(solid_km != 0 ? "Keeping solid k-mer" : "Keeping most frequent k-mer", tab_level);
-            if (mr_v > 0) print("Number of kmer kept:  " + std::to_string(first_n.size()), tab_level);
+            if (mr_v > 0) print("Number of kmer kept:  " + std::to_string(cur.first_n.size()), tab_level);
             if (!exact_out.empty()) {
                 if (mr_v > 0) print("Exporting exact kmer count", tab_level);
-                if (!export_counter(first_n, (uint32_t)k, exact_out + run_suffix + "." + which_end)) {
+                if (!export_counter(cur.first_n, (uint32_t)k, exact_out + run_suffix + "." + which_end)) {
                     std::cerr << error_pref + "Failed to export exact k-mer count" << std::endl;
                     std::cerr << "Path: " << exact_out + run_suffix + "." + which_end << std::endl;
+                    flush();  // the reference wrote the earlier end's approximate count before failing here
                     return 1;
                 }
             }
-            if (mr_v > 0) print("Approximate k-mer count", tab_level);
-            pair_vector error_counter;
-            try {
-                devices();
-                if (!host_exact && dev.shards == 1) {  // one GPU: count on the sample uploaded above
-                    std::vector<uint64_t> km(first_n.size()), ct(first_n.size());
-                    for (size_t i = 0; i < first_n.size(); ++i) km[i] = first_n[i].first;
-                    if (!km.empty() && ac_error_count_sample(dev.ctx, (uint32_t)k, km.data(), (uint32_t)km.size(),
-                                                             &dsample, ct.data()) != AC_OK)
-                        throw std::runtime_error(ac_last_error(dev.ctx));
-                    error_counter.resize(km.size());
-                    for (size_t i = 0; i < km.size(); ++i) error_counter[i] = {km[i], ct[i]};
-                } else {
-                    error_counter = error_count(dev, img, first_n, (uint32_t)k);
-                }
-            } catch (const std::exception& e) {
-                std::cerr << error_pref << "approximate count failed: " << e.what() << std::endl;
-                return 1;
-            }
-            pair_vector sorted_error_count = get_most_frequent(std::move(error_counter), limit, (uint32_t)k);
-            if (mr_v > 0) print("Exporting approximate count", tab_level);
-            if (!export_counter(sorted_error_count, (uint32_t)k, output + run_suffix + "." + which_end)) {
-                std::cerr << error_pref + "Failed to export approximate k-mer count" << std::endl;
-                std::cerr << "Path: " << output + run_suffix + "." + which_end << std::endl;
-                return 1;
-            }
-            if (mr_v > 0) print("Done", tab_level);
+            pending.push_back(std::move(cur));
             // approx_counter.cpp:943-951: the break only happens when verbose
             // (without it the second pass samples read STARTS again and writes
             // them to the .end file -- kept for drop-in fidelity).
@@ -481,6 +494,7 @@ int main(int argc, char const** argv) {
                 bottom = true;
             }
         }
+        if (!flush()) return 1;
         tab_level--;
     }
     return 0;

@@ -21,7 +21,32 @@
 // its set-up broken (the ~Eq table not at LDS address 0) and skipped its work.
 #define AC_DEVERR_WINDOW 1u
 #define AC_DEVERR_SETUP 2u
+#define AC_DEVERR_STAGE 4u  // a staged launch timed out waiting for its host inputs (its work was skipped)
 #define AC_NO_ULEN 0xffffffffu
+
+// Staged launches ("early launch"): the count kernel is launched
+// before the host has packed its inputs and stages them itself.  Per segment,
+// the host writes one header line of the pinned staging block when the
+// segment's packed inputs are complete:
+#define AC_HDR_FLAG 0    // = the launch's generation once the rest is valid
+#define AC_HDR_BYTES 1   // bytes of the segment's region to copy (<= the launch's chunks x AC_STAGE_CHUNK)
+#define AC_HDR_HAS_N 2   // 0: the segment holds no N (its N bitmap was not copied)
+#define AC_HDR_ABORT 3   // nonzero: the host gave up on the call; the waves skip the segment
+// and the kernel's last workgroup writes the launch's result line (line AC_MAX_SEGS):
+#define AC_HDR_DONE 0    // = generation once every count of the launch is in host memory
+#define AC_HDR_ERR 1     // AC_DEVERR_* bits of the launch
+#define AC_HDR_LINES (AC_MAX_SEGS + 1)
+#define AC_STAGE_CHUNK 4096u  // bytes one wave copies per claimed chunk (64 lanes x 16 B x 4)
+#define AC_STAGE_REPL 32      // replicas of a segment's done counter (pollers spread over lines)
+// Device words of a staged launch, one AC_QUEUE_LINE line each, after the
+// launch's sub-queue counters in its queue bank (zeroed with them for the next
+// launch on that bank): groups done, error bits, then per segment: chunk
+// claims, the segment's header copy (verdict, bytes, seen), AC_STAGE_REPL done replicas.
+#define AC_STAGE_L_GROUPS 0
+#define AC_STAGE_L_ERR 1
+#define AC_STAGE_L_SEG(s) (2 + (s) * (2 + AC_STAGE_REPL))
+#define AC_STAGE_LINES (2 + AC_MAX_SEGS * (2 + AC_STAGE_REPL))
+#define AC_STAGE_TIMEOUT_TICKS 50000000ull  // 0.5 s of s_memrealtime (100 MHz): every wait is bounded
 
 namespace acamd {
 
@@ -44,6 +69,12 @@ struct SegDev {
     uint32_t has_n;       // 0: the image holds no N (its N bitmap is not read; every word reads as 0)
     uint32_t ulen;        // AC_NO_ULEN, or every window has this length and window w starts at base
                           // w * ceil32(ulen) (start / length are not read)
+    // staged launches: the segment's packed region (k-mers first) is copied from stage_src (the
+    // pinned block, device-visible address) to stage_dst (device memory; kmers / codes / ... point
+    // into it) in stage_chunks chunks of AC_STAGE_CHUNK bytes once the host flags it
+    const uint8_t* stage_src;
+    uint8_t* stage_dst;
+    uint32_t stage_chunks;
 };
 
 struct LaunchArgs {
@@ -68,6 +99,15 @@ struct LaunchArgs {
     uint32_t* tickets;  // one per AC_QUEUE_LINE u32
     uint32_t* err;      // AC_DEVERR_* bits, or-ed in by the kernel
     uint32_t add_counts;
+    // Staged launch (nonzero): inputs copied in by the kernel once the host flags each segment in
+    // host_hdr (pinned, AC_HDR_LINES lines of AC_QUEUE_LINE u32); counts stored to host memory at
+    // system scope, the launch's completion written to host_hdr's result line.  `stage` = this
+    // launch's AC_STAGE_LINES device lines; total_groups = candidate groups over all segments.
+    uint32_t staged;
+    uint32_t gen;
+    uint32_t* host_hdr;
+    uint32_t* stage;
+    uint32_t total_groups;
     uint32_t n_segs;
     uint32_t m;  // k-mer length
     uint32_t P;  // candidates per lane word

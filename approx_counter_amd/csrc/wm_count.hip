@@ -57,6 +57,7 @@ constexpr int WAVES_PER_BLOCK = AC_WAVES_PER_BLOCK;
 // computed from them.
 }  // namespace
 __device__ uint64_t g_stamps[1 << 21];
+__device__ uint64_t g_stage_stamps[64];  // per segment: [s*4] host flag seen by the poller, [s*4+1] its copy done
 namespace {
 __device__ __forceinline__ void stamp(uint64_t wave, int i) {
     if ((threadIdx.x & 63u) == 0 && wave < (1u << 18)) {
@@ -73,9 +74,13 @@ __device__ __forceinline__ void stamp(uint64_t wave, int i) {
 __device__ __forceinline__ void stamp_val(uint64_t wave, int i, uint64_t v) {
     if ((threadIdx.x & 63u) == 0 && wave < (1u << 18)) g_stamps[wave * 8 + i] = v;
 }
+__device__ __forceinline__ void stage_stamp(uint32_t si, int i) {
+    if ((threadIdx.x & 63u) == 0) g_stage_stamps[si * 4 + i] = __builtin_amdgcn_s_memrealtime();
+}
 #else
 __device__ __forceinline__ void stamp(uint64_t, int) {}
 __device__ __forceinline__ void stamp_val(uint64_t, int, uint64_t) {}
+__device__ __forceinline__ void stage_stamp(uint32_t, int) {}
 #endif
 constexpr uint32_t SEG = 256;  // window bases fetched per pass (16 code words, 8 N-mask words)
 
@@ -147,6 +152,21 @@ __device__ __forceinline__ void load_desc(const uint64_t* start, const uint32_t*
 #endif
 }
 
+// The same with vector loads, for staged launches: their descriptors are copied
+// in by the kernel itself, so they DO change during the launch, and a scalar
+// (constant address space) load could be hoisted above the staging wait or hit
+// a scalar-cache line filled before it.
+typedef const __attribute__((address_space(1))) uint64_t* gu64p;
+typedef const __attribute__((address_space(1))) uint32_t* gu32p;
+__device__ __forceinline__ void load_desc_vec(const uint64_t* start, const uint32_t* length, uint32_t w, uint64_t& base,
+                                              uint32_t& len) {
+    const uint64_t b = ((gu64p)start)[w];
+    const uint32_t l = ((gu32p)length)[w];
+    base = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
+           __builtin_amdgcn_readfirstlane((uint32_t)b);
+    len = __builtin_amdgcn_readfirstlane(l);
+}
+
 // Per-wave ~Eq table: word c*64 + lane = the lane's ~Eq mask for character c
 // (A C G T, then N = all ones), read per base with ds_read_addtid_b32.
 struct TidTable {
@@ -216,11 +236,124 @@ __device__ __forceinline__ uint32_t window_valid(uint64_t base, uint32_t len, ui
 // tools/gen_tid_blocks.py).
 constexpr bool TID_EB0 = true;
 
-// Workgroup LDS: the ~Eq table, then the count vector the waves sum into.
+// Workgroup LDS: the ~Eq table, then the count vector the waves sum into,
+// then the staged launch's verdict for the workgroup's segment.
 struct BlockLds {
     TidTable tab;
     uint32_t cnt[AC_MAX_PACK * 64];
+    uint32_t stage_r;
 };
+
+// Staged launch ("early launch"): the kernel is launched before
+// the host has packed its inputs.  Wave 0 of every workgroup runs this before
+// anything reads the segment.  It claims AC_STAGE_CHUNK-byte chunks of the
+// segment's region (an agent-scope counter).  The wave that wins chunk 0 is the
+// segment's only host poller: it polls the host's flag (= gen, in the pinned
+// header line; system-scope loads, ~0.2 us apart), copies the header's size and
+// N verdict into the segment's device words and raises a device flag; the other
+// chunk winners wait on that device flag.  Each copies its chunks from the
+// pinned block to device memory with write-through (sc1) stores, waits for them
+// and adds 1 to every replica of the segment's done counter.  Every workgroup
+// then polls one replica until all chunks are in, and acquires.  The copied
+// lines were not in any L2 at launch start and are touched by no one before the
+// counter says so, so the readers' plain loads fetch them fresh (the hand-off
+// form of MI355X_MICROARCH.md's visibility section).  Every wait is bounded
+// (AC_STAGE_TIMEOUT_TICKS): a host that never flags makes the waves report
+// AC_DEVERR_STAGE and skip, never hang.  Returns the segment's has_n, or ~0u when
+// the segment is skipped (timeout, or the host's abort flag).
+__device__ __attribute__((noinline)) uint32_t stage_wait(const uint8_t* src, uint8_t* dst, uint32_t chunks,
+                                                         uint32_t* hdr, uint32_t* words, uint32_t gen, uint32_t* err,
+                                                         uint32_t replica, uint32_t si) {
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t* claim = words;
+    uint32_t* info = words + AC_QUEUE_LINE;  // [0] verdict, [1] bytes, [2] header seen
+    uint32_t* done = words + 2 * AC_QUEUE_LINE;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    auto late = [&]() { return __builtin_amdgcn_s_memrealtime() - t0 > AC_STAGE_TIMEOUT_TICKS; };
+    auto load = [&](uint32_t* p, int scope) {
+        uint32_t v = 0;
+        if (lane == 0)
+            v = scope ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                      : __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return __builtin_amdgcn_readfirstlane(v);
+    };
+    bool ok = true, seen = false;
+    uint32_t bytes = 0, verdict = 0;
+    __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)src, 0, 0, 0x00020000);
+    __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)dst, 0, 0, 0x00020000);
+    for (;;) {
+        uint32_t c = 0;
+        if (lane == 0) c = __hip_atomic_fetch_add(claim, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        c = __builtin_amdgcn_readfirstlane(c);
+        if (c >= chunks) break;
+        if (!seen) {
+            if (c == 0) {  // the segment's host poller
+                while (load(hdr + AC_HDR_FLAG, 1) != gen) {
+                    if (late()) {
+                        ok = false;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(8);
+                }
+                if (!ok) break;
+                stage_stamp(si, 0);
+                bytes = load(hdr + AC_HDR_BYTES, 1);
+                verdict = load(hdr + AC_HDR_ABORT, 1) ? ~0u : (load(hdr + AC_HDR_HAS_N, 1) ? 1u : 0u);
+                if (bytes > chunks * AC_STAGE_CHUNK) verdict = ~0u;  // a header the launch cannot hold: skip
+                if (lane == 0) {
+                    __hip_atomic_store(info, verdict, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(info + 1, bytes, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (lane == 0) __hip_atomic_store(info + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {  // the other chunk winners wait for the poller's device flag
+                while (load(info + 2, 0) == 0u) {
+                    if (late()) {
+                        ok = false;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(4);
+                }
+                if (!ok) break;
+                verdict = load(info, 0);
+                bytes = load(info + 1, 0);
+            }
+            // range-checked descriptors: bytes past the region read as 0 and are not stored
+            rs = __builtin_amdgcn_make_buffer_rsrc((void*)src, 0, (int)bytes, 0x00020000);
+            rd = __builtin_amdgcn_make_buffer_rsrc((void*)dst, 0, (int)bytes, 0x00020000);
+            seen = true;
+        }
+        if (verdict != ~0u) {
+            typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+            v4u v[4];
+            const uint32_t o = c * AC_STAGE_CHUNK + lane * 16u;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, o + u * 1024u, 0, 17);  // sc0 sc1
+#pragma unroll
+            for (int u = 0; u < 4; ++u) __builtin_amdgcn_raw_buffer_store_b128(v[u], rd, o + u * 1024u, 0, 16);  // sc1
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (c == 0) stage_stamp(si, 1);
+        if (lane < AC_STAGE_REPL)
+            __hip_atomic_fetch_add(done + lane * AC_QUEUE_LINE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    while (ok && load(done + replica * AC_QUEUE_LINE, 0) < chunks) {
+        if (late()) {
+            ok = false;
+            break;
+        }
+        __builtin_amdgcn_s_sleep(8);
+    }
+    if (!ok) {
+        if (lane == 0) atomicOr(err, AC_DEVERR_STAGE);
+        return ~0u;
+    }
+#ifndef AC_STAGE_NO_ACQUIRE  // A/B build: no L1 invalidate (nothing on this CU read the region before)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    return load(info, 0);
+}
 
 // The remainder (< 16 bases) of a segment: blocks of 8, 4, 2, 1 bases.
 template <int P>
@@ -294,10 +427,28 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
     // every byte offset fits 32 bits.
     // (inputs pinned in SGPRs by an asm operand: hipcc must see them wave-uniform, or it wraps every
     // fetch in a waterfall loop)
+    // Staged launch: the segment's inputs are not there yet; wave 0 stages them (stage_wait), the
+    // workgroup's other waves wait at a barrier, then everyone reads the verdict from LDS.
+    uint32_t has_n = sg.has_n;
+    bool skip = false;
+    if (a.staged && sg.stage_chunks) {  // (a segment sent ahead of a staged launch has no chunks)
+        if (wib == 0) {
+            const uint32_t r = stage_wait(sg.stage_src, sg.stage_dst, sg.stage_chunks,
+                                          a.host_hdr + (uint32_t)si * AC_QUEUE_LINE,
+                                          a.stage + AC_STAGE_L_SEG(si) * AC_QUEUE_LINE, a.gen, a.err,
+                                          blockIdx.x % AC_STAGE_REPL, (uint32_t)si);
+            if (lane == 0) lds.stage_r = r;
+            stamp(wave, 7);  // diagnostic builds (staged): the staging wait is over
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        const uint32_t r = __builtin_amdgcn_readfirstlane(lds.stage_r);
+        skip = r == ~0u;
+        has_n = skip ? 0u : r;
+    }
     const uint32_t* codes_p = sg.codes;
     const uint32_t* nmask_p = sg.nmask;
     // (an N-free image: a zero-sized N-bitmap descriptor, whose loads all return 0 without a memory access)
-    uint32_t code_bytes = (uint32_t)(sg.n_bases >> 2), nmask_bytes = sg.has_n ? (uint32_t)(sg.n_bases >> 3) : 0u;
+    uint32_t code_bytes = (uint32_t)(sg.n_bases >> 2), nmask_bytes = has_n ? (uint32_t)(sg.n_bases >> 3) : 0u;
     asm volatile("" : "+s"(codes_p), "+s"(nmask_p), "+s"(code_bytes), "+s"(nmask_bytes));
     Image im;
     im.codes = __builtin_amdgcn_make_buffer_rsrc((void*)codes_p, 0, (int)code_bytes, 0x00020000);
@@ -314,10 +465,14 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
     uint32_t ulen = sg.ulen;
     asm volatile("" : "+s"(ulen));
     const uint32_t ustride = ulen == AC_NO_ULEN ? 0u : (ulen + 31u) & ~31u;
+    uint32_t staged = a.staged;
+    asm volatile("" : "+s"(staged));
     auto desc = [&](uint32_t ww, uint64_t& base_out, uint32_t& len_out) __attribute__((always_inline)) {
         if (ulen != AC_NO_ULEN) {
             base_out = (uint64_t)ww * ustride;
             len_out = ulen;
+        } else if (staged) {
+            load_desc_vec(g_start, g_length, ww, base_out, len_out);
         } else {
             load_desc(g_start, g_length, ww, base_out, len_out);
         }
@@ -436,7 +591,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
             if (c < jc_items) return item_of(c);
         }
     };
-    uint32_t item = (j < n_items && eb_ok) ? item_of(rank) : n_items;
+    uint32_t item = (j < n_items && eb_ok && !skip) ? item_of(rank) : n_items;
     uint32_t pending = 0;
     uint32_t w = item * chunk, item_end = min(sg.n_windows, w + chunk);
 
@@ -473,7 +628,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
 #pragma unroll
         for (int p = 0; p < P; ++p) lds.cnt[p * 64 + lane] = 0u;
     }
-    stamp(wave, 7);  // diagnostic builds: the wave's own prologue done, before the barrier
+    if (!a.staged) stamp(wave, 7);  // diagnostic builds: the wave's own prologue done, before the barrier
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     stamp(wave, 1);
 
@@ -590,6 +745,9 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
 #pragma unroll
     for (int p = 0; p < P; ++p)
         if (cnt[p]) __hip_atomic_fetch_add(&lds.cnt[p * 64 + lane], cnt[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    // (every wave's error-word atomics are performed before its workgroup's ticket: a staged
+    // launch's last group reads the word)
+    if (a.staged) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 #ifdef AC_COUNTS_DIRECT  // A/B variant: every workgroup adds straight into the (pre-zeroed) counts
     if (wib == 0) {
@@ -632,12 +790,30 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
                 if (cand[p] < sg.n_kmers) {
                     if (a.add_counts) {
                         if (v) atomicAdd(&sg.counts[cand[p]], v);
+                    } else if (a.staged) {  // host memory the host reads before the stream completes
+                        __hip_atomic_store(&sg.counts[cand[p]], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     } else {
                         sg.counts[cand[p]] = v;
                     }
                 }
             }
             if (lane == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (a.staged) {
+                // the launch's last group publishes its error bits, then its completion, to the host
+                // (its counts went out as system-scope stores; each group's, drained before its add)
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                uint32_t last = 0;
+                if (lane == 0)
+                    last = __hip_atomic_fetch_add(a.stage + AC_STAGE_L_GROUPS * AC_QUEUE_LINE, 1u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT) == a.total_groups - 1u;
+                if (__builtin_amdgcn_readfirstlane(last) && lane == 0) {
+                    uint32_t* res = a.host_hdr + AC_MAX_SEGS * AC_QUEUE_LINE;
+                    const uint32_t e = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(res + AC_HDR_ERR, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    __hip_atomic_store(res + AC_HDR_DONE, a.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
+            }
         }
     }
 #endif
@@ -669,7 +845,11 @@ hipError_t occupancy(int cu_count, uint32_t* waves) {
 
 #ifdef AC_STAMPS
 hipError_t debug_stamps(void* host, size_t bytes) {
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), bytes < sizeof(g_stamps) ? bytes : sizeof(g_stamps), 0,
+    // g_stamps, then g_stage_stamps
+    const size_t a = bytes < sizeof(g_stamps) ? bytes : sizeof(g_stamps);
+    hipError_t e = hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), a, 0, hipMemcpyDeviceToHost);
+    if (e != hipSuccess || bytes < sizeof(g_stamps) + sizeof(g_stage_stamps)) return e;
+    return hipMemcpyFromSymbol((char*)host + sizeof(g_stamps), HIP_SYMBOL(g_stage_stamps), sizeof(g_stage_stamps), 0,
                                hipMemcpyDeviceToHost);
 }
 #endif

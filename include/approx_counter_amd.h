@@ -182,6 +182,40 @@ ac_status ac_error_count_sample(ac_ctx* ctx, uint32_t k, const uint64_t* kmers, 
                                 const ac_windows* dev, uint64_t* counts);
 
 /*
+ * ac_sample_upload into upload slot `slot` (0 .. AC_MAX_JOBS-1; slot 0 is
+ * ac_sample_upload's), so both read ends of a run stay on the device at once:
+ * each is uploaded once and serves its exact count and the fused approximate
+ * count below.  Valid until the next upload into the same slot.
+ */
+ac_status ac_sample_upload_slot(ac_ctx* ctx, int slot, const ac_windows* host, ac_windows* dev);
+
+/* One errorCount call (approx_counter.cpp:922) over a packed sample: host
+ * k-mers, host uint64 counts; `sample` is a device sample (ac_error_count_samples)
+ * or a host image (ac_error_count_images). */
+typedef struct ac_sample_job {
+    const uint64_t* kmers;
+    uint32_t n_kmers;
+    ac_windows sample;
+    uint64_t* counts;
+} ac_sample_job;
+
+/*
+ * errorCount for up to AC_MAX_JOBS calls sharing k -- both read ends of one run
+ * (the loop at approx_counter.cpp:858-953) -- in ONE fused kernel launch over
+ * samples already on the device (ac_sample_upload_slot): the CLI's path, where
+ * each end's upload first serves its exact count.  Synchronous.
+ */
+ac_status ac_error_count_samples(ac_ctx* ctx, uint32_t k, const ac_sample_job* jobs, uint32_t n_jobs);
+
+/*
+ * The same over host images: on one device one fused launch; on an
+ * ac_create_multi context every job's windows are cut into one contiguous shard
+ * per device (balanced by bases), each device counts its shards of all jobs in
+ * one fused launch, and the shard counts are summed (the CLI's -g N).
+ */
+ac_status ac_error_count_images(ac_ctx* ctx, uint32_t k, const ac_sample_job* jobs, uint32_t n_jobs);
+
+/*
  * Host packing of Dna5 windows into a window image (no reference counterpart:
  * SeqAn keeps 1 byte per base; this is the boundary's wire format).
  *   dna5     : window bytes, ordValues 0..3 for ACGT, >= 4 for N
@@ -307,18 +341,23 @@ int ac_plan_host_cpus(const char* const* rank_cpulists, int n_ranks, int rank, c
 
 /*
  * How ac_error_count_jobs moves the packed inputs (no reference counterpart):
- * 1 = zero-copy (the kernel reads the pinned staging block over PCIe), 0 = the
- * DMA path: each job copied into device memory as soon as it is packed, without
- * its N bitmap when it holds no N and without window descriptors when its
- * windows have one length (either way the kernel writes the counts into the
- * pinned block), -1 =
- * not decided yet.  Unless AC_STAGE_ZEROCOPY=1/0 forces one: a call whose
- * image x candidate groups exceeds 256 MB always takes the DMA (zero-copy may
- * read the image over PCIe once per group) and then reports 0; for smaller
- * calls a context times its first synchronous calls both ways (they alternate;
- * 10 calls), uses the faster by median of each path's last 4 calls, and every
- * 64th call takes the other path to keep its figures current: which one wins
- * depends on the host (PCIe / host-memory latency under other load).
+ * 2 = the early launch (default for calls counted in one part on one device):
+ * the count kernel is launched before the host packs, the host flags each job
+ * in the pinned block as soon as it is packed, and the kernel copies the job
+ * into device memory itself and counts it while later jobs are still being
+ * packed; its last workgroup writes the counts and a completion word into
+ * pinned memory, which the host polls (AC_STAGE_EARLY=0 turns it off).
+ * Otherwise 1 = zero-copy (the kernel reads the pinned staging block over PCIe),
+ * 0 = the DMA path: each job copied into device memory as soon as it is packed,
+ * without its N bitmap when it holds no N and without window descriptors when
+ * its windows have one length (either way the kernel writes the counts into the
+ * pinned block), -1 = not decided yet.  Unless AC_STAGE_ZEROCOPY=1/0 forces one:
+ * a call whose image x candidate groups exceeds 256 MB always takes the DMA
+ * (zero-copy may read the image over PCIe once per group) and then reports 0;
+ * for smaller calls a context times its first synchronous calls both ways (they
+ * alternate; 10 calls), uses the faster by median of each path's last 4 calls,
+ * and every 64th call takes the other path to keep its figures current: which
+ * one wins depends on the host (PCIe / host-memory latency under other load).
  */
 int ac_stage_mode(const ac_ctx* ctx);
 

@@ -64,6 +64,23 @@ def test_forbidden_solid_and_limits(counter):
     check(counter, wins, 16, 1.0, solid=10**6)  # nothing that solid
 
 
+@pytest.mark.parametrize("k", [16, 22])
+def test_overlapping_windows_more_positions_than_bases(counter, k):
+    """ac_windows allows overlapping windows: here every window starts at image base 0,
+    so the sample holds 6x more k-mer positions than the image has bases.  The
+    partitioned path's dense key arrays are sized by the image, so it must detect the
+    excess and recount on the hash table, not return short counts."""
+    rng = random.Random(77 + k)
+    w = cases.rand_seq(rng, 100, p_n=0.0)
+    img = ac.pack_windows([w])
+    dup = ac.PackedSample(img.codes, img.nmask, np.zeros(6, np.uint64), np.full(6, 100, np.uint32), img.n_bases)
+    thr = float(host_ref.adjust_threshold(1.5, 16, k))
+    got, n_dist, had_n = counter.exact_count(k, dup, thr, (), 10**6)
+    exp, exp_dist, exp_n = expected([w] * 6, k, thr, limit=10**6)
+    assert got == exp and (n_dist, had_n) == (exp_dist, exp_n)
+    assert all(c >= 6 for _, c in got)
+
+
 def test_edge_windows(counter):
     check(counter, [], 16, 1.0)
     check(counter, ["", "ACG", "N" * 40], 16, 1.0)

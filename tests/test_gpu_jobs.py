@@ -3,6 +3,8 @@ in, packed by the host pool, one DMA, one fused launch, counts back) and of the
 device error word (ac_check), against the CPU oracle.  Bit-exact everywhere."""
 import json
 import os
+import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -10,6 +12,8 @@ import pytest
 import approx_counter_amd as ac
 import oracle
 from tests import cases
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
@@ -219,24 +223,67 @@ def test_multi_context_shuffled_overlapping_windows():
 
 
 @pytest.mark.skipif("AC_STAGE_ZEROCOPY" in os.environ, reason="transfer path forced by the environment")
-def test_transfer_path_probe_both_ways_bit_exact():
-    """A fresh context alternates zero-copy and DMA over its first synchronous calls
-    (ac_stage_mode -1 until then), keeps the faster, and every call is bit-exact."""
-    a = cases.planted_case(31, 16, 200, 300, win_len=(0, 150), p_n=0.02)
-    b = cases.planted_case(32, 16, 90, 260, win_len=(80, 120))
-    exp = [oracle.count_myers(16, *a), oracle.count_myers(16, *b)]
+def early_rotation(calls=30):
+    """Rotates three different workloads (different sizes, N / no N, equal / ragged windows,
+    1-3 jobs) through one context's early-launch stage; every call checked."""
+    rng = np.random.default_rng(5)
+    work = []
+    for seed, (nw, lens, p_n, n_jobs) in enumerate([(900, (100, 100), 0.0, 2), (2500, (0, 150), 0.02, 3),
+                                                      (400, (101, 101), 0.01, 1)]):
+        jobs, exp = [], []
+        for j in range(n_jobs):
+            km, wins = cases.planted_case(300 + 10 * seed + j, 16, int(rng.integers(60, 400)), nw, win_len=lens,
+                                          p_n=p_n)
+            jobs.append((km, ac.Dna5Sample.from_windows(wins)))
+            exp.append(oracle.count_myers(16, km, wins))
+        work.append((ac.Jobs(jobs), exp))
     c = ac.ApproxCounter(0)
     try:
-        assert c.stage_mode() == -1
-        jobs = ac.Jobs([(a[0], _shuffled_sample(a[1], 5)), (b[0], ac.Dna5Sample.from_windows(b[1]))])
-        modes = []
-        for _ in range(12):
+        for i in range(calls):
+            jobs, exp = work[i % 3]
             got = c.count_jobs(16, jobs)
-            assert np.array_equal(got[0], exp[0]) and np.array_equal(got[1], exp[1])
-            modes.append(c.stage_mode())
-        assert modes[8] == -1 and modes[9] in (0, 1) and len(set(modes[9:])) == 1, modes
+            assert c.stage_mode() == 2, c.stage_mode()
+            for g, e in zip(got, exp):
+                assert np.array_equal(g, e), i
     finally:
         c.close()
+
+
+@pytest.mark.parametrize("mode", ["1", "2"])
+def test_early_launch_rotating_inputs_bit_exact(mode):
+    """The early-launch stage (ac_stage_mode 2): the kernel is launched before the host
+    packs (mode 2: after the first job, which the copy kernel sends ahead of it), copies
+    each later job into device memory itself once the host flags it, and the host polls a
+    completion word instead of the stream.  Staging slots alternate between calls, so
+    rotating three different workloads through one context makes every call land on a slot
+    that last held other data: any stale line read or early completion shows up as a wrong
+    count.  In a child process per mode (AC_STAGE_EARLY is read once per process)."""
+    env = dict(os.environ, AC_STAGE_EARLY=mode, PYTHONPATH=ROOT)
+    code = "from tests.test_gpu_jobs import early_rotation; early_rotation(45); print('OK')"
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=200, cwd=ROOT)
+    assert r.returncode == 0 and "OK" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])
+
+
+def test_early_launch_unflagged_job_fails_cleanly():
+    """The early-launch kernel's waits are bounded: a job the host never flags (test hook)
+    makes its waves give up after 0.5 s, report it, and the launch still completes -- the
+    call fails with AC_ERR_INTERNAL instead of hanging, in a child process (the hook is read
+    once per process)."""
+    code = (
+        "import numpy as np, approx_counter_amd as ac\n"
+        "from tests import cases\n"
+        "a = cases.planted_case(41, 16, 100, 200, win_len=(100, 101))\n"
+        "b = cases.planted_case(42, 16, 100, 200, win_len=(100, 101))\n"
+        "c = ac.ApproxCounter(0)\n"
+        "try:\n"
+        "    c.count_jobs(16, [(a[0], ac.Dna5Sample.from_windows(a[1])), (b[0], ac.Dna5Sample.from_windows(b[1]))])\n"
+        "    print('NO ERROR')\n"
+        "except ac.ApproxCounterError as e:\n"
+        "    print('STATUS', e.status, e)\n"
+    )
+    env = dict(os.environ, AC_STAGE_TEST_UNFLAGGED="1", AC_STAGE_EARLY="1", PYTHONPATH=ROOT)
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=100, cwd=ROOT)
+    assert "STATUS 4" in r.stdout and "timed out" in r.stdout, (r.stdout, r.stderr[-2000:])
 
 
 def test_image_size_limit_rejected(counter):
@@ -306,3 +353,43 @@ def test_rccl_allreduce_single_rank(counter):
     got = out.cpu().numpy().view(np.uint32).astype(np.uint64)
     assert np.array_equal(got[:300], oracle.count_myers(16, *a))
     assert np.array_equal(got[300:], oracle.count_myers(16, *b))
+
+
+def _permuted_image(wins, seed):
+    """A packed image whose window descriptors come in shuffled order, plus one window
+    listed twice (overlap): (image, the windows in descriptor order)."""
+    img = ac.pack_windows(wins)
+    rng = np.random.default_rng(seed)
+    order = rng.permutation(len(wins))
+    order = np.concatenate([order, order[:1]])
+    return (ac.PackedSample(img.codes, img.nmask, img.start[order].copy(), img.length[order].copy(), img.n_bases),
+            [wins[i] for i in order])
+
+
+@pytest.mark.parametrize("n_gpus", [0, 3])
+def test_images_fused_and_sharded(n_gpus):
+    """ac_error_count_images (the CLI's approximate count): both read ends' host images in
+    ONE fused launch per device; on an n_gpus context each end's windows are cut into one
+    shard per device and the shard counts summed.  Shuffled and repeated descriptors."""
+    a = cases.planted_case(51, 16, 300, 700, win_len=(100, 100), p_n=0.01)
+    b = cases.planted_case(52, 16, 200, 600, win_len=(0, 101), p_n=0.01)
+    ia, wa = _permuted_image(a[1], 1)
+    ib, wb = _permuted_image(b[1], 2)
+    with ac.ApproxCounter(0, n_gpus=n_gpus) as c:
+        got = c.count_images(16, [(a[0], ia), (b[0], ib)])
+    assert np.array_equal(got[0], oracle.count_myers(16, a[0], wa))
+    assert np.array_equal(got[1], oracle.count_myers(16, b[0], wb))
+
+
+def test_samples_two_upload_slots_fused(counter):
+    """Both ends uploaded once (slots 0 and 1), the exact count run on each upload, then one
+    fused approximate launch over the two device samples (ac_error_count_samples)."""
+    a = cases.planted_case(61, 16, 250, 500, win_len=(100, 100), p_n=0.01)
+    b = cases.planted_case(62, 22, 120, 400, win_len=(151, 151), p_n=0.01)
+    for k, (x, y) in ((16, (a, a)), (22, (b, b))):
+        ix, iy = ac.pack_windows(x[1]), ac.pack_windows(y[1][::-1])
+        dx = counter.upload_sample(ix, 0)
+        dy = counter.upload_sample(iy, 1)
+        got = counter.count_samples(k, [(x[0], dx), (y[0][::-1].copy(), dy)])
+        assert np.array_equal(got[0], oracle.count_myers(k, x[0], x[1]))
+        assert np.array_equal(got[1], oracle.count_myers(k, y[0][::-1].copy(), y[1][::-1]))
