@@ -128,6 +128,8 @@ def load():
     L.ac_check.restype = ctypes.c_int
     L.ac_stage_mode.argtypes = [vp]
     L.ac_stage_mode.restype = ctypes.c_int
+    L.ac_exact_path.argtypes = [vp]
+    L.ac_exact_path.restype = ctypes.c_int
     pint = ctypes.POINTER(ctypes.c_int)
     L.ac_set_host_cpus.argtypes = [pint, ctypes.c_int, ctypes.c_int]
     L.ac_set_host_cpus.restype = ctypes.c_int

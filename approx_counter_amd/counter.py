@@ -102,6 +102,11 @@ class Dna5Sample:
         self.bases = np.ascontiguousarray(bases, dtype=np.uint8)
         self.offset = np.ascontiguousarray(offset, dtype=np.uint64)
         self.length = np.ascontiguousarray(length, dtype=np.uint32)
+        if self.offset.shape != self.length.shape:
+            raise ValueError("Dna5Sample: offset and length differ in size")
+        # ac_dna5_windows carries no size for `bases`: the packer would read past the buffer
+        if self.length.size and int((self.offset + self.length.astype(np.uint64)).max()) > self.bases.size:
+            raise ValueError("Dna5Sample: a window reaches past the end of `bases`")
         if self.bases.size == 0:
             self.bases = np.zeros(1, np.uint8)
 
@@ -263,6 +268,10 @@ class ApproxCounter:
     def count_samples(self, k: int, parts) -> list:
         """ac_error_count_samples: [(kmers, device sample from upload_sample), ...], one fused launch."""
         return self._sample_jobs(self._L.ac_error_count_samples, k, parts)
+
+    def exact_path(self) -> int:
+        """ac_exact_path: 1 partitioned, 0 hash table, -1 no exact count yet."""
+        return int(self._L.ac_exact_path(self._h))
 
     def stage_mode(self) -> int:
         """ac_stage_mode: 1 zero-copy, 0 DMA, -1 not decided yet (count_jobs probes both first)."""

@@ -99,10 +99,15 @@ struct ac_ctx {
         size_t h_cap = 0, d_cap = 0;
         hipEvent_t ev = nullptr;
         bool pending = false;
+        // the early launch's header (flags, completion): coherent (fine-grained) pinned memory, so
+        // the kernel's polls of it reach host memory every time instead of an L2 line
+        uint32_t* hdr = nullptr;
+        uint32_t* hdr_d = nullptr;
     } slot[3 * AC_STAGE_MAX_PARTS];  // synchronous parts, then two sets of submit parts
     uint32_t next_slot = 0;          // the submit set the next submit uses
     uint32_t gen = 0;                // generation of the last early-launch call (never 0 once used)
     uint32_t early_flip = 0;         // early-launch calls alternate between staging slots 0 and 1
+    int exact_path = -1;             // the last exact count's path: 1 partitioned, 0 hash table
     // zero-copy vs DMA choice of the host-buffer stage (ac_stage_mode)
     int zc_choice = -1;
     int zc_last = -1;  // 0: the last synchronous call was too large for zero-copy, 2: it was an early launch (ac_stage_mode)
@@ -599,6 +604,7 @@ void ac_destroy(ac_ctx* ctx) {
     if (ctx->h_err) (void)hipHostFree(ctx->h_err);
     for (auto& sl : ctx->slot) {
         if (sl.ev) (void)hipEventSynchronize(sl.ev);
+        if (sl.hdr) (void)hipHostFree(sl.hdr);
         if (sl.h) (void)hipHostFree(sl.h);
         if (sl.d) (void)hipFree(sl.d);
         if (sl.ev) (void)hipEventDestroy(sl.ev);
@@ -874,20 +880,21 @@ ac_status ac_exact_count_device(ac_ctx* ctx, uint32_t k, const ac_windows* dev, 
         return fail(ctx, AC_ERR_INVALID, "NULL output or forbidden array");
     AC_HIP(ctx, hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
-    // k <= 16 takes the partitioned path (exact_count.hip: dense keys, bucket
-    // partition, per-bucket LDS count; no global table); k > 16, or a bucket
-    // that outgrows its LDS table, the hash-table path.  AC_EXACT_HASH=1
-    // forces the hash table (A/B).
+    // The partitioned path (exact_count.hip: dense keys -- 32-bit for k <= 16, 64-bit above --,
+    // bucket partition, per-bucket LDS count; no global table); a sample too large for it, or
+    // a bucket that outgrows its LDS table, takes the hash-table path.  AC_EXACT_HASH=1 forces
+    // the hash table (A/B; tests/test_gpu_exact.py runs both).
     const bool compact = k <= acamd::EXACT_COMPACT_MAX_K;
     static const bool force_hash = std::getenv("AC_EXACT_HASH") != nullptr;
-    bool partitioned = compact && !force_hash;
+    bool partitioned = !force_hash;
+    const size_t key_bytes = compact ? sizeof(uint32_t) : sizeof(uint64_t);
     // k-mer positions <= image bases: the capacity of the dense key arrays,
     // and of the list when every kept entry must be listed (threshold 1).
     const uint64_t key_cap = std::max<uint64_t>(32, dev->n_bases);
-    // Up to 8,192 buckets of <= ~2,048 keys (the per-bucket LDS table holds
-    // 4,096; the histogram / scatter kernels keep one LDS cursor per bucket):
-    // larger samples take the hash table.
-    if (key_cap > (uint64_t(8192) << 11)) partitioned = false;
+    // Up to 2^16 buckets of <= ~2,048 keys (the per-bucket LDS table holds 4,096; 1,024 super-buckets
+    // of 64 buckets, one LDS cursor each in the scatters): 134M positions, cfg4's 10^6 windows per
+    // read end included; larger samples take the hash table.
+    if (key_cap > (uint64_t(1) << (16 + 11))) partitioned = false;
     // Distinct kept k-mers <= image positions (a k-mer is fixed by its image position, whichever
     // overlapping windows cover it), so this list never overflows; n_bases / 2 (entries seen at
     // least twice, disjoint windows) did for duplicated windows.
@@ -935,24 +942,26 @@ ac_status ac_exact_count_device(ac_ctx* ctx, uint32_t k, const ac_windows* dev, 
     if (partitioned) {
         // buckets: about 1,024-2,048 keys each (the LDS table holds 4,096)
         uint32_t nb_log2 = 6;
-        while (nb_log2 < 13 && (key_cap >> nb_log2) > 2048) ++nb_log2;
+        while (nb_log2 < 16 && (key_cap >> nb_log2) > 2048) ++nb_log2;
         a.nb_log2 = nb_log2;
         a.key_cap = key_cap;
-        a.s_log2 = nb_log2 > 7 ? 7 : nb_log2;  // 128 super-buckets of <= 64 buckets
-        a.n_chunks = (uint32_t)((key_cap + EXACT_CHUNK - 1) / EXACT_CHUNK);
+        // super-buckets of <= 64 buckets, at least 128 of them when there are that many buckets
+        a.s_log2 = std::max(std::min(nb_log2, 7u), nb_log2 - 6u);
+        const uint32_t chunk = acamd::exact_part_chunk(k);
+        a.n_chunks = (uint32_t)((key_cap + chunk - 1) / chunk);
         a.n_chunks2 = a.n_chunks + (1u << a.s_log2);
         const size_t NB = size_t(1) << nb_log2, S = size_t(1) << a.s_log2;
         const size_t h1 = S * a.n_chunks, h2 = (NB / S) * a.n_chunks2;
-        if (ac_status s2 = grow(ctx, &ctx->e_buf[6], &ctx->e_cap[6], sizeof(uint32_t) * key_cap)) return s2;
-        if (ac_status s2 = grow(ctx, &ctx->e_buf[7], &ctx->e_cap[7], sizeof(uint32_t) * key_cap)) return s2;
-        if (ac_status s2 = grow(ctx, &ctx->e_buf[8], &ctx->e_cap[8], sizeof(uint32_t) * key_cap)) return s2;
+        if (ac_status s2 = grow(ctx, &ctx->e_buf[6], &ctx->e_cap[6], key_bytes * key_cap)) return s2;
+        if (ac_status s2 = grow(ctx, &ctx->e_buf[7], &ctx->e_cap[7], key_bytes * key_cap)) return s2;
+        if (ac_status s2 = grow(ctx, &ctx->e_buf[8], &ctx->e_cap[8], key_bytes * key_cap)) return s2;
         if (ac_status s2 = grow(ctx, &ctx->e_buf[9], &ctx->e_cap[9], sizeof(uint32_t) * (h1 + h2 + S))) return s2;
         if (ac_status s2 = grow(ctx, &ctx->e_buf[10], &ctx->e_cap[10], sizeof(uint32_t) * (NB + 1))) return s2;
         if (ac_status s2 = grow(ctx, &ctx->e_buf[11], &ctx->e_cap[11], sizeof(uint32_t) * NB * EXACT_PHIST)) return s2;
         a.phist = (uint32_t*)ctx->e_buf[11];
-        a.keys = (uint32_t*)ctx->e_buf[6];
-        a.parts = (uint32_t*)ctx->e_buf[7];
-        a.tmp = (uint32_t*)ctx->e_buf[8];
+        a.keys = ctx->e_buf[6];
+        a.parts = ctx->e_buf[7];
+        a.tmp = ctx->e_buf[8];
         a.h1 = (uint32_t*)ctx->e_buf[9];
         a.h2 = a.h1 + h1;
         a.stot = a.h2 + h2;
@@ -988,6 +997,7 @@ ac_status ac_exact_count_device(ac_ctx* ctx, uint32_t k, const ac_windows* dev, 
         AC_HIP(ctx, hipStreamSynchronize(st));
     }
     if (ac_status rc = device_error(ctx, *(const uint32_t*)(h_small.data() + 40))) return rc;
+    ctx->exact_path = partitioned ? 1 : 0;
     const uint32_t* hist = (const uint32_t*)(h_small.data() + 64);
     uint64_t kept = 0;
     for (int i = 0; i < EXACT_HIST_BINS; ++i) kept += hist[i];
@@ -1303,7 +1313,7 @@ struct JobPlan {
     uint64_t n_bases[AC_MAX_JOBS] = {};
     size_t off_kmers[AC_MAX_JOBS] = {}, off_codes[AC_MAX_JOBS] = {}, off_nmask[AC_MAX_JOBS] = {};
     size_t off_start[AC_MAX_JOBS] = {}, off_len[AC_MAX_JOBS] = {}, off_counts[AC_MAX_JOBS] = {};
-    size_t off_err = 0, off_hdr = 0, total = 0;
+    size_t off_err = 0, total = 0;
     bool early = false;  // the early-launch stage (the kernel stages its own inputs, host-polled completion)
     uint32_t gen = 0;    // its generation (the header flags and completion word carry it)
     int slot = 0;     // staging slot (set by the caller: a synchronous part q uses slot q, a submit part its set's)
@@ -1312,9 +1322,7 @@ struct JobPlan {
     bool zc_eligible = true;  // false: the image is too large for zero-copy (DMA, not measured)
 };
 
-// AC_STAGE_PARTS (1-4) and AC_STAGE_SPLIT (with two parts, the first part's
-// share of the bases, default 0.5): switches of the synchronous stage.
-// Without AC_STAGE_PARTS: calls whose pack and DMA take hundreds of
+// Calls whose pack and DMA take hundreds of
 // microseconds or more are cut into parts (equal bases, one stream each), so
 // part q + 1 is packed and sent while part q counts: two parts from 2^17
 // windows, four from 2^19.  Same box, interleaved (profiles/r02_stage_parts_ab2.log):
@@ -1324,11 +1332,6 @@ struct JobPlan {
 // and 3.42 one-part DMA.
 constexpr uint64_t STAGE_PARTS2_MIN_WINDOWS = 1ull << 17, STAGE_PARTS4_MIN_WINDOWS = 1ull << 19;
 int stage_parts(uint64_t total_w) {
-    static const int env = [] {
-        const char* e = std::getenv("AC_STAGE_PARTS");
-        return e ? std::max(1, std::min(AC_STAGE_MAX_PARTS, std::atoi(e))) : 0;
-    }();
-    if (env) return env;
     return total_w >= STAGE_PARTS4_MIN_WINDOWS ? 4 : total_w >= STAGE_PARTS2_MIN_WINDOWS ? 2 : 1;
 }
 // Zero-copy stage (default; AC_STAGE_ZEROCOPY=0 = DMA in and out): the count
@@ -1338,7 +1341,6 @@ int stage_parts(uint64_t total_w) {
 // the contiguous item ranges of the work queues make each XCD read a slice of
 // the sample; it saves the DMA (1.2 MB, ~27 us at cfg2), the ~9 us
 // DMA-to-kernel dependency and the D2H blit.
-// AC_STAGE_HOSTALLOC=coherent|noncoherent|wc: the pinned block's flags (A/B).
 int stage_zerocopy_env() {  // 1 / 0 forced by AC_STAGE_ZEROCOPY, -1 = automatic
     static const int v = [] {
         const char* e = std::getenv("AC_STAGE_ZEROCOPY");
@@ -1385,49 +1387,12 @@ void stage_zerocopy_record(ac_ctx* ctx, bool zc, double us) {
         ctx->zc_choice = median(ctx->zc_us[1]) <= median(ctx->zc_us[0]) ? 1 : 0;
     }
 }
-unsigned stage_host_flags() {
-    static const unsigned v = [] {
-        const char* e = std::getenv("AC_STAGE_HOSTALLOC");
-        if (e && std::string(e) == "coherent") return (unsigned)hipHostMallocCoherent;
-        if (e && std::string(e) == "noncoherent") return (unsigned)hipHostMallocNonCoherent;
-        if (e && std::string(e) == "wc") return (unsigned)hipHostMallocWriteCombined;
-        return (unsigned)hipHostMallocDefault;
-    }();
-    return v;
-}
-
-// DMA-mode transfer of a one-part call (default, AC_STAGE_BLIT=0 turns it off):
-// a copy kernel on the compute queue reads the pinned block once over PCIe and
-// writes the device block, so the count kernel follows it on the same queue;
-// otherwise hipMemcpyAsync (the copy engine, whose completion -> kernel start
-// costs ~9 us at cfg2).  With the job-by-job pipeline below: cfg2 sync 114-118
-// vs 130-132 us, step p50 0.156-0.158 vs 0.164-0.167 ms on one loaded box
-// (profiles/r02_stage_pipe_blit_ab.log); alone it gained nothing (128 vs 130 us).
-int stage_blit() {
-    static const int v = [] {
-        const char* e = std::getenv("AC_STAGE_BLIT");
-        return e ? (std::atoi(e) != 0 ? 1 : 0) : 1;
-    }();
-    return v;
-}
-// DMA mode packs and sends job by job, so job j's inputs travel while job j + 1
-// is packed (default; AC_STAGE_PIPE=0 = pack everything, then one transfer).
-int stage_pipe() {
-    static const int v = [] {
-        const char* e = std::getenv("AC_STAGE_PIPE");
-        return e ? (std::atoi(e) != 0 ? 1 : 0) : 1;
-    }();
-    return v;
-}
-// Equal-length windows counted with arithmetic descriptors (default;
-// AC_STAGE_ULEN=0 sends and reads the descriptors, A/B)
-int stage_ulen() {
-    static const int v = [] {
-        const char* e = std::getenv("AC_STAGE_ULEN");
-        return e ? (std::atoi(e) != 0 ? 1 : 0) : 1;
-    }();
-    return v;
-}
+// DMA-mode transfer of a one-part call: a copy kernel on the compute queue reads the pinned
+// block once over PCIe and writes the device block, so the count kernel follows it on the
+// same queue, rather than hipMemcpyAsync (the copy engine, whose completion -> kernel start
+// costs ~9 us at cfg2); job by job, so job j's inputs travel while job j + 1 is packed; equal
+// windows counted with arithmetic descriptors.  Each won its A/B (profiles/r02_stage_pipe_blit_ab.log:
+// sync 114-118 vs 130-132 us; r02_stage_ulen_ab.log), and the switches are gone.
 // Shape (A/B builds: tools/variants.sh).  64-thread workgroups with 4 loads in flight per
 // thread measured faster on one box -- cfg2 stage p50 0.146-0.147 ms vs 0.150-0.159 for
 // 256 x 2 (profiles/r02_blit_shape_ab.log) -- but no GPU box was free to run the test
@@ -1460,15 +1425,6 @@ hipError_t stage_blit_launch(const void* src_dev, void* dst, size_t bytes, hipSt
     const uint32_t blocks = (uint32_t)((n16 + per - 1) / per);
     stage_blit_kernel<<<blocks, BLIT_THREADS, 0, stream>>>((const u32x4*)src_dev, (u32x4*)dst, (uint32_t)n16);
     return hipGetLastError();
-}
-
-double stage_split() {
-    static const double v = [] {
-        const char* e = std::getenv("AC_STAGE_SPLIT");
-        const double f = e ? std::atof(e) : 0.5;
-        return std::max(0.05, std::min(0.95, f));
-    }();
-    return v;
 }
 
 // The early-launch stage for one-part synchronous calls (default; AC_STAGE_EARLY=0 = the
@@ -1609,8 +1565,6 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
         p.off_counts[j] = off;
         off = align256(off + sizeof(uint32_t) * jobs[j].n_kmers);
     }
-    p.off_hdr = off;  // the early launch's header lines (AC_HDR_LINES of them, 128 B each)
-    off = align256(off + sizeof(uint32_t) * AC_QUEUE_LINE * AC_HDR_LINES);
     p.total = off;
     // Zero-copy's worst case moves the image over PCIe once per candidate group (ZC_MAX_PCIE_BYTES).
     uint64_t pcie_bytes = 0;
@@ -1634,7 +1588,7 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
         sl.hd = nullptr;
         sl.h_cap = 0;
         const size_t cap = p.total + p.total / 4;
-        AC_HIP(ctx, hipHostMalloc(&sl.h, cap, stage_host_flags()));
+        AC_HIP(ctx, hipHostMalloc(&sl.h, cap, hipHostMallocDefault));
         sl.h_cap = cap;
         AC_HIP(ctx, hipHostGetDevicePointer(&sl.hd, sl.h, 0));
     }
@@ -1651,8 +1605,13 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
     *(uint32_t*)(h + p.off_err) = 0u;
     // early launch: flags and the completion word cleared before the launch (the slot's last
     // launch has finished: its event was waited for above)
-    uint32_t* hdr = (uint32_t*)(h + p.off_hdr);
-    if (p.early) std::memset(hdr, 0, sizeof(uint32_t) * AC_QUEUE_LINE * AC_HDR_LINES);
+    const size_t hdr_bytes = sizeof(uint32_t) * AC_QUEUE_LINE * AC_HDR_LINES;
+    if (p.early && !sl.hdr) {
+        AC_HIP(ctx, hipHostMalloc((void**)&sl.hdr, hdr_bytes, hipHostMallocCoherent | hipHostMallocMapped));
+        AC_HIP(ctx, hipHostGetDevicePointer((void**)&sl.hdr_d, sl.hdr, 0));
+    }
+    uint32_t* hdr = sl.hdr;
+    if (p.early) std::memset(hdr, 0, hdr_bytes);
     mark(1);
     // per task: did its windows hold an N (its N-bitmap words, or-ed after packing; still in cache)
     std::vector<uint8_t> task_n(tasks.size(), 0);
@@ -1684,7 +1643,7 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
                 any = true;
                 equal = equal && x.len_diff == 0u && x.first_len == l0;
             }
-        ulen[j] = (any && equal && stage_ulen()) ? l0 : AC_NO_ULEN;
+        ulen[j] = (any && equal) ? l0 : AC_NO_ULEN;
     }
     char* d = zc ? (char*)sl.hd : (char*)sl.d;
     // In both modes the kernel writes the error word and the counts straight into the pinned
@@ -1717,7 +1676,7 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
         StageLaunch stg;
         if (++ctx->gen == 0) ++ctx->gen;
         p.gen = stg.gen = ctx->gen;
-        stg.host_hdr = (uint32_t*)(hd + p.off_hdr);
+        stg.host_hdr = sl.hdr_d;
         for (uint32_t j = 0; j < p.n; ++j) {
             const size_t end = ulen[j] != AC_NO_ULEN ? p.off_start[j] : (j + 1 < p.n ? p.off_kmers[j + 1] : p.off_err);
             region[j] = end - p.off_kmers[j];
@@ -1772,6 +1731,7 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
                 static const bool unflag = std::getenv("AC_STAGE_TEST_UNFLAGGED") != nullptr;
                 if (!(unflag && j + 1 == p.n))
                     __atomic_store_n(&line[AC_HDR_FLAG], p.gen, __ATOMIC_RELEASE);  // the kernel's waves may go
+                if (j == 0) mark(3);  // (AC_STAGE_TRACE: launch -> first job flagged, in "h2d_enq")
             }
             t0 = t1;
         }
@@ -1782,10 +1742,10 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
     // DMA mode sends the inputs [r0, r1) of the slot (copy engine or blit kernel)
     auto transfer = [&](size_t r0, size_t r1) -> hipError_t {
         if (r1 <= r0) return hipSuccess;
-        if (stage_blit() && part == 0 && wave_div == 0) return stage_blit_launch(hd + r0, d + r0, r1 - r0, stream);
+        if (part == 0 && wave_div == 0) return stage_blit_launch(hd + r0, d + r0, r1 - r0, stream);
         return hipMemcpyAsync(d + r0, h + r0, r1 - r0, hipMemcpyHostToDevice, stream);
     };
-    if (!zc && stage_pipe() && p.n > 1) {
+    if (!zc && p.n > 1) {
         // job by job: job j's inputs travel while job j + 1 is packed.  One pool job for all
         // tasks (they are in job order); the caller packs job j's share, waits for its last
         // task, sends it, then helps with job j + 1 while the workers carry on.
@@ -1878,7 +1838,7 @@ uint32_t part_cut(const uint32_t* length, uint32_t n, double frac) {
 }
 
 // Every job's part boundaries of a single-device call in `parts` parts, once
-// (equal shares of the bases; two parts: AC_STAGE_SPLIT of them in the first).
+// (equal shares of the bases).
 std::vector<std::vector<uint32_t>> part_cuts(const ac_job* jobs, uint32_t n_jobs, int parts) {
     std::vector<std::vector<uint32_t>> cuts;
     for (uint32_t j = 0; j < n_jobs; ++j) {
@@ -1886,7 +1846,7 @@ std::vector<std::vector<uint32_t>> part_cuts(const ac_job* jobs, uint32_t n_jobs
         if (parts == 1)
             cuts.push_back({0u, n});
         else if (parts == 2)
-            cuts.push_back({0u, part_cut(jobs[j].sample.length, n, stage_split()), n});
+            cuts.push_back({0u, part_cut(jobs[j].sample.length, n, 0.5), n});
         else
             cuts.push_back(shard_cuts(jobs[j].sample.length, n, (size_t)parts));
     }
@@ -1991,7 +1951,7 @@ ac_status ac_error_count_jobs(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint3
             // the kernel's last workgroup writes the completion word after every count: poll it
             // instead of waiting for the stream (the launch's event is waited for when the slot is
             // next used)
-            const uint32_t* res = (const uint32_t*)(h + u.plan.off_hdr) + AC_MAX_SEGS * AC_QUEUE_LINE;
+            const uint32_t* res = sl.hdr + AC_MAX_SEGS * AC_QUEUE_LINE;
             if (ac_status st = wait_early(u.c, res + AC_HDR_DONE, u.plan.gen, u.stream)) return st;
             err_word = __atomic_load_n(res + AC_HDR_ERR, __ATOMIC_ACQUIRE);
         } else {
@@ -2093,6 +2053,8 @@ ac_status ac_error_count_jobs_submit(ac_ctx* ctx, uint32_t k, const ac_job* jobs
     }
     return AC_OK;
 }
+
+int ac_exact_path(const ac_ctx* ctx) { return ctx ? ctx->exact_path : -1; }
 
 int ac_stage_mode(const ac_ctx* ctx) {
     if (!ctx) return -1;

@@ -65,15 +65,15 @@ struct ExactArgs {
     uint32_t* out_cnts;
     unsigned long long* n_out;
     uint64_t out_cap;
-    // Partitioned path (k <= 16): every k-mer position's key
+    // Partitioned path: every k-mer position's key
     // written densely (`keys`, n_keys of them), moved into 2^s_log2
     // super-buckets (`tmp`; per-chunk histogram h1 [chunk][super], sizes
     // stot), then into the 2^nb_log2 buckets (`parts`; per level-2 chunk
     // histogram h2 [chunk][sub]; bucket starts bstart, nb + 1 of them); one
     // workgroup per bucket counts its keys in LDS.  No global hash table.
-    uint32_t* keys;
-    uint32_t* tmp;
-    uint32_t* parts;
+    void* keys;   // uint32_t keys for k <= 16, uint64_t above
+    void* tmp;
+    void* parts;
     unsigned long long* n_keys;
     uint32_t* h1;
     uint32_t* h2;
@@ -81,7 +81,7 @@ struct ExactArgs {
     uint32_t* bstart;  // nb + 1
     uint32_t nb_log2;
     uint32_t s_log2;    // super-buckets: nb_log2 - s_log2 <= 6
-    uint32_t n_chunks;  // level-1 grid: ceil(key capacity / EXACT_CHUNK)
+    uint32_t n_chunks;  // level-1 grid: ceil(key capacity / exact_part_chunk(k))
     uint32_t n_chunks2; // level-2 grid bound: n_chunks + 2^s_log2
     uint64_t key_cap;
     uint32_t list_min;   // the count kernel lists kept entries with count >= list_min
@@ -92,8 +92,7 @@ struct ExactArgs {
 
 #define EXACT_PHIST 32  // per-bucket partial histogram bins (counts 1..32; larger counts go straight to hist)
 
-#define EXACT_CHUNK 8192  // keys per histogram / scatter workgroup of either partition level (16,384: 2 scatter workgroups per CU, level-2 scatter 37 us)
-#define EXACT_MAX_SUPER 128  // level-1 super-buckets (at most)
+#define EXACT_MAX_SUPER 1024  // level-1 super-buckets (at most): 2^16 buckets of <= 64 sub-buckets each
 #define EXACT_MAX_SUB 64     // buckets per super-bucket (at most)
 #define EXACT_BUCKET_SLOTS 4096  // LDS counting table of the per-bucket kernel (32 KB of keys + counts)
 
@@ -105,6 +104,9 @@ hipError_t launch_exact_gather(const ExactArgs& a, bool from_list, uint64_t n_li
 // hist / list / special like insert + scan).  `count_only` re-runs just the
 // per-bucket count (with a.list_min / a.emit_only) on the partition already built.
 hipError_t launch_exact_partitioned(const ExactArgs& a, hipStream_t stream);
+// Keys per histogram / scatter chunk of the partitioned path for k (8,192 32-bit or 4,096 64-bit keys:
+// one chunk staged in 32 KB of LDS; 16,384 gave 2 scatter workgroups per CU, level-2 scatter 37 us).
+uint32_t exact_part_chunk(uint32_t k);
 hipError_t launch_exact_part_count(const ExactArgs& a, hipStream_t stream);
 
 }  // namespace acamd

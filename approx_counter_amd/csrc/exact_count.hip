@@ -444,27 +444,36 @@ __global__ __launch_bounds__(EXACT_THREADS) void exact_gather_list_kernel(ExactA
 }
 
 // ---------------------------------------------------------------------------
-// Partitioned path (k <= 16).  The hash-table insert above is bound by its
-// random read-modify-write atomics in HBM (~7.5M at 10^5 windows, ~380 us of
-// a 540 us insert; profiles/r02_exact_log.md).  Here every step streams:
+// Partitioned path (every k: 32-bit keys for k <= 16, 64-bit keys above).  The
+// hash-table insert above is bound by its random read-modify-write atomics in
+// HBM (~7.5M at 10^5 windows, ~380 us of a 540 us insert;
+// profiles/r02_exact_log.md).  Here every step streams:
 //   keys     each window block writes its k-mer keys densely (one reservation
 //            per 1,024 positions), no aggregation
-//   hist     per chunk of EXACT_CHUNK keys, the count of keys per bucket
-//            (bucket = high bits of the key's hash)
+//   hist     per chunk of keys, the count of keys per bucket (bucket = high
+//            bits of the key's hash)
 //   colscan  chunk offsets inside each bucket, bucket starts
 //   scatter  keys to their bucket's range (LDS cursors per bucket)
 //   count    one workgroup per bucket counts its keys in an LDS table and
 //            runs the low-complexity / forbidden filters, the histogram and
 //            the list of the scan kernel above
-// Keys are only grouped, never ordered, so nothing has to be stable.
+// Keys are only grouped, never ordered, so nothing has to be stable.  Up to
+// 2^16 buckets of ~2,048 keys (134M k-mer positions: cfg4's 10^6 windows per
+// read end fit); larger samples take the hash table.
 
-constexpr uint32_t MAX_NB_LOG2 = 13;
+constexpr uint32_t MAX_NB_LOG2 = 16;
 constexpr uint32_t COUNT_PROBES = 64;
 
-// Hash of a k <= 16 key for the partition (its top bits pick the bucket) and
-// the per-bucket LDS table (its low bits pick the slot): a 32-bit mixer
-// (two u32 multiplies; the 64-bit murmur finaliser costs ~8 quarter-rate
-// multiplies and the partition hashes every key five times).
+// Keys per histogram / scatter chunk: the scatter stages a chunk in LDS (32 KB).
+template <class K>
+struct PartKey {
+    static constexpr uint32_t CHUNK = (uint32_t)(32768 / sizeof(K));
+};
+
+// Hash of a key for the partition (its top bits pick the bucket) and the
+// per-bucket LDS table (its low bits pick the slot): a 32-bit mixer (two u32
+// multiplies; the 64-bit murmur finaliser costs ~8 quarter-rate multiplies and
+// the partition hashes every key five times); 64-bit keys fold their high half in.
 __device__ __forceinline__ uint32_t part_hash(uint32_t x) {
     x ^= x >> 16;
     x *= 0x7feb352du;
@@ -473,8 +482,12 @@ __device__ __forceinline__ uint32_t part_hash(uint32_t x) {
     x ^= x >> 16;
     return x;
 }
+__device__ __forceinline__ uint32_t part_hash(uint64_t x) {
+    return part_hash((uint32_t)x ^ part_hash((uint32_t)(x >> 32) + 0x9e3779b9u));
+}
 
-__device__ __forceinline__ uint32_t bucket_of(uint32_t key, uint32_t nb_log2) {
+template <class K>
+__device__ __forceinline__ uint32_t bucket_of(K key, uint32_t nb_log2) {
     return part_hash(key) >> (32u - nb_log2);
 }
 
@@ -497,6 +510,26 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t& excl, 
     }
     __syncthreads();  // wsum may be reused
     excl = before + incl - x;
+    return total;
+}
+
+// In-place exclusive prefix of v[0, n) in LDS (n up to a few thousand: each
+// thread scans a contiguous run); returns the total.  The caller has a barrier
+// between the writes of v and this call; the scanned v is visible on return.
+__device__ __forceinline__ uint32_t block_scan_lds(uint32_t* v, uint32_t n, uint32_t* wsum) {
+    const uint32_t t = threadIdx.x;
+    const uint32_t per = (n + EXACT_THREADS - 1) / EXACT_THREADS;
+    const uint32_t r0 = min(n, t * per), r1 = min(n, r0 + per);
+    uint32_t local = 0;
+    for (uint32_t i = r0; i < r1; ++i) local += v[i];
+    uint32_t run;
+    const uint32_t total = block_excl_scan(local, run, wsum);
+    for (uint32_t i = r0; i < r1; ++i) {
+        const uint32_t x = v[i];
+        v[i] = run;
+        run += x;
+    }
+    __syncthreads();
     return total;
 }
 
@@ -526,11 +559,13 @@ constexpr uint32_t SEG_POS = 16;
 // them fill the 256 threads once (16 windows left 62 % of the threads idle).
 constexpr uint32_t KEYS_WINDOWS = 42;
 
+template <class K>
 __global__ __launch_bounds__(EXACT_THREADS) void part_keys_kernel(ExactArgs a) {
     __shared__ uint32_t wseg[KEYS_WINDOWS + 1];  // prefix sums of segments per window
     __shared__ uint32_t wsum[EXACT_THREADS / 64];
     __shared__ unsigned long long base_sh;
     __shared__ uint32_t n_had;
+    K* keys_out = (K*)a.keys;
     const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
     const uint32_t w0 = blockIdx.x * KEYS_WINDOWS;
     const uint32_t nw = min(KEYS_WINDOWS, a.n_windows - w0);
@@ -556,11 +591,11 @@ __global__ __launch_bounds__(EXACT_THREADS) void part_keys_kernel(ExactArgs a) {
     const uint32_t total = wseg[nw];
     const uint32_t k = a.k;
     const uint64_t kmask = (1ull << k) - 1ull;
-    const uint32_t keymask = k == 16u ? 0xffffffffu : ((1u << (2u * k)) - 1u);
+    const K keymask = 2u * k >= 8u * sizeof(K) ? (K)~(K)0 : (K)(((K)1 << (2u * k)) - 1u);
     uint32_t had = 0;
     for (uint32_t s0 = 0; s0 < total; s0 += EXACT_THREADS) {  // block-uniform rounds
         const uint32_t sg = s0 + t;
-        uint32_t key[SEG_POS];
+        K key[SEG_POS];
         uint32_t valid = 0, c = 0;
         if (sg < total) {
             uint32_t i = 0, r = nw;  // the window holding segment sg: the last i with wseg[i] <= sg
@@ -574,14 +609,14 @@ __global__ __launch_bounds__(EXACT_THREADS) void part_keys_kernel(ExactArgs a) {
             const uint32_t np = min(SEG_POS, npos - p0);
             const uint64_t b = wst + p0;
             // the first position: gathered; N flags of bases b .. b + k + np - 2 (<= 47 bits)
-            uint32_t cur = (uint32_t)to_dna2int(gather_bits(a.codes, b, 2u, 2u * k, a.n_bases >> 4), k);
+            K cur = (K)to_dna2int(gather_bits(a.codes, b, 2u, 2u * k, a.n_bases >> 4), k);
             const uint64_t nbits = gather_bits(a.nmask, b, 1u, k + np - 1u, a.n_bases >> 5);
             // codes of bases b + k .. b + k + np - 2 for the rolling steps (<= 15 bases: 30 bits)
             const uint64_t nxt = np > 1u ? gather_bits(a.codes, b + k, 2u, 2u * (np - 1u), a.n_bases >> 4) : 0ull;
 #pragma unroll
             for (uint32_t j = 0; j < SEG_POS; ++j) {
                 if (j < np) {
-                    if (j) cur = ((cur << 2) | (uint32_t)((nxt >> (2u * (j - 1u))) & 3u)) & keymask;
+                    if (j) cur = (K)(((K)(cur << 2) | (K)((nxt >> (2u * (j - 1u))) & 3u)) & keymask);
                     if ((nbits >> j) & kmask) {
                         ++had;  // count_kmers skips k-mers holding an N (approx_counter.cpp:498, 513-517)
                     } else {
@@ -614,7 +649,7 @@ __global__ __launch_bounds__(EXACT_THREADS) void part_keys_kernel(ExactArgs a) {
 #pragma unroll
         for (uint32_t j = 0; j < SEG_POS; ++j)
             if (valid & (1u << j)) {
-                if (dst < a.key_cap) a.keys[dst] = key[j];
+                if (dst < a.key_cap) keys_out[dst] = key[j];
                 ++dst;
             }
         __syncthreads();  // wsum / base_sh are reused by the next round
@@ -631,25 +666,26 @@ __global__ __launch_bounds__(EXACT_THREADS) void part_keys_kernel(ExactArgs a) {
 // (hist + scans + scatter 166 us at 10^5 windows; profiles/r02_exact_log.md).
 // Level 1 moves the keys into S = 2^s_log2 super-buckets (the top s_log2 bits),
 // level 2 splits each super-bucket into its SUB = NB / S buckets.  Both levels
-// work on chunks of EXACT_CHUNK keys, so a super-bucket swollen by one
-// adapter k-mer is still split over many workgroups.
+// work on chunks of keys, so a super-bucket swollen by one adapter k-mer is
+// still split over many workgroups.
 
-__device__ __forceinline__ uint32_t super_of(uint32_t key, uint32_t s_log2) {
+template <class K>
+__device__ __forceinline__ uint32_t super_of(K key, uint32_t s_log2) {
     return part_hash(key) >> (32u - s_log2);
 }
 
 // f(key) for the keys src[lo, hi), the workgroup's threads striding; PART_BATCH
 // loads per thread are issued before their keys are used.
 constexpr uint32_t PART_BATCH = 8;
-template <class F>
-__device__ __forceinline__ void for_keys(const uint32_t* src, uint64_t lo, uint64_t hi, F f) {
+template <class K, class F>
+__device__ __forceinline__ void for_keys(const K* src, uint64_t lo, uint64_t hi, F f) {
     const uint32_t t = threadIdx.x;
     for (uint64_t i0 = lo; i0 < hi; i0 += EXACT_THREADS * PART_BATCH) {
-        uint32_t v[PART_BATCH];
+        K v[PART_BATCH];
 #pragma unroll
         for (uint32_t r = 0; r < PART_BATCH; ++r) {
             const uint64_t i = i0 + r * EXACT_THREADS + t;
-            v[r] = i < hi ? src[i] : 0u;
+            v[r] = i < hi ? src[i] : (K)0;
         }
 #pragma unroll
         for (uint32_t r = 0; r < PART_BATCH; ++r)
@@ -663,14 +699,16 @@ __device__ __forceinline__ uint32_t part_n(const ExactArgs& a) {
 }
 
 // Level 1, per chunk: h1[chunk][s] = its keys in super-bucket s.
+template <class K>
 __global__ __launch_bounds__(EXACT_THREADS) void part_hist1_kernel(ExactArgs a) {
+    constexpr uint32_t CHUNK = PartKey<K>::CHUNK;
     __shared__ uint32_t h[EXACT_MAX_SUPER];
     const uint32_t S = 1u << a.s_log2, t = threadIdx.x;
     for (uint32_t i = t; i < S; i += EXACT_THREADS) h[i] = 0;
     __syncthreads();
     const uint32_t n = part_n(a);
-    const uint64_t lo = (uint64_t)blockIdx.x * EXACT_CHUNK, hi = min((uint64_t)n, lo + EXACT_CHUNK);
-    for_keys(a.keys, lo, hi, [&](uint32_t key) { atomicAdd(&h[super_of(key, a.s_log2)], 1u); });
+    const uint64_t lo = (uint64_t)blockIdx.x * CHUNK, hi = min((uint64_t)n, lo + CHUNK);
+    for_keys((const K*)a.keys, lo, hi, [&](K key) { atomicAdd(&h[super_of(key, a.s_log2)], 1u); });
     __syncthreads();
     for (uint32_t i = t; i < S; i += EXACT_THREADS) a.h1[(uint64_t)blockIdx.x * S + i] = h[i];
 }
@@ -697,17 +735,17 @@ __global__ __launch_bounds__(EXACT_THREADS) void part_scan1_kernel(ExactArgs a) 
 
 // Every workgroup of the later steps rebuilds, from stot, the super-buckets'
 // starts (sstart[0..S]) and the first level-2 chunk of each (cbeg[0..S]).
-__device__ __forceinline__ void super_layout(const ExactArgs& a, uint32_t* sstart, uint32_t* cbeg, uint32_t* wsum) {
+__device__ __forceinline__ void super_layout(const ExactArgs& a, uint32_t chunk, uint32_t* sstart, uint32_t* cbeg,
+                                             uint32_t* wsum) {
     const uint32_t S = 1u << a.s_log2, t = threadIdx.x;
-    const uint32_t v = t < S ? a.stot[t] : 0u;
-    const uint32_t c = (v + EXACT_CHUNK - 1u) / EXACT_CHUNK;
-    uint32_t ev, ec;
-    const uint32_t tv = block_excl_scan(v, ev, wsum);
-    const uint32_t tc = block_excl_scan(c, ec, wsum);
-    if (t < S) {
-        sstart[t] = ev;
-        cbeg[t] = ec;
+    for (uint32_t i = t; i < S; i += EXACT_THREADS) {
+        const uint32_t v = a.stot[i];
+        sstart[i] = v;
+        cbeg[i] = (v + chunk - 1u) / chunk;
     }
+    __syncthreads();
+    const uint32_t tv = block_scan_lds(sstart, S, wsum);
+    const uint32_t tc = block_scan_lds(cbeg, S, wsum);
     if (t == 0) {
         sstart[S] = tv;
         cbeg[S] = tc;
@@ -715,64 +753,65 @@ __device__ __forceinline__ void super_layout(const ExactArgs& a, uint32_t* sstar
     __syncthreads();
 }
 
-// Scatter of one chunk (n <= EXACT_CHUNK keys src[lo, lo + n)) into bins:
-// the keys are first grouped by bin in LDS (`stage`), then written out in that
-// order, so each bin's keys leave as one contiguous run at gcur[bin] (the
-// chunk's global start in that bin) instead of as isolated 4-byte stores.
-// `cnt` (nbins <= EXACT_THREADS, zeroed by the caller) and `stage` are LDS.
-constexpr uint32_t SCATTER_PER = EXACT_CHUNK / EXACT_THREADS;
-template <class Bin>
-__device__ __forceinline__ void staged_scatter(const uint32_t* __restrict__ src, uint64_t lo, uint32_t n,
-                                               uint32_t* __restrict__ dst, uint32_t nbins, uint32_t* cnt,
-                                               const uint32_t* gcur, uint32_t* stage, uint32_t* wsum, Bin bin) {
+// Scatter of one chunk (n <= CHUNK keys src[lo, lo + n)) into bins: the keys
+// are first grouped by bin in LDS (`stage`), then written out in that order, so
+// each bin's keys leave as one contiguous run at gcur[bin] (the chunk's global
+// start in that bin) instead of as isolated stores.  `cnt` (nbins entries,
+// zeroed by the caller) and `stage` are LDS.
+template <class K, class Bin>
+__device__ __forceinline__ void staged_scatter(const K* __restrict__ src, uint64_t lo, uint32_t n, K* __restrict__ dst,
+                                               uint32_t nbins, uint32_t* cnt, const uint32_t* gcur, K* stage,
+                                               uint32_t* wsum, Bin bin) {
+    constexpr uint32_t PER = PartKey<K>::CHUNK / EXACT_THREADS;
     const uint32_t t = threadIdx.x;
-    uint32_t key[SCATTER_PER], rank[SCATTER_PER];
+    K key[PER];
+    uint32_t rank[PER];
 #pragma unroll
-    for (uint32_t r = 0; r < SCATTER_PER; ++r) {
+    for (uint32_t r = 0; r < PER; ++r) {
         const uint32_t i = r * EXACT_THREADS + t;
-        key[r] = i < n ? src[lo + i] : 0u;
+        key[r] = i < n ? src[lo + i] : (K)0;
     }
 #pragma unroll
-    for (uint32_t r = 0; r < SCATTER_PER; ++r)
+    for (uint32_t r = 0; r < PER; ++r)
         if (r * EXACT_THREADS + t < n) rank[r] = atomicAdd(&cnt[bin(key[r])], 1u);
     __syncthreads();
-    uint32_t lstart;
-    block_excl_scan(t < nbins ? cnt[t] : 0u, lstart, wsum);
-    if (t < nbins) cnt[t] = lstart;
-    __syncthreads();
+    block_scan_lds(cnt, nbins, wsum);
 #pragma unroll
-    for (uint32_t r = 0; r < SCATTER_PER; ++r)
+    for (uint32_t r = 0; r < PER; ++r)
         if (r * EXACT_THREADS + t < n) stage[cnt[bin(key[r])] + rank[r]] = key[r];
     __syncthreads();
     for (uint32_t i = t; i < n; i += EXACT_THREADS) {
-        const uint32_t k = stage[i], b = bin(k);
+        const K k = stage[i];
+        const uint32_t b = bin(k);
         dst[gcur[b] + (i - cnt[b])] = k;
     }
 }
 
 // Level 1 scatter: each chunk's keys to its ranges of the super-buckets (LDS cursors).
+template <class K>
 __global__ __launch_bounds__(EXACT_THREADS) void part_scatter1_kernel(ExactArgs a) {
+    constexpr uint32_t CHUNK = PartKey<K>::CHUNK;
     __shared__ uint32_t sstart[EXACT_MAX_SUPER + 1], cbeg[EXACT_MAX_SUPER + 1], wsum[EXACT_THREADS / 64];
     __shared__ uint32_t cur[EXACT_MAX_SUPER], cnt[EXACT_MAX_SUPER];
-    __shared__ uint32_t stage[EXACT_CHUNK];
+    __shared__ K stage[CHUNK];
     const uint32_t S = 1u << a.s_log2, t = threadIdx.x;
-    super_layout(a, sstart, cbeg, wsum);
+    super_layout(a, CHUNK, sstart, cbeg, wsum);
     for (uint32_t i = t; i < S; i += EXACT_THREADS) {
         cur[i] = sstart[i] + a.h1[(uint64_t)blockIdx.x * S + i];
         cnt[i] = 0;
     }
     __syncthreads();
     const uint32_t n = part_n(a);
-    const uint64_t lo = (uint64_t)blockIdx.x * EXACT_CHUNK;
+    const uint64_t lo = (uint64_t)blockIdx.x * CHUNK;
     if (lo >= n) return;
     const uint32_t s_log2 = a.s_log2;
-    staged_scatter(a.keys, lo, (uint32_t)min((uint64_t)EXACT_CHUNK, n - lo), a.tmp, S, cnt, cur, stage, wsum,
-                   [=](uint32_t key) { return super_of(key, s_log2); });
+    staged_scatter((const K*)a.keys, lo, (uint32_t)min((uint64_t)CHUNK, n - lo), (K*)a.tmp, S, cnt, cur, stage, wsum,
+                   [=](K key) { return super_of(key, s_log2); });
 }
 
 // Level-2 chunk i: its super-bucket and key range [lo, hi) in tmp; false past the last chunk.
-__device__ __forceinline__ bool chunk2(const ExactArgs& a, const uint32_t* sstart, const uint32_t* cbeg, uint32_t i,
-                                       uint32_t& s, uint32_t& lo, uint32_t& hi) {
+__device__ __forceinline__ bool chunk2(const ExactArgs& a, uint32_t chunk, const uint32_t* sstart, const uint32_t* cbeg,
+                                       uint32_t i, uint32_t& s, uint32_t& lo, uint32_t& hi) {
     const uint32_t S = 1u << a.s_log2;
     if (i >= cbeg[S]) return false;
     uint32_t l = 0, r = S;  // the last s with cbeg[s] <= i (super-buckets without chunks share cbeg)
@@ -781,32 +820,35 @@ __device__ __forceinline__ bool chunk2(const ExactArgs& a, const uint32_t* sstar
         if (cbeg[m] <= i) l = m; else r = m;
     }
     s = l;
-    lo = sstart[s] + (i - cbeg[s]) * EXACT_CHUNK;
-    hi = min(sstart[s + 1], lo + EXACT_CHUNK);
+    lo = sstart[s] + (i - cbeg[s]) * chunk;
+    hi = min(sstart[s + 1], lo + chunk);
     return true;
 }
 
 // Level 2, per chunk of a super-bucket: h2[chunk][j] = its keys in sub-bucket j.
+template <class K>
 __global__ __launch_bounds__(EXACT_THREADS) void part_hist2_kernel(ExactArgs a) {
+    constexpr uint32_t CHUNK = PartKey<K>::CHUNK;
     __shared__ uint32_t sstart[EXACT_MAX_SUPER + 1], cbeg[EXACT_MAX_SUPER + 1], wsum[EXACT_THREADS / 64];
     __shared__ uint32_t h[EXACT_MAX_SUB];
     const uint32_t SUB = 1u << (a.nb_log2 - a.s_log2), t = threadIdx.x;
-    super_layout(a, sstart, cbeg, wsum);
+    super_layout(a, CHUNK, sstart, cbeg, wsum);
     uint32_t s, lo, hi;
-    if (!chunk2(a, sstart, cbeg, blockIdx.x, s, lo, hi)) return;
+    if (!chunk2(a, CHUNK, sstart, cbeg, blockIdx.x, s, lo, hi)) return;
     for (uint32_t j = t; j < SUB; j += EXACT_THREADS) h[j] = 0;
     __syncthreads();
-    for_keys(a.tmp, lo, hi, [&](uint32_t key) { wave_bin_add(h, bucket_of(key, a.nb_log2) & (SUB - 1u)); });
+    for_keys((const K*)a.tmp, lo, hi, [&](K key) { wave_bin_add(h, bucket_of(key, a.nb_log2) & (SUB - 1u)); });
     __syncthreads();
     for (uint32_t j = t; j < SUB; j += EXACT_THREADS) a.h2[(uint64_t)blockIdx.x * SUB + j] = h[j];
 }
 
 // Level 2, per super-bucket (one wave each, lane j = sub-bucket j): bucket
 // starts bstart[s * SUB + j] (and bstart[NB]), h2 -> each chunk's cursor.
+template <class K>
 __global__ __launch_bounds__(EXACT_THREADS) void part_scan2_kernel(ExactArgs a) {
     __shared__ uint32_t sstart[EXACT_MAX_SUPER + 1], cbeg[EXACT_MAX_SUPER + 1], wsum[EXACT_THREADS / 64];
     const uint32_t S = 1u << a.s_log2, SUB = 1u << (a.nb_log2 - a.s_log2);
-    super_layout(a, sstart, cbeg, wsum);
+    super_layout(a, PartKey<K>::CHUNK, sstart, cbeg, wsum);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t s = blockIdx.x * (EXACT_THREADS / 64) + (threadIdx.x >> 6);
     if (s >= S) return;
@@ -834,41 +876,50 @@ __global__ __launch_bounds__(EXACT_THREADS) void part_scan2_kernel(ExactArgs a) 
 }
 
 // Level 2 scatter: a chunk's keys to their buckets in `parts`.
+template <class K>
 __global__ __launch_bounds__(EXACT_THREADS) void part_scatter2_kernel(ExactArgs a) {
+    constexpr uint32_t CHUNK = PartKey<K>::CHUNK;
     __shared__ uint32_t sstart[EXACT_MAX_SUPER + 1], cbeg[EXACT_MAX_SUPER + 1], wsum[EXACT_THREADS / 64];
     __shared__ uint32_t cur[EXACT_MAX_SUB], cnt[EXACT_MAX_SUB];
-    __shared__ uint32_t stage[EXACT_CHUNK];
+    __shared__ K stage[CHUNK];
     const uint32_t SUB = 1u << (a.nb_log2 - a.s_log2), t = threadIdx.x;
-    super_layout(a, sstart, cbeg, wsum);
+    super_layout(a, CHUNK, sstart, cbeg, wsum);
     uint32_t s, lo, hi;
-    if (!chunk2(a, sstart, cbeg, blockIdx.x, s, lo, hi)) return;
+    if (!chunk2(a, CHUNK, sstart, cbeg, blockIdx.x, s, lo, hi)) return;
     for (uint32_t j = t; j < SUB; j += EXACT_THREADS) {
         cur[j] = a.h2[(uint64_t)blockIdx.x * SUB + j];
         cnt[j] = 0;
     }
     __syncthreads();
     const uint32_t nb_log2 = a.nb_log2;
-    staged_scatter(a.tmp, lo, hi - lo, a.parts, SUB, cnt, cur, stage, wsum,
-                   [=](uint32_t key) { return bucket_of(key, nb_log2) & (SUB - 1u); });
+    staged_scatter((const K*)a.tmp, lo, hi - lo, (K*)a.parts, SUB, cnt, cur, stage, wsum,
+                   [=](K key) { return bucket_of(key, nb_log2) & (SUB - 1u); });
 }
 
+// DUST score of a key (getComplexity, approx_counter.cpp:247-267): the packed
+// 4-bit-bin form for 32-bit keys (k <= 16), the general one above.
+__device__ __forceinline__ float key_complexity(uint32_t key, uint32_t k) { return complexity16(key, k); }
+__device__ __forceinline__ float key_complexity(uint64_t key, uint32_t k) { return complexity(key, k); }
+
 // One workgroup per bucket: count its keys in LDS, then filter, histogram and
-// list them like exact_scan_kernel (the all-T 16-mer, whose key + 1 wraps to
-// 0, is tallied in special[0] and handled by part_special_kernel).  LDS is
-// kept under 80 KB (two workgroups per CU): the table, a 32-bin histogram of
-// the counts 1..32 written out per bucket (phist, summed by
-// part_hist_reduce_kernel: thousands of buckets adding into the same few
-// global bins would serialise), larger counts straight to the global
-// histogram, and a small appender.  An adapter k-mer fills most of its
-// bucket with one key: a wave first merges the lanes holding its first lane's
-// key, so the LDS add on that slot is one per wave instead of one per lane.
+// list them like exact_scan_kernel (the all-T k-mer whose key + 1 wraps to 0 --
+// the 16-mer of 32-bit keys, the 32-mer of 64-bit keys -- is tallied in
+// special[0] and handled by part_special_kernel).  LDS is kept at ~46 KB
+// (32-bit keys: three workgroups per CU) / ~62 KB (64-bit keys: two): the
+// table, a 32-bin histogram of the counts 1..32 written out per bucket (phist,
+// summed by part_hist_reduce_kernel: thousands of buckets adding into the same
+// few global bins would serialise), larger counts straight to the global
+// histogram, and a small appender.  An adapter k-mer fills most of its bucket
+// with one key: a wave first merges the lanes holding its first lane's key, so
+// the LDS add on that slot is one per wave instead of one per lane.
 constexpr uint32_t COUNT_APPEND = 512;
 
 constexpr uint32_t COUNT_BATCH = 8;  // keys per thread loaded together (one memory latency per batch)
 
+template <class K>
 __global__ __launch_bounds__(EXACT_THREADS) void part_count_kernel(ExactArgs a) {
     constexpr uint32_t SLOTS = EXACT_BUCKET_SLOTS;
-    __shared__ uint32_t tk[SLOTS];  // key + 1; 0 = empty
+    __shared__ K tk[SLOTS];  // key + 1; 0 = empty
     __shared__ uint32_t tc[SLOTS];
     __shared__ uint16_t occ[SLOTS];  // the slots claimed, in claim order: only they are scored and cleared
     __shared__ uint32_t n_occ;
@@ -878,6 +929,7 @@ __global__ __launch_bounds__(EXACT_THREADS) void part_count_kernel(ExactArgs a) 
     __shared__ uint32_t app_n;
     __shared__ unsigned long long app_b;
     __shared__ uint32_t n_allt;
+    const K* parts = (const K*)a.parts;
     const uint32_t t = threadIdx.x;
     const uint32_t NB = 1u << a.nb_log2;
     for (uint32_t i = t; i < SLOTS; i += EXACT_THREADS) {
@@ -894,12 +946,12 @@ __global__ __launch_bounds__(EXACT_THREADS) void part_count_kernel(ExactArgs a) 
     // only the claimed slots are cleared.  The first batch of keys of the next
     // bucket is requested before this bucket is scored, so its load latency
     // hides behind the scoring.
-    uint32_t nxt[COUNT_BATCH];
-    auto load_batch = [&](uint32_t* dst, uint32_t i0, uint32_t hi) __attribute__((always_inline)) {
+    K nxt[COUNT_BATCH];
+    auto load_batch = [&](K* dst, uint32_t i0, uint32_t hi) __attribute__((always_inline)) {
 #pragma unroll
         for (uint32_t r = 0; r < COUNT_BATCH; ++r) {
             const uint32_t i = i0 + r * EXACT_THREADS + t;
-            dst[r] = i < hi ? a.parts[i] : 0u;
+            dst[r] = i < hi ? parts[i] : (K)0;
         }
     };
     if (blockIdx.x < NB) load_batch(nxt, a.bstart[blockIdx.x], a.bstart[blockIdx.x + 1]);
@@ -909,7 +961,7 @@ __global__ __launch_bounds__(EXACT_THREADS) void part_count_kernel(ExactArgs a) 
         const uint32_t lo = a.bstart[b], hi = a.bstart[b + 1];
         uint32_t allt = 0;
         for (uint32_t i0 = lo; i0 < hi; i0 += EXACT_THREADS * COUNT_BATCH) {  // block-uniform batches
-            uint32_t kb[COUNT_BATCH];
+            K kb[COUNT_BATCH];
             if (i0 == lo) {
 #pragma unroll
                 for (uint32_t r = 0; r < COUNT_BATCH; ++r) kb[r] = nxt[r];
@@ -920,9 +972,12 @@ __global__ __launch_bounds__(EXACT_THREADS) void part_count_kernel(ExactArgs a) 
             for (uint32_t r = 0; r < COUNT_BATCH; ++r) {
                 const uint32_t i = i0 + r * EXACT_THREADS + t;
                 const bool have = i < hi;
-                const uint32_t key = kb[r], stored = key + 1u;
+                const K key = kb[r], stored = (K)(key + 1u);
                 // lanes holding the wave's first key: one add of their number
-                const uint32_t k0 = __builtin_amdgcn_readfirstlane(key);
+                const uint32_t lo32 = __builtin_amdgcn_readfirstlane((uint32_t)key);
+                K k0 = (K)lo32;
+                if constexpr (sizeof(K) == 8)
+                    k0 |= (K)__builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)key >> 32)) << 32;
                 const uint64_t same = __ballot(have && key == k0);
                 uint32_t add = 1u;
                 bool go = have;
@@ -938,9 +993,9 @@ __global__ __launch_bounds__(EXACT_THREADS) void part_count_kernel(ExactArgs a) 
                     uint32_t h = part_hash(key) & (SLOTS - 1u);
                     uint32_t probe = 0;
                     for (; probe < COUNT_PROBES; ++probe) {
-                        uint32_t cur = tk[h];
+                        K cur = tk[h];
                         if (cur == 0u) {
-                            cur = atomicCAS(&tk[h], 0u, stored);
+                            cur = atomicCAS(&tk[h], (K)0, stored);
                             if (cur == 0u) {  // claimed: list the slot for scoring and clearing
                                 cur = stored;
                                 occ[atomicAdd(&n_occ, 1u)] = (uint16_t)h;
@@ -966,12 +1021,13 @@ __global__ __launch_bounds__(EXACT_THREADS) void part_count_kernel(ExactArgs a) 
             uint64_t key = 0;
             if (s0 + t < m) {
                 const uint32_t s = occ[s0 + t];
-                key = tk[s] - 1u;
+                const K kk = (K)(tk[s] - 1u);
+                key = (uint64_t)kk;
                 c = tc[s];
                 tk[s] = 0;  // cleared for the next bucket
                 tc[s] = 0;
-                if (complexity16((uint32_t)key, a.k) >= a.lc_threshold) c = 0;  // haveLowComplexity (214-234)
-                else if (is_forbidden(a, key)) c = 0;              // isForbiddenKmer (330-332)
+                if (key_complexity(kk, a.k) >= a.lc_threshold) c = 0;  // haveLowComplexity (214-234)
+                else if (is_forbidden(a, key)) c = 0;                  // isForbiddenKmer (330-332)
             }
             if (!a.emit_only && c) {
                 if (c == 1u) ++ones;
@@ -1012,11 +1068,11 @@ __global__ __launch_bounds__(EXACT_THREADS) void part_hist_reduce_kernel(ExactAr
     }
 }
 
-// The all-T 16-mer (counted apart in special[0]): filters, histogram, list.
-__global__ void part_special_kernel(ExactArgs a) {
+// The all-T k-mer whose key + 1 wraps (counted apart in special[0]): filters,
+// histogram, list.  key = all ones of the key width.
+__global__ void part_special_kernel(ExactArgs a, uint64_t key) {
     const uint32_t c = a.special[0];
     if (!c) return;
-    const uint64_t key = 0xffffffffull;
     if (complexity(key, a.k) >= a.lc_threshold || is_forbidden(a, key)) return;
     if (!a.emit_only) atomicAdd(&a.hist[min(c, (uint32_t)EXACT_HIST_BINS - 1u)], 1u);
     if (c >= a.list_min) {
@@ -1028,36 +1084,50 @@ __global__ void part_special_kernel(ExactArgs a) {
     }
 }
 
-}  // namespace
-
-hipError_t launch_exact_part_count(const ExactArgs& a, hipStream_t stream) {
-    // persistent workgroups: three per CU (LDS ~46 KB each)
-    const uint32_t grid = std::min<uint32_t>(1u << a.nb_log2, 256u * 3u);
-    hipLaunchKernelGGL(part_count_kernel, dim3(grid), dim3(EXACT_THREADS), 0, stream, a);
+template <class K>
+hipError_t part_count(const ExactArgs& a, hipStream_t stream) {
+    // persistent workgroups: three per CU for 32-bit keys (LDS ~46 KB each), two for 64-bit (~62 KB)
+    const uint32_t per_cu = sizeof(K) == 4 ? 3u : 2u;
+    const uint32_t grid = std::min<uint32_t>(1u << a.nb_log2, 256u * per_cu);
+    hipLaunchKernelGGL(part_count_kernel<K>, dim3(grid), dim3(EXACT_THREADS), 0, stream, a);
     if (!a.emit_only)
         hipLaunchKernelGGL(part_hist_reduce_kernel, dim3(EXACT_PHIST), dim3(EXACT_THREADS), 0, stream, a);
-    hipLaunchKernelGGL(part_special_kernel, dim3(1), dim3(1), 0, stream, a);
+    hipLaunchKernelGGL(part_special_kernel, dim3(1), dim3(1), 0, stream, a, (uint64_t)(K)~(K)0);
     return hipGetLastError();
 }
 
-hipError_t launch_exact_partitioned(const ExactArgs& a, hipStream_t stream) {
+template <class K>
+hipError_t partitioned(const ExactArgs& a, hipStream_t stream) {
+    constexpr uint32_t CHUNK = PartKey<K>::CHUNK;
     if (a.nb_log2 < 6 || a.nb_log2 > MAX_NB_LOG2) return hipErrorInvalidValue;
     const uint32_t NB = 1u << a.nb_log2;
-    const uint32_t wblocks = (a.n_windows + KEYS_WINDOWS - 1) / KEYS_WINDOWS;
-    if (wblocks) hipLaunchKernelGGL(part_keys_kernel, dim3(wblocks), dim3(EXACT_THREADS), 0, stream, a);
     const uint32_t S = 1u << a.s_log2;
     if (a.s_log2 > a.nb_log2 || S > EXACT_MAX_SUPER || (NB >> a.s_log2) > EXACT_MAX_SUB || !a.n_chunks ||
-        a.n_chunks2 < a.n_chunks + S)
+        (uint64_t)a.n_chunks * CHUNK < a.key_cap || a.n_chunks2 < a.n_chunks + S)
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL(part_hist1_kernel, dim3(a.n_chunks), dim3(EXACT_THREADS), 0, stream, a);
+    const uint32_t wblocks = (a.n_windows + KEYS_WINDOWS - 1) / KEYS_WINDOWS;
+    if (wblocks) hipLaunchKernelGGL(part_keys_kernel<K>, dim3(wblocks), dim3(EXACT_THREADS), 0, stream, a);
+    hipLaunchKernelGGL(part_hist1_kernel<K>, dim3(a.n_chunks), dim3(EXACT_THREADS), 0, stream, a);
     hipLaunchKernelGGL(part_scan1_kernel, dim3(S), dim3(EXACT_THREADS), 0, stream, a);
-    hipLaunchKernelGGL(part_scatter1_kernel, dim3(a.n_chunks), dim3(EXACT_THREADS), 0, stream, a);
-    hipLaunchKernelGGL(part_hist2_kernel, dim3(a.n_chunks2), dim3(EXACT_THREADS), 0, stream, a);
-    hipLaunchKernelGGL(part_scan2_kernel, dim3((S + EXACT_THREADS / 64 - 1) / (EXACT_THREADS / 64)), dim3(EXACT_THREADS),
-                       0, stream, a);
-    hipLaunchKernelGGL(part_scatter2_kernel, dim3(a.n_chunks2), dim3(EXACT_THREADS), 0, stream, a);
+    hipLaunchKernelGGL(part_scatter1_kernel<K>, dim3(a.n_chunks), dim3(EXACT_THREADS), 0, stream, a);
+    hipLaunchKernelGGL(part_hist2_kernel<K>, dim3(a.n_chunks2), dim3(EXACT_THREADS), 0, stream, a);
+    hipLaunchKernelGGL(part_scan2_kernel<K>, dim3((S + EXACT_THREADS / 64 - 1) / (EXACT_THREADS / 64)),
+                       dim3(EXACT_THREADS), 0, stream, a);
+    hipLaunchKernelGGL(part_scatter2_kernel<K>, dim3(a.n_chunks2), dim3(EXACT_THREADS), 0, stream, a);
     if (hipError_t e = hipGetLastError()) return e;
-    return launch_exact_part_count(a, stream);
+    return part_count<K>(a, stream);
+}
+
+}  // namespace
+
+uint32_t exact_part_chunk(uint32_t k) { return k <= EXACT_COMPACT_MAX_K ? PartKey<uint32_t>::CHUNK : PartKey<uint64_t>::CHUNK; }
+
+hipError_t launch_exact_part_count(const ExactArgs& a, hipStream_t stream) {
+    return a.k <= EXACT_COMPACT_MAX_K ? part_count<uint32_t>(a, stream) : part_count<uint64_t>(a, stream);
+}
+
+hipError_t launch_exact_partitioned(const ExactArgs& a, hipStream_t stream) {
+    return a.k <= EXACT_COMPACT_MAX_K ? partitioned<uint32_t>(a, stream) : partitioned<uint64_t>(a, stream);
 }
 
 hipError_t launch_exact_insert(const ExactArgs& a, hipStream_t stream) {

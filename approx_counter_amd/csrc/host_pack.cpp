@@ -387,8 +387,7 @@ bool have_avx2() {
 }
 
 bool have_avx512() {
-    static const bool v = __builtin_cpu_supports("avx512bw") && __builtin_cpu_supports("avx512vl") &&
-                          std::getenv("AC_NO_AVX512") == nullptr;
+    static const bool v = __builtin_cpu_supports("avx512bw") && __builtin_cpu_supports("avx512vl");
     return v;
 }
 

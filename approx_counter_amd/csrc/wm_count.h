@@ -40,12 +40,14 @@
 #define AC_STAGE_REPL 32      // replicas of a segment's done counter (pollers spread over lines)
 // Device words of a staged launch, one AC_QUEUE_LINE line each, after the
 // launch's sub-queue counters in its queue bank (zeroed with them for the next
-// launch on that bank): groups done, error bits, then per segment: chunk
-// claims, the segment's header copy (verdict, bytes, seen), AC_STAGE_REPL done replicas.
+// launch on that bank; only word 0 of a line is ever used, as the next launch
+// zeroes word 0 of each): groups done, error bits, then per segment: chunk
+// claims, the segment's header copy (verdict, bytes, seen: a line each),
+// AC_STAGE_REPL done replicas.
 #define AC_STAGE_L_GROUPS 0
 #define AC_STAGE_L_ERR 1
-#define AC_STAGE_L_SEG(s) (2 + (s) * (2 + AC_STAGE_REPL))
-#define AC_STAGE_LINES (2 + AC_MAX_SEGS * (2 + AC_STAGE_REPL))
+#define AC_STAGE_L_SEG(s) (2 + (s) * (4 + AC_STAGE_REPL))
+#define AC_STAGE_LINES (2 + AC_MAX_SEGS * (4 + AC_STAGE_REPL))
 #define AC_STAGE_TIMEOUT_TICKS 50000000ull  // 0.5 s of s_memrealtime (100 MHz): every wait is bounded
 
 namespace acamd {

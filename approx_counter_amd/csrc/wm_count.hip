@@ -265,9 +265,12 @@ __device__ __attribute__((noinline)) uint32_t stage_wait(const uint8_t* src, uin
                                                          uint32_t* hdr, uint32_t* words, uint32_t gen, uint32_t* err,
                                                          uint32_t replica, uint32_t si) {
     const uint32_t lane = threadIdx.x & 63u;
+    // (one word per line: a launch zeroes only word 0 of each line of the next launch's bank)
     uint32_t* claim = words;
-    uint32_t* info = words + AC_QUEUE_LINE;  // [0] verdict, [1] bytes, [2] header seen
-    uint32_t* done = words + 2 * AC_QUEUE_LINE;
+    uint32_t* verdict_w = words + AC_QUEUE_LINE;
+    uint32_t* bytes_w = words + 2 * AC_QUEUE_LINE;
+    uint32_t* seen_w = words + 3 * AC_QUEUE_LINE;
+    uint32_t* done = words + 4 * AC_QUEUE_LINE;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     auto late = [&]() { return __builtin_amdgcn_s_memrealtime() - t0 > AC_STAGE_TIMEOUT_TICKS; };
     auto load = [&](uint32_t* p, int scope) {
@@ -301,13 +304,13 @@ __device__ __attribute__((noinline)) uint32_t stage_wait(const uint8_t* src, uin
                 verdict = load(hdr + AC_HDR_ABORT, 1) ? ~0u : (load(hdr + AC_HDR_HAS_N, 1) ? 1u : 0u);
                 if (bytes > chunks * AC_STAGE_CHUNK) verdict = ~0u;  // a header the launch cannot hold: skip
                 if (lane == 0) {
-                    __hip_atomic_store(info, verdict, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(info + 1, bytes, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(verdict_w, verdict, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(bytes_w, bytes, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                if (lane == 0) __hip_atomic_store(info + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (lane == 0) __hip_atomic_store(seen_w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             } else {  // the other chunk winners wait for the poller's device flag
-                while (load(info + 2, 0) == 0u) {
+                while (load(seen_w, 0) == 0u) {
                     if (late()) {
                         ok = false;
                         break;
@@ -315,8 +318,8 @@ __device__ __attribute__((noinline)) uint32_t stage_wait(const uint8_t* src, uin
                     __builtin_amdgcn_s_sleep(4);
                 }
                 if (!ok) break;
-                verdict = load(info, 0);
-                bytes = load(info + 1, 0);
+                verdict = load(verdict_w, 0);
+                bytes = load(bytes_w, 0);
             }
             // range-checked descriptors: bytes past the region read as 0 and are not stored
             rs = __builtin_amdgcn_make_buffer_rsrc((void*)src, 0, (int)bytes, 0x00020000);
@@ -334,8 +337,10 @@ __device__ __attribute__((noinline)) uint32_t stage_wait(const uint8_t* src, uin
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (c == 0) stage_stamp(si, 1);
+        uint32_t prev = 0;
         if (lane < AC_STAGE_REPL)
-            __hip_atomic_fetch_add(done + lane * AC_QUEUE_LINE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            prev = __hip_atomic_fetch_add(done + lane * AC_QUEUE_LINE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__builtin_amdgcn_readfirstlane(prev) + 1u == chunks) stage_stamp(si, 2);  // (diagnostic builds) last chunk in
     }
     while (ok && load(done + replica * AC_QUEUE_LINE, 0) < chunks) {
         if (late()) {
@@ -352,7 +357,7 @@ __device__ __attribute__((noinline)) uint32_t stage_wait(const uint8_t* src, uin
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
-    return load(info, 0);
+    return load(verdict_w, 0);
 }
 
 // The remainder (< 16 bases) of a segment: blocks of 8, 4, 2, 1 bases.

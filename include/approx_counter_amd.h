@@ -170,6 +170,13 @@ ac_status ac_exact_count_device(ac_ctx* ctx, uint32_t k, const ac_windows* dev, 
                                 uint64_t* kmers_out, uint64_t* counts_out, uint64_t capacity, uint64_t* n_out,
                                 uint64_t* n_distinct, uint64_t* had_n);
 
+/* Which counting path the last exact count of ctx took (for measurement and
+ * tests): 1 = partitioned (dense keys, bucket partition, per-bucket LDS count;
+ * every k, samples up to 2^27 k-mer positions), 0 = the global hash table
+ * (larger samples, a bucket that outgrew its LDS table, or AC_EXACT_HASH=1),
+ * -1 = none yet. */
+int ac_exact_path(const ac_ctx* ctx);
+
 /* Same with a host sample (uploads it with ac_sample_upload first). */
 ac_status ac_exact_count(ac_ctx* ctx, uint32_t k, const ac_windows* host, float lc_threshold,
                          const uint64_t* forbidden, uint32_t n_forbidden, uint64_t limit, uint64_t solid,
@@ -234,7 +241,9 @@ ac_status ac_pack_windows(const uint8_t* dna5, const uint64_t* seq_start, const 
  * (approx_counter.cpp:38, filled by sampleSequences 415-476), one byte per
  * base.  Window i is bases[offset[i] .. offset[i] + length[i]); bases are
  * Dna5 ordinals (0..3 = A C G T, anything else = N; SeqAn's ordValue).
- * Windows may overlap or come in any order.
+ * Windows may overlap or come in any order.  Precondition (the struct carries
+ * no size for `bases`, so the library cannot check it): every
+ * offset[i] + length[i] lies within the caller's `bases` buffer.
  */
 typedef struct ac_dna5_windows {
     const uint8_t* bases;

@@ -115,3 +115,19 @@ def test_pack_matches_reference_packing_random():
         pos += (w.size + 31) // 32 * 32
     assert np.array_equal(s.nmask, exp_nmask)
     assert np.array_equal(s.codes, exp_codes)
+
+
+def test_dna5_sample_rejects_windows_past_the_buffer():
+    """ac_dna5_windows has no size for `bases`: the Python side checks that no
+    window reaches past the buffer before the packer could read beyond it."""
+    import numpy as np
+    import pytest
+
+    import approx_counter_amd as ac
+
+    ok = ac.Dna5Sample(np.zeros(10, np.uint8), np.array([0, 5], np.uint64), np.array([5, 5], np.uint32))
+    assert ok.n_windows == 2
+    with pytest.raises(ValueError):
+        ac.Dna5Sample(np.zeros(10, np.uint8), np.array([0, 6], np.uint64), np.array([5, 5], np.uint32))
+    with pytest.raises(ValueError):
+        ac.Dna5Sample(np.zeros(10, np.uint8), np.array([0], np.uint64), np.array([5, 5], np.uint32))

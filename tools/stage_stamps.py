@@ -54,8 +54,11 @@ def main():
         for s in np.unique(seg):
             m = seg == s
             print(f" seg {s}: flag seen {(stage[4 * s] - t0) / 100:7.1f}, poller's copy done "
-                  f"{(stage[4 * s + 1] - t0) / 100:7.1f}")
+                  f"{(stage[4 * s + 1] - t0) / 100:7.1f}, last chunk in {(stage[4 * s + 2] - t0) / 100:7.1f}")
             print("   entry           ", pct(us[m, 0]))
+            wait_end = (raw[:, 7] - t0) / 100.0
+            w0 = m & (np.arange(n) % 4 == 0)
+            print("   staging waited  ", pct(wait_end[w0]), "(wave 0 of each workgroup)")
             print("   counting starts ", pct(us[m, 1]))
             print("   counting ends   ", pct(us[m, 2]))
             print("   exit            ", pct(us[m, 3]))
