@@ -109,10 +109,7 @@ struct ac_ctx {
     uint32_t early_flip = 0;         // early-launch calls alternate between staging slots 0 and 1
     int exact_path = -1;             // the last exact count's path: 1 partitioned, 0 hash table
     // zero-copy vs DMA choice of the host-buffer stage (ac_stage_mode)
-    int zc_choice = -1;
-    int zc_last = -1;  // 0: the last synchronous call was too large for zero-copy, 2: it was an early launch (ac_stage_mode)
-    uint32_t zc_probe = 0, zc_calls = 0;
-    std::vector<double> zc_us[2];
+    int last_mode = -1;  // ac_stage_mode: 2 the last jobs call was an early launch, 0 the DMA path
 };
 
 namespace {
@@ -261,6 +258,7 @@ struct StageLaunch {
     const uint8_t* src[AC_MAX_SEGS] = {};
     uint8_t* dst[AC_MAX_SEGS] = {};
     uint32_t chunks[AC_MAX_SEGS] = {};
+    uint32_t* err_out = nullptr;  // device word the launch's error bits are also or-ed into (submits: ac_check)
 };
 
 ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hipStream_t stream,
@@ -421,6 +419,7 @@ ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hi
         a.stage = sc.queue + ((uint64_t)sc.bank * sc.qcap + n_counters) * AC_QUEUE_LINE;
         a.err = a.stage + AC_STAGE_L_ERR * AC_QUEUE_LINE;
         a.total_groups = groups_total;
+        a.err_out = stage->err_out;
     }
     // Live segments' queue_begin values are increasing; the kernel picks the
     // last live segment whose queue_begin <= its sub-queue.
@@ -1318,8 +1317,7 @@ struct JobPlan {
     uint32_t gen = 0;    // its generation (the header flags and completion word carry it)
     int slot = 0;     // staging slot (set by the caller: a synchronous part q uses slot q, a submit part its set's)
     int scratch = 0;  // count-kernel scratch set (ac_ctx::sc)
-    bool zc = true;  // this call's transfer mode (zero-copy or DMA)
-    bool zc_eligible = true;  // false: the image is too large for zero-copy (DMA, not measured)
+
 };
 
 // Calls whose pack and DMA take hundreds of
@@ -1333,59 +1331,6 @@ struct JobPlan {
 constexpr uint64_t STAGE_PARTS2_MIN_WINDOWS = 1ull << 17, STAGE_PARTS4_MIN_WINDOWS = 1ull << 19;
 int stage_parts(uint64_t total_w) {
     return total_w >= STAGE_PARTS4_MIN_WINDOWS ? 4 : total_w >= STAGE_PARTS2_MIN_WINDOWS ? 2 : 1;
-}
-// Zero-copy stage (default; AC_STAGE_ZEROCOPY=0 = DMA in and out): the count
-// kernel reads the packed inputs straight from the pinned host block and
-// writes the counts back into it.  Each window is fetched one window ahead of
-// its use (~8 us of slack at 8 waves/SIMD), which hides the PCIe latency, and
-// the contiguous item ranges of the work queues make each XCD read a slice of
-// the sample; it saves the DMA (1.2 MB, ~27 us at cfg2), the ~9 us
-// DMA-to-kernel dependency and the D2H blit.
-int stage_zerocopy_env() {  // 1 / 0 forced by AC_STAGE_ZEROCOPY, -1 = automatic
-    static const int v = [] {
-        const char* e = std::getenv("AC_STAGE_ZEROCOPY");
-        return e ? (std::atoi(e) != 0 ? 1 : 0) : -1;
-    }();
-    return v;
-}
-// Zero-copy won on one box (the kernel took the same time as on device-resident
-// input) and lost badly on another (kernel + completion 217 vs 107 us, host
-// under other tenants' load), and on one box it turned slow in
-// the middle of a run (cfg3: 9.9 ms per step after fast probes), so a context
-// keeps measuring: its synchronous calls alternate zero-copy / DMA until
-// ZC_PROBES timed calls of each (after one untimed, cold call of each), it then
-// uses the faster by median of each path's last ZC_PROBES calls, and every
-// ZC_REPROBE-th call takes the other path to refresh that path's figures.
-// Submits use zero-copy until a choice exists.  Calls whose zero-copy would
-// move too much over PCIe take the DMA path and are not measured (below).
-constexpr uint32_t ZC_PROBES = 4;
-constexpr uint32_t ZC_REPROBE = 64;
-// Zero-copy reads the image once per candidate group wherever an XCD's L2 does
-// not keep it (on the slow boxes nothing is kept: ~55 GB/s of PCIe reads).  Up
-// to ZC_MAX_PCIE_BYTES of image x groups the measurements above decide (cfg2 6
-// MB, cfg5 100 MB, cfg3 150 MB: zero-copy 3.26-3.39 vs DMA 3.47-3.59 ms per cfg3
-// step on a fast box, profiles/r02_stage_auto_cfg3.log); beyond it (cfg4: 390
-// MB; zero-copy 15.8-18 vs DMA 13.7 ms per step) the call takes the DMA.
-constexpr uint64_t ZC_MAX_PCIE_BYTES = 256ull << 20;
-bool stage_zerocopy(ac_ctx* ctx, bool sync) {
-    if (stage_zerocopy_env() >= 0) return stage_zerocopy_env() == 1;
-    if (ctx->zc_choice < 0) return !sync || ctx->zc_probe % 2 == 0;
-    if (sync && ++ctx->zc_calls % ZC_REPROBE == 0) return ctx->zc_choice != 1;  // refresh the other path
-    return ctx->zc_choice == 1;
-}
-void stage_zerocopy_record(ac_ctx* ctx, bool zc, double us) {
-    if (stage_zerocopy_env() >= 0) return;
-    if (ctx->zc_choice < 0 && ctx->zc_probe++ < 2) return;  // the cold call of each path
-    std::vector<double>& v = ctx->zc_us[zc ? 1 : 0];
-    v.push_back(us);
-    if (v.size() > ZC_PROBES) v.erase(v.begin());
-    if (ctx->zc_us[0].size() >= ZC_PROBES && ctx->zc_us[1].size() >= ZC_PROBES) {
-        auto median = [](std::vector<double> x) {
-            std::sort(x.begin(), x.end());
-            return x[x.size() / 2];
-        };
-        ctx->zc_choice = median(ctx->zc_us[1]) <= median(ctx->zc_us[0]) ? 1 : 0;
-    }
 }
 // DMA-mode transfer of a one-part call: a copy kernel on the compute queue reads the pinned
 // block once over PCIe and writes the device block, so the count kernel follows it on the
@@ -1427,13 +1372,15 @@ hipError_t stage_blit_launch(const void* src_dev, void* dst, size_t bytes, hipSt
     return hipGetLastError();
 }
 
-// The early-launch stage for one-part synchronous calls (default; AC_STAGE_EARLY=0 = the
-// pack -> transfer -> launch order of round 2, 2 = the first job sent ahead of the launch by
-// the copy kernel, the others staged by the count kernel).
+// The early-launch stage for calls counted in one part on one device, synchronous calls and
+// submits alike (default: AC_STAGE_EARLY=1).  0 = the pack -> copy kernel -> launch order of
+// round 2; 2 = the first job sent ahead of the launch by the copy kernel, the others staged by
+// the count kernel.  Same box, interleaved (profiles/r03_m2/summary.log): cfg2 step 0.141-0.143
+// vs 0.148-0.149 ms.
 int stage_early() {
     static const int v = [] {
         const char* e = std::getenv("AC_STAGE_EARLY");
-        return e ? std::max(0, std::min(2, std::atoi(e))) : 0;
+        return e ? std::max(0, std::min(2, std::atoi(e))) : 1;
     }();
     return v;
 }
@@ -1566,14 +1513,6 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
         off = align256(off + sizeof(uint32_t) * jobs[j].n_kmers);
     }
     p.total = off;
-    // Zero-copy's worst case moves the image over PCIe once per candidate group (ZC_MAX_PCIE_BYTES).
-    uint64_t pcie_bytes = 0;
-    const uint32_t cpw = acamd::cands_per_wave(acamd::pack_factor(k));
-    for (uint32_t j = 0; j < p.n; ++j)
-        pcie_bytes += p.n_bases[j] / 8 * 3 * ((jobs[j].n_kmers + cpw - 1) / cpw);  // 2-bit codes + N bitmap
-    p.zc_eligible = p.zc_eligible && pcie_bytes <= ZC_MAX_PCIE_BYTES;  // (a multi-part call is DMA-only)
-    if (!p.zc_eligible && stage_zerocopy_env() < 0) p.zc = false;
-    if (p.early) p.zc = false;
     // The slot: wait until the launch that last read it has finished, grow it.
     ac_ctx::Slot& sl = ctx->slot[p.slot];
     if (sl.pending) {
@@ -1581,7 +1520,6 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
         sl.pending = false;
     }
     if (!sl.ev) AC_HIP(ctx, hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming));
-    const bool zc = p.zc;
     if (sl.h_cap < p.total) {
         if (sl.h) (void)hipHostFree(sl.h);
         sl.h = nullptr;
@@ -1592,8 +1530,7 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
         sl.h_cap = cap;
         AC_HIP(ctx, hipHostGetDevicePointer(&sl.hd, sl.h, 0));
     }
-    if (!zc)
-        if (ac_status st = grow(ctx, &sl.d, &sl.d_cap, p.total)) return st;
+    if (ac_status st = grow(ctx, &sl.d, &sl.d_cap, p.total)) return st;
     char* h = (char*)sl.h;
     for (uint32_t j = 0; j < p.n; ++j) {
         if (jobs[j].n_kmers) std::memcpy(h + p.off_kmers[j], jobs[j].kmers, sizeof(uint64_t) * jobs[j].n_kmers);
@@ -1645,9 +1582,9 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
             }
         ulen[j] = (any && equal) ? l0 : AC_NO_ULEN;
     }
-    char* d = zc ? (char*)sl.hd : (char*)sl.d;
-    // In both modes the kernel writes the error word and the counts straight into the pinned
-    // block (hd), so no copy comes back (profiles/r02_stage_dma_back_ab.log).
+    char* d = (char*)sl.d;
+    // The kernel writes the error word and the counts straight into the pinned block (hd), so
+    // no copy comes back (profiles/r02_stage_dma_back_ab.log).
     char* hd = (char*)sl.hd;
     auto make_segs = [&](ac_segment* segs) {
         uint64_t cbase = 0;
@@ -1677,6 +1614,7 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
         if (++ctx->gen == 0) ++ctx->gen;
         p.gen = stg.gen = ctx->gen;
         stg.host_hdr = sl.hdr_d;
+        stg.err_out = d_counts ? ctx->d_err : nullptr;  // a submit reports through ac_check
         for (uint32_t j = 0; j < p.n; ++j) {
             const size_t end = ulen[j] != AC_NO_ULEN ? p.off_start[j] : (j + 1 < p.n ? p.off_kmers[j + 1] : p.off_err);
             region[j] = end - p.off_kmers[j];
@@ -1694,8 +1632,6 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
             mark(4);
             return AC_OK;
         };
-        if (pre == 0)
-            if (ac_status st = go()) return st;
         std::atomic<uint32_t> left[AC_MAX_JOBS];
         for (uint32_t j = 0; j < AC_MAX_JOBS; ++j) left[j].store(0, std::memory_order_relaxed);
         for (const Task& x : tasks) left[x.job].fetch_add(1, std::memory_order_relaxed);
@@ -1703,7 +1639,13 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
             pack(t);
             left[tasks[t].job].fetch_sub(1, std::memory_order_release);
         };
+        // the workers start packing job 0 while this thread launches the kernel
         pool.begin((uint32_t)tasks.size(), pack_counted);
+        if (pre == 0)
+            if (ac_status st = go()) {
+                pool.finish();
+                return st;
+            }
         uint32_t t0 = 0;
         for (uint32_t j = 0; j < p.n; ++j) {
             uint32_t t1 = t0;
@@ -1745,7 +1687,7 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
         if (part == 0 && wave_div == 0) return stage_blit_launch(hd + r0, d + r0, r1 - r0, stream);
         return hipMemcpyAsync(d + r0, h + r0, r1 - r0, hipMemcpyHostToDevice, stream);
     };
-    if (!zc && p.n > 1) {
+    if (p.n > 1) {
         // job by job: job j's inputs travel while job j + 1 is packed.  One pool job for all
         // tasks (they are in job order); the caller packs job j's share, waits for its last
         // task, sends it, then helps with job j + 1 while the workers carry on.
@@ -1783,7 +1725,7 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
         pool.run((uint32_t)tasks.size(), pack);
         for (uint32_t j = 0; j < p.n; ++j) no_n[j] = job_no_n(j);
         mark(2);
-        if (!zc) AC_HIP(ctx, transfer(0, p.off_err));
+        AC_HIP(ctx, transfer(0, p.off_err));
     }
     mark(3);
     ac_segment segs[AC_MAX_JOBS];
@@ -1902,13 +1844,10 @@ ac_status ac_error_count_jobs(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint3
             u.plan.n = n_jobs;
             u.plan.slot = q;
             u.plan.scratch = q;
-            // parts are for large calls: DMA only (zero-copy would read the whole image per group)
-            u.plan.zc_eligible = parts == 1;
             if (parts == 1 && stage_early() && live_work(jobs, n_jobs)) {
                 // one part: the early-launch stage (alternating slots 0 / 1, so a call never waits for
                 // the previous call's launch to retire before it packs)
                 u.plan.early = true;
-                u.plan.zc_eligible = false;
                 u.plan.slot = (int)ctx->early_flip;
                 ctx->early_flip ^= 1u;
             }
@@ -1921,16 +1860,6 @@ ac_status ac_error_count_jobs(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint3
     }
     // Units are staged one after another on the host pool; a unit's DMA and
     // kernel run while the next one is packed.
-    const double t_call = now_us();
-    // the transfer path, decided once per context per call (the parts of one device share it;
-    // multi-part calls are DMA-only and do not advance the context's probe cadence)
-    for (size_t g = 0; g < units.size(); ++g) {
-        Unit& u = units[g];
-        if (g > 0 && u.c == units[g - 1].c)
-            u.plan.zc = units[g - 1].plan.zc;
-        else
-            u.plan.zc = (u.plan.zc_eligible || stage_zerocopy_env() >= 0) && stage_zerocopy(u.c, true);
-    }
     for (size_t g = 0; g < units.size(); ++g) {
         Unit& u = units[g];
         AC_HIP(u.c, hipSetDevice(u.c->device));
@@ -1975,13 +1904,7 @@ ac_status ac_error_count_jobs(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint3
             for (uint32_t i = 0; i < jobs[j].n_kmers; ++i) jobs[j].counts[i] += hc[i];
         }
     }
-    if (first_err == AC_OK) {
-        const double us = now_us() - t_call;
-        for (size_t g = 0; g < units.size(); ++g)  // once per context (parts of one device share it)
-            if ((g == 0 || units[g].c != units[g - 1].c) && units[g].plan.zc_eligible)
-                stage_zerocopy_record(units[g].c, units[g].plan.zc, us);
-        units[0].c->zc_last = units[0].plan.early ? 2 : units[0].plan.zc_eligible ? -1 : 0;
-    }
+    if (first_err == AC_OK) units[0].c->last_mode = units[0].plan.early ? 2 : 0;
     if (g_trace.on) {
         g_trace.sum[7] += now_us() - t_sync;
         g_trace.cur[7] += now_us() - t_sync;
@@ -2016,7 +1939,6 @@ ac_status ac_error_count_jobs_submit(ac_ctx* ctx, uint32_t k, const ac_job* jobs
     const int set = (int)ctx->next_slot;
     ctx->next_slot ^= 1u;
     const std::vector<std::vector<uint32_t>> cuts = part_cuts(jobs, n_jobs, parts);
-    const bool zc = parts == 1 && stage_zerocopy(ctx, false);
     if (parts > 1) {
         AC_HIP(ctx, hipMemsetAsync(d_counts, 0, sizeof(uint32_t) * n_counts, caller));
         if (!ctx->sub_zero_ev) AC_HIP(ctx, hipEventCreateWithFlags(&ctx->sub_zero_ev, hipEventDisableTiming));
@@ -2038,8 +1960,8 @@ ac_status ac_error_count_jobs_submit(ac_ctx* ctx, uint32_t k, const ac_job* jobs
         }
         p.slot = AC_STAGE_MAX_PARTS * (1 + set) + q;
         p.scratch = AC_STAGE_MAX_PARTS + q;
-        p.zc_eligible = parts == 1;
-        p.zc = zc;
+        // one part: the early launch, counts and errors into device memory (ac_check reads them)
+        p.early = parts == 1 && stage_early() && live_work(jobs, n_jobs);
         if (ac_status rc = stage_and_launch(ctx, k, jobs, p, st, d_counts, q, (parts > 1 && q == 0) ? 2u : 0u,
                                             parts == 1))
             return rc;
@@ -2056,13 +1978,7 @@ ac_status ac_error_count_jobs_submit(ac_ctx* ctx, uint32_t k, const ac_job* jobs
 
 int ac_exact_path(const ac_ctx* ctx) { return ctx ? ctx->exact_path : -1; }
 
-int ac_stage_mode(const ac_ctx* ctx) {
-    if (!ctx) return -1;
-    if (stage_zerocopy_env() >= 0) return stage_zerocopy_env();
-    if (ctx->zc_last == 2) return 2;  // the last call took the early-launch stage
-    if (ctx->zc_last == 0) return 0;  // the last call's image is DMA-only
-    return ctx->zc_choice;
-}
+int ac_stage_mode(const ac_ctx* ctx) { return ctx ? ctx->last_mode : -1; }
 
 #ifdef AC_STAMPS
 // Diagnostic builds only: per-wave timestamps of the last launch (not declared in the public header).

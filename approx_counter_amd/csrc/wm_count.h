@@ -110,6 +110,7 @@ struct LaunchArgs {
     uint32_t* host_hdr;
     uint32_t* stage;
     uint32_t total_groups;
+    uint32_t* err_out;  // staged: the launch's error bits are also or-ed in here when set (submits)
     uint32_t n_segs;
     uint32_t m;  // k-mer length
     uint32_t P;  // candidates per lane word

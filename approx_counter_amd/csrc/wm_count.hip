@@ -244,6 +244,10 @@ struct BlockLds {
     uint32_t stage_r;
 };
 
+#ifndef AC_STAGE_LOAD_AUX
+#define AC_STAGE_LOAD_AUX 2  // cache policy of the staging copy's loads: nt (A/B builds: 17 = sc0 sc1)
+#endif
+
 // Staged launch ("early launch"): the kernel is launched before
 // the host has packed its inputs.  Wave 0 of every workgroup runs this before
 // anything reads the segment.  It claims AC_STAGE_CHUNK-byte chunks of the
@@ -331,7 +335,10 @@ __device__ __attribute__((noinline)) uint32_t stage_wait(const uint8_t* src, uin
             v4u v[4];
             const uint32_t o = c * AC_STAGE_CHUNK + lane * 16u;
 #pragma unroll
-            for (int u = 0; u < 4; ++u) v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, o + u * 1024u, 0, 17);  // sc0 sc1
+            // (nontemporal, like the copy kernel's loads of the same pinned block: nothing read these
+            // lines before the flag in this launch, so no cache holds them; system-scope loads
+            // were split into narrow PCIe reads: 330 KB took ~15 us instead of ~6)
+            for (int u = 0; u < 4; ++u) v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, o + u * 1024u, 0, AC_STAGE_LOAD_AUX);
 #pragma unroll
             for (int u = 0; u < 4; ++u) __builtin_amdgcn_raw_buffer_store_b128(v[u], rd, o + u * 1024u, 0, 16);  // sc1
         }
@@ -353,7 +360,12 @@ __device__ __attribute__((noinline)) uint32_t stage_wait(const uint8_t* src, uin
         if (lane == 0) atomicOr(err, AC_DEVERR_STAGE);
         return ~0u;
     }
-#ifndef AC_STAGE_NO_ACQUIRE  // A/B build: no L1 invalidate (nothing on this CU read the region before)
+    // No acquire fence: it would only invalidate this CU's L1, and no CU can hold a line of the
+    // region (nothing reads it before the counter says it is complete, and a launch starts with
+    // clean caches).  With 8 workgroups per CU the fences cost ~8 us of staging per call (an A/B:
+    // profiles/r03_m1/summary.log; -DAC_STAGE_ACQUIRE builds restore it).  Stale-line hazards are
+    // what tests/test_gpu_jobs.py::test_early_launch_rotating_inputs_bit_exact rotates data for.
+#ifdef AC_STAGE_ACQUIRE
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
@@ -814,6 +826,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
                 if (__builtin_amdgcn_readfirstlane(last) && lane == 0) {
                     uint32_t* res = a.host_hdr + AC_MAX_SEGS * AC_QUEUE_LINE;
                     const uint32_t e = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (e && a.err_out) atomicOr(a.err_out, e);
                     __hip_atomic_store(res + AC_HDR_ERR, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     __hip_atomic_store(res + AC_HDR_DONE, a.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -309,20 +309,18 @@ def main():
         geo = kc.last_launch()
         kc.close()
 
-    # ---- transfer path of the host-buffer stage (untimed): large images always take the DMA;
-    # otherwise the library times its first synchronous calls with zero-copy and with DMA,
-    # alternately, and keeps the faster (ac_stage_mode; the winner depends on the host's
-    # PCIe / memory latency under load).
+    # ---- the stage's path (ac_stage_mode, after the cold call above): the early launch for calls
+    # counted in one part (the count kernel launched first, staging each read end itself as soon
+    # as the host has packed it), the DMA path (copy engine, 2-4 parts) for >= 2^17 windows.
     tune_calls = 0
-    while counter.stage_mode() < 0 and tune_calls < 32:
+    while counter.stage_mode() < 0 and tune_calls < 4:
         counter.count_jobs(args.k, jobs)
         tune_calls += 1
-    stage_path = {2: "early-launch", 1: "zero-copy", 0: "dma"}.get(counter.stage_mode(), "undecided")
+    stage_path = {2: "early-launch", 0: "dma"}.get(counter.stage_mode(), "undecided")
 
     # ---- pipelined leg (informational, 1 GPU): host-buffer steps back to back, max(steps, 100)
-    # of them.  Run before the stage: the zero-copy path itself runs ~8 % slower for its first
-    # ~80 calls (profiles/r02_trace_percall2.log), so the stage is timed in steady state; one
-    # stage call on the cold context is reported as stage_cold_call_ms. ----------------------
+    # of them.  Run before the stage, so the stage is timed in steady state; one stage call on
+    # the cold context is reported as stage_cold_call_ms. ------------------------------------
     pipelined = None
     if world == 1 and not args.no_pipelined:
         bufs = [torch.zeros(max(1, jobs.n_counts), dtype=torch.int32, device=dev) for _ in range(2)]
@@ -432,14 +430,15 @@ def main():
             "data": DATA_NOTE,
             "config": {"workload": workload_name, "k": args.k, "sn": args.sn, "sl": args.sl, "lim": args.lim,
                        "candidates": n_c, "kmer_bp_per_step": units_job, "kmer_bp_per_rank_step": units_rank,
-                       "stage": ("Dna5 host buffers -> pack (host pool, pinned) -> "
-                                 + ("1 fused launch reading the pinned block (zero-copy)" if stage_path == "zero-copy"
-                                    else ("per read end: pack, then a copy kernel reads it over PCIe into HBM "
-                                          "while the next end is packed -> 1 fused launch (>= 2^17 windows: 2 parts, "
-                                          ">= 2^19: 4, each packed and sent by the copy engine while the previous "
-                                          "part counts)")) + " (both ends)"
+                       "stage": ("Dna5 host buffers -> "
+                                 + ("1 fused count launch issued first, then per read end: pack (host pool, "
+                                    "pinned) + flag; the kernel copies each flagged end into HBM itself and counts it "
+                                    "while the next end is packed" if stage_path == "early-launch"
+                                    else ("per read end: pack (host pool, pinned), copy into HBM while the next end "
+                                          "is packed -> 1 fused launch (>= 2^17 windows: 2 parts, >= 2^19: 4)"))
+                                 + " (both ends)"
                                  + (" -> RCCL all-reduce -> counts D2H" if world > 1 else
-                                    " -> counts written to pinned host memory by the kernel")),
+                                    " -> counts stored to pinned host memory by the kernel, completion polled")),
                        "stage_path": stage_path,
                        "parallelism": (f"{args.scaling} window shards x{world}, "
                                        f"{'RCCL' if backend == 'nccl' else backend} all-reduce of counts")
@@ -454,9 +453,8 @@ def main():
                             "note": "rank 0's pack pool: GPU-local CPUs split among the local ranks, at most its "
                                     "share of the cgroup CPU quota (ac_host_pool_cpus)"}
         out["stage_path_choice"] = {"path": stage_path, "untimed_calls": tune_calls,
-                                    "note": "zero-copy vs DMA chosen by the library (ac_stage_mode): DMA when "
-                                            "image x candidate groups > 256 MB, else timed both ways over the first "
-                                            "synchronous calls and re-checked every 64th call"}
+                                    "note": "ac_stage_mode: early launch for calls counted in one part, DMA parts "
+                                            "for >= 2^17 windows (no timing-based choice since round 3)"}
         if kern_ms is not None:
             ops = OPS_PER_BASE_WORD / P * units_rank  # algorithmic lane-ops per launch (this rank)
             achieved = ops / (kern_ms * 1e-3)

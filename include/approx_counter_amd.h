@@ -266,10 +266,11 @@ typedef struct ac_job {
  * synchronous call, host buffers in and out: jobs[j].counts[i] = M1 count of
  * jobs[j].kmers[i] over jobs[j].sample.  The whole stage runs here: the Dna5
  * windows are packed to 2-bit codes + N bitmap by the host worker pool
- * straight into a pinned staging block, read by the kernel over PCIe or sent
- * into device memory job by job (ac_stage_mode), counted by ONE fused kernel
- * launch over all jobs (calls of >= 2^17 windows: 2-4 parts, each launched
- * once it is sent), and the kernel writes the counts into the pinned block.  On an
+ * straight into a pinned staging block, moved into device memory job by job
+ * (ac_stage_mode: by the count kernel itself -- launched first -- or by a copy
+ * ahead of it), counted by ONE fused kernel launch over all jobs (calls of >=
+ * 2^17 windows: 2-4 parts, each launched once it is sent), and the kernel writes
+ * the counts into the pinned block.  On an
  * ac_create_multi context every job's windows are split into contiguous shards
  * balanced by bases, one per device, and the shard counts are summed.
  * Replaces the index build (537-541), the OpenMP search loop (547-599) and
@@ -349,24 +350,19 @@ int ac_plan_host_cpus(const char* const* rank_cpulists, int n_ranks, int rank, c
                       const int* core_of, int n_core_of, int* out, int cap);
 
 /*
- * How ac_error_count_jobs moves the packed inputs (no reference counterpart):
- * 2 = the early launch (default for calls counted in one part on one device):
- * the count kernel is launched before the host packs, the host flags each job
- * in the pinned block as soon as it is packed, and the kernel copies the job
- * into device memory itself and counts it while later jobs are still being
- * packed; its last workgroup writes the counts and a completion word into
- * pinned memory, which the host polls (AC_STAGE_EARLY=0 turns it off).
- * Otherwise 1 = zero-copy (the kernel reads the pinned staging block over PCIe),
- * 0 = the DMA path: each job copied into device memory as soon as it is packed,
- * without its N bitmap when it holds no N and without window descriptors when
- * its windows have one length (either way the kernel writes the counts into the
- * pinned block), -1 = not decided yet.  Unless AC_STAGE_ZEROCOPY=1/0 forces one:
- * a call whose image x candidate groups exceeds 256 MB always takes the DMA
- * (zero-copy may read the image over PCIe once per group) and then reports 0;
- * for smaller calls a context times its first synchronous calls both ways (they
- * alternate; 10 calls), uses the faster by median of each path's last 4 calls,
- * and every 64th call takes the other path to keep its figures current: which
- * one wins depends on the host (PCIe / host-memory latency under other load).
+ * How the last ac_error_count_jobs call on ctx moved its packed inputs (no
+ * reference counterpart): 2 = the early launch, for calls counted in one part
+ * on one device (default; AC_STAGE_EARLY=0 turns it off): the count kernel is
+ * launched before the host packs, the host flags each job in a pinned header as
+ * soon as it is packed, the kernel copies the flagged job into device memory
+ * itself and counts it while later jobs are still being packed, and its last
+ * workgroup stores the counts and a completion word into pinned memory, which
+ * the host polls.  0 = the DMA path (calls of >= 2^17 windows, cut into 2-4
+ * parts, each packed and copied by the copy engine while the previous part
+ * counts; or AC_STAGE_EARLY=0): a job is sent without its N bitmap when it holds
+ * no N and without window descriptors when its windows have one length.  -1 = no
+ * call yet.  ac_error_count_jobs_submit takes the early launch for one-part calls
+ * too (its counts and errors go to device memory; ac_check reports the errors).
  */
 int ac_stage_mode(const ac_ctx* ctx);
 

@@ -222,7 +222,6 @@ def test_multi_context_shuffled_overlapping_windows():
             assert np.array_equal(multi.count(16, kmers, shuffled), exp), shards
 
 
-@pytest.mark.skipif("AC_STAGE_ZEROCOPY" in os.environ, reason="transfer path forced by the environment")
 def early_rotation(calls=30):
     """Rotates three different workloads (different sizes, N / no N, equal / ragged windows,
     1-3 jobs) through one context's early-launch stage; every call checked."""
@@ -302,7 +301,6 @@ def test_image_size_limit_rejected(counter):
     assert np.array_equal(seg.counts_numpy(), oracle.count_myers(16, kmers, wins, 16))
 
 
-@pytest.mark.skipif("AC_STAGE_ZEROCOPY" in os.environ, reason="transfer path forced by the environment")
 def test_large_image_takes_dma_path():
     """A call whose zero-copy would move more than 256 MB over PCIe (image x candidate
     groups; zero-copy may read the image once per group) is staged by DMA: a fresh

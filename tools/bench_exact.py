@@ -75,12 +75,21 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-host", action="store_true")
+    ap.add_argument("--fast", action="store_true",
+                    help="vectorised equal-length windows (tools/synth.make_windows_fast) instead of make_reads: "
+                         "for the 10^6-window (cfg4) sample")
     a = ap.parse_args()
 
     import torch  # noqa: F401  (device runtime first, see _lib.load)
 
-    reads, _ = make_reads(a.reads, read_len=a.read_len, seed=1)
-    windows = windows_from_reads(reads, a.sl, False)
+    if a.fast:
+        from tools.synth import make_windows_fast
+
+        w2d, _ = make_windows_fast(a.reads, a.sl, seed=1)
+        windows = list(w2d)
+    else:
+        reads, _ = make_reads(a.reads, read_len=a.read_len, seed=1)
+        windows = windows_from_reads(reads, a.sl, False)
     H = host_lib()
     thr = float(H.ach_adjust_threshold(1.0, 16, a.k))
     sample = ac.pack_windows(windows)
@@ -109,12 +118,13 @@ def main():
             once()
             times.append(time.perf_counter() - t0)
         gpu = list(zip(km[: n_out.value].tolist(), ct[: n_out.value].tolist()))
+        path = {1: "partitioned", 0: "hash table"}.get(c.exact_path(), "?")
 
     gpu_s = float(np.median(times))
     out = {"metric": "exact_count_kmer_positions_per_s", "value": n_pos / gpu_s, "unit": "kmer positions/s",
            "ms_per_call": gpu_s * 1e3, "ms_min": min(times) * 1e3, "steps": a.steps,
            "config": {"workload": "exact count + top-lim, start windows", "reads": len(windows), "sl": a.sl,
-                      "k": a.k, "lim": a.lim, "kmer_positions": n_pos, "distinct": n_dist.value},
+                      "k": a.k, "lim": a.lim, "kmer_positions": n_pos, "distinct": n_dist.value}, "path": path,
            "data": "synthetic"}
     if not a.no_host:
         host, n_host, hn, host_s = host_stage(H, windows, a.k, thr, a.lim)
