@@ -12,8 +12,15 @@
 #ifndef AC_WAVES_PER_BLOCK
 #define AC_WAVES_PER_BLOCK 4  // waves per workgroup, all on one candidate group (shared ~Eq table, counts summed in LDS)
 #endif
+#ifndef AC_WORDS
+#define AC_WORDS 1  // lane words per wave (P candidates each): 2 = two NFAs per lane sharing each base's SALU work
+#endif
 #ifndef AC_WAVES_PER_SIMD
+#if AC_WORDS == 2
+#define AC_WAVES_PER_SIMD 4  // two words: twice the registers, half the waves (the same lane words in flight)
+#else
 #define AC_WAVES_PER_SIMD 8  // resident count-kernel waves per SIMD, set by the LDS allocation (<= 64 VGPRs)
+#endif
 #endif
 
 // Device error word bits (ac_check, include/approx_counter_amd.h): a window
@@ -117,7 +124,7 @@ struct LaunchArgs {
 };
 
 inline uint32_t pack_factor(uint32_t k) { return (32u / k) < AC_MAX_PACK ? (32u / k) : AC_MAX_PACK; }
-inline uint32_t cands_per_wave(uint32_t P) { return 64u * P; }
+inline uint32_t cands_per_wave(uint32_t P) { return 64u * P * AC_WORDS; }
 
 // Waves of the count kernel for pattern pack P that fit on the device at once.
 hipError_t resident_waves(uint32_t P, int cu_count, uint32_t* waves);

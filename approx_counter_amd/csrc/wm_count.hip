@@ -170,7 +170,7 @@ __device__ __forceinline__ void load_desc_vec(const uint64_t* start, const uint3
 // Per-wave ~Eq table: word c*64 + lane = the lane's ~Eq mask for character c
 // (A C G T, then N = all ones), read per base with ds_read_addtid_b32.
 struct TidTable {
-    uint32_t e[5 * 64];
+    uint32_t e[AC_WORDS * 5 * 64];  // lane word w's table at e[w * 320]
 };
 
 // Lane `lane`'s word of window bases [sb, sb + 256): lanes 0-15 the 16 code
@@ -240,7 +240,7 @@ constexpr bool TID_EB0 = true;
 // then the staged launch's verdict for the workgroup's segment.
 struct BlockLds {
     TidTable tab;
-    uint32_t cnt[AC_MAX_PACK * 64];
+    uint32_t cnt[AC_WORDS * AC_MAX_PACK * 64];
     uint32_t stage_r;
 };
 
@@ -372,28 +372,42 @@ __device__ __attribute__((noinline)) uint32_t stage_wait(const uint8_t* src, uin
     return load(verdict_w, 0);
 }
 
+// The NFA blocks over the wave's AC_WORDS lane-word states (two words: the
+// generated tid2_* blocks, one base's SALU work and text shared by both words).
+#if AC_WORDS == 2
+#define AC_NFA(nb, s, ...) tid2_block##nb<P, TID_EB0>(s[0], s[1], __VA_ARGS__)
+#define AC_NFA_FIRST(s, ...) tid2_block32_first<P, TID_EB0>(s[0], s[1], __VA_ARGS__)
+#else
+#define AC_NFA(nb, s, ...) tid_block##nb<P, TID_EB0>(s[0], __VA_ARGS__)
+#define AC_NFA_FIRST(s, ...) tid_block32_first<P, TID_EB0>(s[0], __VA_ARGS__)
+#endif
+
 // The remainder (< 16 bases) of a segment: blocks of 8, 4, 2, 1 bases.
 template <int P>
-__device__ __forceinline__ void tid_tail(TidNfa& s, uint32_t code, uint32_t nm, uint32_t rem, uint32_t eb) {
+__device__ __forceinline__ void tid_tail(TidNfa* s, uint32_t code, uint32_t nm, uint32_t rem, uint32_t eb) {
     if (rem & 8u) {
-        tid_block8<P, TID_EB0>(s, code, nm & 0xffu, eb);
+        AC_NFA(8, s, code, nm & 0xffu, eb);
         code >>= 16;
         nm >>= 8;
     }
     if (rem & 4u) {
-        tid_block4<P, TID_EB0>(s, code, nm & 0xfu, eb);
+        AC_NFA(4, s, code, nm & 0xfu, eb);
         code >>= 8;
         nm >>= 4;
     }
     if (rem & 2u) {
-        tid_block2<P, TID_EB0>(s, code, nm & 0x3u, eb);
+        AC_NFA(2, s, code, nm & 0x3u, eb);
         code >>= 4;
         nm >>= 2;
     }
-    if (rem & 1u) tid_block1<P, TID_EB0>(s, code, nm & 0x1u, eb);
+    if (rem & 1u) AC_NFA(1, s, code, nm & 0x1u, eb);
 }
 
-template <int P>
+// STAGED: the early-launch instantiation (staging wait, vector descriptor loads,
+// system-scope count stores, completion word).  The plain launches get a kernel
+// without any of it: in one kernel the extra live values cost SGPR spills inside
+// the count loop (+2.5 % VALU, +3.4 % SALU instructions, ~5 % time at cfg2).
+template <int P, bool STAGED>
 __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
     const uint32_t lane = threadIdx.x & 63u;
     // Workgroup b serves one block-queue (all its waves on one candidate
@@ -448,7 +462,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
     // workgroup's other waves wait at a barrier, then everyone reads the verdict from LDS.
     uint32_t has_n = sg.has_n;
     bool skip = false;
-    if (a.staged && sg.stage_chunks) {  // (a segment sent ahead of a staged launch has no chunks)
+    if (STAGED && sg.stage_chunks) {  // (a segment sent ahead of a staged launch has no chunks)
         if (wib == 0) {
             const uint32_t r = stage_wait(sg.stage_src, sg.stage_dst, sg.stage_chunks,
                                           a.host_hdr + (uint32_t)si * AC_QUEUE_LINE,
@@ -482,13 +496,11 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
     uint32_t ulen = sg.ulen;
     asm volatile("" : "+s"(ulen));
     const uint32_t ustride = ulen == AC_NO_ULEN ? 0u : (ulen + 31u) & ~31u;
-    uint32_t staged = a.staged;
-    asm volatile("" : "+s"(staged));
     auto desc = [&](uint32_t ww, uint64_t& base_out, uint32_t& len_out) __attribute__((always_inline)) {
         if (ulen != AC_NO_ULEN) {
             base_out = (uint64_t)ww * ustride;
             len_out = ulen;
-        } else if (staged) {
+        } else if (STAGED) {
             load_desc_vec(g_start, g_length, ww, base_out, len_out);
         } else {
             load_desc(g_start, g_length, ww, base_out, len_out);
@@ -499,17 +511,19 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
     // first m - 3 bases, whose hit accumulation the first block skips (12 of them).
     const bool skip_first = m >= 15u;
 
-    uint32_t cand[P];
+    // Q = AC_WORDS x P candidates per lane: slot q = w * P + p is pattern p of lane word w
+    constexpr int Q = AC_WORDS * P;
+    uint32_t cand[Q];
 #pragma unroll
-    for (int p = 0; p < P; ++p) cand[p] = g * (64u * P) + (uint32_t)p * 64u + lane;
+    for (int q = 0; q < Q; ++q) cand[q] = g * (64u * Q) + (uint32_t)q * 64u + lane;
     uint32_t first = 0;
 #pragma unroll
     for (int p = 0; p < P; ++p) first |= 1u << (31 - p);
     // Initial rows (empty text): R1 has character 0 set, R2 characters 0 and 1.
     const uint32_t d1_init = ~first, d2_init = ~(first | (first >> P));
-    uint32_t cnt[P];
+    uint32_t cnt[Q];
 #pragma unroll
-    for (int p = 0; p < P; ++p) cnt[p] = 0;
+    for (int q = 0; q < Q; ++q) cnt[q] = 0;
     const uint32_t eb = __builtin_amdgcn_readfirstlane(
         (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)(&lds.tab.e[0]));
     // The eb0 blocks address the table from LDS 0.  Never expected otherwise;
@@ -634,18 +648,25 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
     // 12 us, tools/stamps.py).  The barrier waits for LDS only, not for the
     // window prefetches.
     if (wib == 0) {
-        uint64_t km[P];
 #pragma unroll
-        for (int p = 0; p < P; ++p) km[p] = cand[p] < sg.n_kmers ? sg.kmers[cand[p]] : 0ull;
-        uint32_t ph, pl;
-        build_masks<P>(km, a.m, ph, pl);
+        for (int w = 0; w < AC_WORDS; ++w) {
+            uint64_t km[P];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) lds.tab.e[c * 64 + lane] = ((c & 2) ? ~ph : ph) | ((c & 1) ? ~pl : pl);
-        lds.tab.e[4 * 64 + lane] = ~0u;
+            for (int p = 0; p < P; ++p) {
+                const uint32_t c = cand[w * P + p];
+                km[p] = c < sg.n_kmers ? sg.kmers[c] : 0ull;
+            }
+            uint32_t ph, pl;
+            build_masks<P>(km, a.m, ph, pl);
+            uint32_t* tw = &lds.tab.e[w * 5 * 64];
 #pragma unroll
-        for (int p = 0; p < P; ++p) lds.cnt[p * 64 + lane] = 0u;
+            for (int c = 0; c < 4; ++c) tw[c * 64 + lane] = ((c & 2) ? ~ph : ph) | ((c & 1) ? ~pl : pl);
+            tw[4 * 64 + lane] = ~0u;
+        }
+#pragma unroll
+        for (int q = 0; q < Q; ++q) lds.cnt[q * 64 + lane] = 0u;
     }
-    if (!a.staged) stamp(wave, 7);  // diagnostic builds: the wave's own prologue done, before the barrier
+    if (!STAGED) stamp(wave, 7);  // diagnostic builds: the wave's own prologue done, before the barrier
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     stamp(wave, 1);
 
@@ -672,12 +693,15 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
         if (!ok && lane == 0) atomicOr(a.err, AC_DEVERR_WINDOW);
         const uint32_t nb0 = ok ? min(SEG, len) : 0u;
         const uint32_t nfull0 = nb0 >> 4;
-        TidNfa s = {~0u, d1_init, d2_init, ~0u >> P, d1_init >> P, d2_init >> P, ~0u, d1_init, d2_init};
+        TidNfa s[AC_WORDS];
+#pragma unroll
+        for (int w = 0; w < AC_WORDS; ++w)
+            s[w] = TidNfa{~0u, d1_init, d2_init, ~0u >> P, d1_init >> P, d2_init >> P, ~0u, d1_init, d2_init};
         auto block32 = [&](uint32_t f, uint32_t ch) __attribute__((always_inline)) {
             const uint32_t code = __builtin_amdgcn_readlane(f, ch);
             const uint32_t code2 = __builtin_amdgcn_readlane(f, ch + 1u);
             const uint32_t nm = __builtin_amdgcn_readlane(f, 16u + (ch >> 1));
-            tid_block32<P, TID_EB0>(s, code, code2, nm, eb);
+            AC_NFA(32, s, code, code2, nm, eb);
         };
         // step 1 (after block 0): the claim's result -> the next item's descriptor,
         // or the next window's first words
@@ -686,7 +710,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
                 const uint32_t code = __builtin_amdgcn_readlane(f0, 0u);
                 const uint32_t code2 = __builtin_amdgcn_readlane(f0, 1u);
                 const uint32_t nm = __builtin_amdgcn_readlane(f0, 16u);
-                tid_block32_first<P, TID_EB0>(s, code, code2, nm, eb);
+                AC_NFA_FIRST(s, code, code2, nm, eb);
             } else {
                 block32(f0, 0u);
             }
@@ -711,7 +735,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
                 if (ch < nfull) {
                     const uint32_t code = __builtin_amdgcn_readlane(f, ch);
                     const uint32_t nm = (__builtin_amdgcn_readlane(f, 16u + (ch >> 1)) >> ((ch & 1u) * 16u)) & 0xffffu;
-                    tid_block16<P, TID_EB0>(s, code, nm, eb);
+                    AC_NFA(16, s, code, nm, eb);
                 }
                 if (nb & 15u) {
                     const uint32_t code = __builtin_amdgcn_readlane(f, nfull);
@@ -728,10 +752,12 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
                 segment(f, sb, 0u);
             }
 #pragma unroll
-            for (int p = 0; p < P; ++p) {
-                const uint32_t lb = 31u - ((m - 1u) * P + (uint32_t)p);
-                cnt[p] += 3u - ((s.a0 >> lb) & 1u) - ((s.a1 >> lb) & 1u) - ((s.a2 >> lb) & 1u);
-            }
+            for (int w = 0; w < AC_WORDS; ++w)
+#pragma unroll
+                for (int p = 0; p < P; ++p) {
+                    const uint32_t lb = 31u - ((m - 1u) * P + (uint32_t)p);
+                    cnt[w * P + p] += 3u - ((s[w].a0 >> lb) & 1u) - ((s[w].a1 >> lb) & 1u) - ((s[w].a2 >> lb) & 1u);
+                }
         }
         // advance the cursor; at an item boundary move to the claimed item
         // (descriptor and first words already requested) or steal one
@@ -760,35 +786,35 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
     // cfg2 with one atomic per wave; profiles/r01_kernel_log.md).  Then the
     // group's last workgroup (ticket) moves the sums to the counts.
 #pragma unroll
-    for (int p = 0; p < P; ++p)
-        if (cnt[p]) __hip_atomic_fetch_add(&lds.cnt[p * 64 + lane], cnt[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    for (int q = 0; q < Q; ++q)
+        if (cnt[q]) __hip_atomic_fetch_add(&lds.cnt[q * 64 + lane], cnt[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     // (every wave's error-word atomics are performed before its workgroup's ticket: a staged
     // launch's last group reads the word)
-    if (a.staged) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (STAGED) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 #ifdef AC_COUNTS_DIRECT  // A/B variant: every workgroup adds straight into the (pre-zeroed) counts
     if (wib == 0) {
 #pragma unroll
-        for (int p = 0; p < P; ++p) {
-            const uint32_t v = lds.cnt[p * 64 + lane];
-            if (cand[p] < sg.n_kmers && v) atomicAdd(&sg.counts[cand[p]], v);
+        for (int q = 0; q < Q; ++q) {
+            const uint32_t v = lds.cnt[q * 64 + lane];
+            if (cand[q] < sg.n_kmers && v) atomicAdd(&sg.counts[cand[q]], v);
         }
     }
 #else
     if (wib == 0) {
-        uint32_t* acc = a.acc + sg.acc_begin + g * (64u * P);
+        uint32_t* acc = a.acc + sg.acc_begin + g * (64u * Q);
         // Returning atomics, their results consumed before the ticket: every add
         // has been performed (device-coherent) before this workgroup's ticket.
         // No release/acquire fence: at agent scope those write back the whole
         // XCD L2 (measured: +28 us at cfg2).
         uint32_t sink = 0;
 #pragma unroll
-        for (int p = 0; p < P; ++p) {
-            const uint32_t v = lds.cnt[p * 64 + lane];
+        for (int q = 0; q < Q; ++q) {
+            const uint32_t v = lds.cnt[q * 64 + lane];
 #ifdef AC_TIMING_NO_ATOMICS  // timing-only build: results discarded (kept live by an impossible store)
-            if (v == 0xdeadbeefu) acc[p * 64 + lane] = 1u;
+            if (v == 0xdeadbeefu) acc[q * 64 + lane] = 1u;
 #else
-            if (v) sink |= __hip_atomic_fetch_add(&acc[p * 64 + lane], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (v) sink |= __hip_atomic_fetch_add(&acc[q * 64 + lane], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #endif
         }
         asm volatile("" ::"v"(sink));
@@ -802,20 +828,20 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
         t = __builtin_amdgcn_readfirstlane(t);
         if (t == n_wg - 1u) {  // every other workgroup of the group has added its sums
 #pragma unroll
-            for (int p = 0; p < P; ++p) {
-                const uint32_t v = __hip_atomic_exchange(&acc[p * 64 + lane], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (cand[p] < sg.n_kmers) {
+            for (int q = 0; q < Q; ++q) {
+                const uint32_t v = __hip_atomic_exchange(&acc[q * 64 + lane], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (cand[q] < sg.n_kmers) {
                     if (a.add_counts) {
-                        if (v) atomicAdd(&sg.counts[cand[p]], v);
-                    } else if (a.staged) {  // host memory the host reads before the stream completes
-                        __hip_atomic_store(&sg.counts[cand[p]], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        if (v) atomicAdd(&sg.counts[cand[q]], v);
+                    } else if (STAGED) {  // host memory the host reads before the stream completes
+                        __hip_atomic_store(&sg.counts[cand[q]], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     } else {
-                        sg.counts[cand[p]] = v;
+                        sg.counts[cand[q]] = v;
                     }
                 }
             }
             if (lane == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (a.staged) {
+            if (STAGED) {
                 // the launch's last group publishes its error bits, then its completion, to the host
                 // (its counts went out as system-scope stores; each group's, drained before its add)
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -840,20 +866,21 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
 
 }  // namespace
 
-template <int P>
+template <int P, bool STAGED>
 __global__ __launch_bounds__(64 * WAVES_PER_BLOCK, AC_WAVES_PER_SIMD) void wm2_count_kernel(LaunchArgs a) {
     // The LDS allocation also caps residency at AC_WAVES_PER_SIMD waves per
     // SIMD (8: faster than 6 or 10, profiles/r01_kernel_log.md).
     constexpr int kBlocksPerCu = 4 * AC_WAVES_PER_SIMD / WAVES_PER_BLOCK;
     __shared__ BlockLds lds[(160 * 1024 / kBlocksPerCu) / sizeof(BlockLds)];
-    count_body<P>(a, lds[0]);
+    count_body<P, STAGED>(a, lds[0]);
 }
 
 namespace {
 template <int P>
 hipError_t occupancy(int cu_count, uint32_t* waves) {
     int blocks = 0;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, wm2_count_kernel<P>, 64 * WAVES_PER_BLOCK, 0);
+    hipError_t e =
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, wm2_count_kernel<P, false>, 64 * WAVES_PER_BLOCK, 0);
     if (e != hipSuccess) return e;
     if (blocks < 1) blocks = 1;
     *waves = (uint32_t)blocks * WAVES_PER_BLOCK * (uint32_t)cu_count;
@@ -886,13 +913,21 @@ hipError_t launch_wm2_count(const LaunchArgs& args, hipStream_t stream) {
     if (args.total_waves == 0) return hipSuccess;
     const uint64_t blocks = (args.total_waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
     const dim3 grid((uint32_t)blocks), block(64 * WAVES_PER_BLOCK);
+#define AC_LAUNCH(PP)                                                                     \
+    case PP:                                                                              \
+        if (args.staged)                                                                  \
+            hipLaunchKernelGGL((wm2_count_kernel<PP, true>), grid, block, 0, stream, args);  \
+        else                                                                              \
+            hipLaunchKernelGGL((wm2_count_kernel<PP, false>), grid, block, 0, stream, args); \
+        break;
     switch (args.P) {
-        case 1: hipLaunchKernelGGL(wm2_count_kernel<1>, grid, block, 0, stream, args); break;
-        case 2: hipLaunchKernelGGL(wm2_count_kernel<2>, grid, block, 0, stream, args); break;
-        case 3: hipLaunchKernelGGL(wm2_count_kernel<3>, grid, block, 0, stream, args); break;
-        case 4: hipLaunchKernelGGL(wm2_count_kernel<4>, grid, block, 0, stream, args); break;
+        AC_LAUNCH(1)
+        AC_LAUNCH(2)
+        AC_LAUNCH(3)
+        AC_LAUNCH(4)
         default: return hipErrorInvalidValue;
     }
+#undef AC_LAUNCH
     return hipGetLastError();
 }
 

@@ -30,6 +30,7 @@ AHEAD = 4  # LDS reads in flight ahead of the base being computed
 WAIT_PAIR = True  # one s_waitcnt per two bases (the SALU is the CU-shared resource)
 NE = AHEAD + 3  # rotating ~Eq registers (base i's is read by rows 0-2 at steps i..i+2)
 FIRST_SKIP = 12  # bases of a window's start with no possible occurrence end (k >= 15: k - 3 >= 12)
+TABLE_BYTES = 5 * 64 * 4  # one lane word's ~Eq table (5 characters x 64 lanes x u32); word w's at w * this
 
 
 def m0_setup(j, with_n, eb0):
@@ -47,105 +48,139 @@ def m0_setup(j, with_n, eb0):
     return s
 
 
-def block(nb, with_n, eb0, skip=0):
+def block(nb, with_n, eb0, skip=0, W=1):
     """Skewed (software-pipelined) schedule: step s runs row 0 of base s, row 1 of
     base s-1 and row 2 of base s-2 -- three independent dependency chains per wave.
     Row r of base i needs row r of base i-1 and row r-1 of bases i-1 and i, all
     produced at earlier steps.  Values live in 4 rotating slots per (row, D/T);
-    slot 3 is the operand register, so blocks of a multiple of 4 bases end in place."""
+    slot 3 is the operand register, so blocks of a multiple of 4 bases end in place.
+    W = 2: two lane words per wave (2 x P candidates per lane) share each base's SALU
+    work; word w reads its own ~Eq table (LDS offset w * 1280 B) and its ops are
+    interleaved with the other word's, six dependency chains per wave."""
 
-    def D(r, i):
-        return f"%[d{r}]" if i % 4 == 3 else f"%[D{r}{i % 4}]"
+    def pre(w):
+        return "" if W == 1 else f"w{w}"
 
-    def T(r, i):
-        return f"%[s{r}]" if i % 4 == 3 else f"%[T{r}{i % 4}]"
+    def D(w, r, i):
+        return f"%[{pre(w)}d{r}]" if i % 4 == 3 else f"%[{pre(w)}D{r}{i % 4}]"
 
-    def E(i):
-        return f"%[e{i % NE}]"
+    def T(w, r, i):
+        return f"%[{pre(w)}s{r}]" if i % 4 == 3 else f"%[{pre(w)}T{r}{i % 4}]"
+
+    def E(w, i):
+        return f"%[{pre(w)}e{i % NE}]"
+
+    def X(w, r):
+        return f"%[{pre(w)}x{r}]"
+
+    def A(w, r):
+        return f"%[{pre(w)}a{r}]"
+
+    def rd(w, i):
+        return f"ds_read_addtid_b32 {E(w, i)}" + (f" offset:{w * TABLE_BYTES}" if w else "")
 
     L = []
     for j in range(min(AHEAD, nb)):
         L += m0_setup(j, with_n, eb0)
-        L += ["s_nop 0", f"ds_read_addtid_b32 {E(j)}"]
+        L += ["s_nop 0"] + [rd(w, j) for w in range(W)]
     for st in range(nb + 2):
         rows = [(r, st - r) for r in range(3) if 0 <= st - r < nb]
         if st < nb:
             issued = min(st + AHEAD, nb)
             if not WAIT_PAIR:
-                L.append(f"s_waitcnt lgkmcnt({issued - (st + 1)})")
+                L.append(f"s_waitcnt lgkmcnt({W * (issued - (st + 1))})")
             elif st % 2 == 0:  # bases st and st+1 (reads complete in order)
-                L.append(f"s_waitcnt lgkmcnt({max(0, issued - min(st + 2, nb))})")
+                L.append(f"s_waitcnt lgkmcnt({W * max(0, issued - min(st + 2, nb))})")
         ahead = st < nb and st + AHEAD < nb
         if ahead:
             L += m0_setup(st + AHEAD, with_n, eb0)
         # phase A: row 0's new D; rows 1-2's x = s_{r-1} & d_{r-1} & t_{r-1}
         for r, i in rows:
-            if r == 0:
-                L.append(f"v_or_b32 {D(0, i)}, {T(0, i - 1)}, {E(i)}")
-            else:
-                L.append(f"v_bitop3_b32 %[x{r}], {T(r - 1, i - 1)}, {D(r - 1, i - 1)}, {T(r - 1, i)} bitop3:0x80")
+            for w in range(W):
+                if r == 0:
+                    L.append(f"v_or_b32 {D(w, 0, i)}, {T(w, 0, i - 1)}, {E(w, i)}")
+                else:
+                    L.append(f"v_bitop3_b32 {X(w, r)}, {T(w, r - 1, i - 1)}, {D(w, r - 1, i - 1)}, {T(w, r - 1, i)} "
+                             f"bitop3:0x80")
             if r == 0 and ahead:  # one state after the M0 write
-                L.append(f"ds_read_addtid_b32 {E(st + AHEAD)}")
+                L += [rd(w, st + AHEAD) for w in range(W)]
         # phase B: row 0's shift; rows 1-2's new D = (s_r | ~Eq) & x
         for r, i in rows:
-            if r == 0:
-                L.append(f"v_lshrrev_b32 {T(0, i)}, %[P], {D(0, i)}")
-            else:
-                L.append(f"v_bitop3_b32 {D(r, i)}, {T(r, i - 1)}, {E(i)}, %[x{r}] bitop3:0xa8")
+            for w in range(W):
+                if r == 0:
+                    L.append(f"v_lshrrev_b32 {T(w, 0, i)}, %[P], {D(w, 0, i)}")
+                else:
+                    L.append(f"v_bitop3_b32 {D(w, r, i)}, {T(w, r, i - 1)}, {E(w, i)}, {X(w, r)} bitop3:0xa8")
         # phase C: rows 1-2's shifts, then the hit accumulators (pairs of bases)
         for r, i in rows:
             if r > 0:
-                L.append(f"v_lshrrev_b32 {T(r, i)}, %[P], {D(r, i)}")
+                for w in range(W):
+                    L.append(f"v_lshrrev_b32 {T(w, r, i)}, %[P], {D(w, r, i)}")
         for r, i in rows:
             if i < skip:  # a window's first bases: no occurrence can end there (skip <= k - 3)
                 continue
-            if i % 2 == 1:
-                L.append(f"v_bitop3_b32 %[a{r}], %[a{r}], {D(r, i - 1)}, {D(r, i)} bitop3:0x80")
-            elif i == nb - 1:  # unpaired last base (odd nb)
-                L.append(f"v_and_b32 %[a{r}], %[a{r}], {D(r, i)}")
+            for w in range(W):
+                if i % 2 == 1:
+                    L.append(f"v_bitop3_b32 {A(w, r)}, {A(w, r)}, {D(w, r, i - 1)}, {D(w, r, i)} bitop3:0x80")
+                elif i == nb - 1:  # unpaired last base (odd nb)
+                    L.append(f"v_and_b32 {A(w, r)}, {A(w, r)}, {D(w, r, i)}")
     if (nb - 1) % 4 != 3:  # final state not in the operand slot
-        for r in range(3):
-            L.append(f"v_mov_b32 %[d{r}], {D(r, nb - 1)}")
-            L.append(f"v_mov_b32 %[s{r}], {T(r, nb - 1)}")
+        for w in range(W):
+            for r in range(3):
+                L.append(f"v_mov_b32 %[{pre(w)}d{r}], {D(w, r, nb - 1)}")
+                L.append(f"v_mov_b32 %[{pre(w)}s{r}], {T(w, r, nb - 1)}")
     return L
 
 
-def body(nb, eb0, skip=0):
+def body(nb, eb0, skip=0, W=1):
     """Whole statement text: N-free chunks take the fast path, chunks with an N
     the N-aware one (same registers, so hipcc sees one statement)."""
     L = ["s_mov_b32 %[keep], m0", "s_cmp_lg_u32 %[nm], 0", "s_cbranch_scc1 .Lnpath%="]
-    L += block(nb, False, eb0, skip)
+    L += block(nb, False, eb0, skip, W)
     L += ["s_branch .Lend%=", ".Lnpath%=:"]
-    L += block(nb, True, eb0, skip)
+    L += block(nb, True, eb0, skip, W)
     L += [".Lend%=:", "s_mov_b32 m0, %[keep]"]
     return "\n".join(f'            "{ln}\\n\\t"' for ln in L)
 
 
-def emit(nb, skip=0, name=None):
+def emit(nb, skip=0, name=None, W=1):
     extra = [f"code{i}" for i in range(2, (nb + 15) // 16 + 1)]
     code2_in = "".join(f', [{c}] "s"({c})' for c in extra)
     code2_arg = "".join(f", uint32_t {c}" for c in extra)
-    scratch = [f"D{r}{k}" for r in range(3) for k in range(3)] + [f"T{r}{k}" for r in range(3) for k in range(3)]
-    scratch += ["x1", "x2"] + [f"e{k}" for k in range(NE)]
+    pres = [""] if W == 1 else [f"w{w}" for w in range(W)]
+    scratch = []
+    for p in pres:
+        scratch += [f"{p}D{r}{k}" for r in range(3) for k in range(3)] + [f"{p}T{r}{k}" for r in range(3) for k in range(3)]
+        scratch += [f"{p}x1", f"{p}x2"] + [f"{p}e{k}" for k in range(NE)]
     decl = ", ".join(scratch)
     outs = ", ".join(f'[{v}] "=&v"({v})' for v in scratch)
-    operands = f"""            : [d0] "+v"(s.d0), [d1] "+v"(s.d1), [d2] "+v"(s.d2), [s0] "+v"(s.s0), [s1] "+v"(s.s1),
-              [s2] "+v"(s.s2), [a0] "+v"(s.a0), [a1] "+v"(s.a1), [a2] "+v"(s.a2),
+    states = []
+    for w, p in enumerate(pres):
+        sv = "s" if W == 1 else f"s{w}"
+        states.append(", ".join(f'[{p}{f}] "+v"({sv}.{f})' for f in ("d0", "d1", "d2", "s0", "s1", "s2", "a0", "a1", "a2")))
+    if W == 1:  # (the one-word text exactly as before W existed)
+        state_ops = """[d0] "+v"(s.d0), [d1] "+v"(s.d1), [d2] "+v"(s.d2), [s0] "+v"(s.s0), [s1] "+v"(s.s1),
+              [s2] "+v"(s.s2), [a0] "+v"(s.a0), [a1] "+v"(s.a1), [a2] "+v"(s.a2)"""
+        sig = "TidNfa& s"
+    else:
+        state_ops = ",\n              ".join(states)
+        sig = ", ".join(f"TidNfa& s{w}" for w in range(W))
+    operands = f"""            : {state_ops},
               {outs},
               [t] "=&s"(t), [keep] "=&s"(keep)
             : [code] "s"(code){code2_in}, [nm] "s"(nm), [eb] "s"(eb), [P] "n"(P)
             : "memory", "scc");"""
     return f"""template <int P, bool EB0>
-__device__ __forceinline__ void {name or f"tid_block{nb}"}(TidNfa& s, uint32_t code{code2_arg}, uint32_t nm, uint32_t eb) {{
+__device__ __forceinline__ void {name or f"tid_block{nb}"}({sig}, uint32_t code{code2_arg}, uint32_t nm, uint32_t eb) {{
     uint32_t {decl};
     uint32_t t, keep;
     if constexpr (EB0) {{
         asm volatile(
-{body(nb, True, skip)}
+{body(nb, True, skip, W)}
 {operands}
     }} else {{
         asm volatile(
-{body(nb, False, skip)}
+{body(nb, False, skip, W)}
 {operands}
     }}
 }}
@@ -171,6 +206,11 @@ def main():
     # k - 3 (valid for k >= 15; wm_count.hip picks it then).
     parts.append("// tid_block32 for a window's first 32 bases, k >= 15: no hit accumulation over bases 0-11.")
     parts.append(emit(32, skip=FIRST_SKIP, name="tid_block32_first"))
+    # Two lane words per wave (AC_WORDS = 2 builds, wm_count.hip): the same blocks over two states.
+    parts.append("// Two lane words per wave (AC_WORDS == 2): both words' NFAs, one base's SALU work shared.")
+    for nb in (32, 16, 8, 4, 2, 1):
+        parts.append(emit(nb, W=2, name=f"tid2_block{nb}"))
+    parts.append(emit(32, skip=FIRST_SKIP, name="tid2_block32_first", W=2))
     with open(OUT, "w") as fh:
         fh.write("\n".join(parts))
     print("wrote", OUT)

@@ -46,6 +46,11 @@ exactprof)  # kernel traces of the exact count, partitioned vs hash table, at cf
         python3 "$GRAFT_REPO_ROOT/tools/bench_exact.py" $a --no-host ) > "$d.log" 2>&1 || exit 3
     done
   done ;;
+prof)  # PMC passes + kernel traces of the count kernel (device-resident), and a trace of the bench's stage
+  ( bash tools/pmc_passes.sh cfg2 r03_cfg2 ) > "$OUT/pmc_passes.log" 2>&1 || exit 4
+  ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_bench" -o run -- \
+    python3 "$GRAFT_REPO_ROOT/bench.py" --steps 100 --warmup 10 --no-cpu-baseline --no-pipelined --kernel-launches 100 ) \
+    > "$OUT/prof_bench.log" 2>&1 || exit 5 ;;
 cli)
   run cli_cfg2 300 python3 tools/cli_e2e.py --reads 10000 --lim 500
   run cli_cfg3 400 python3 tools/cli_e2e.py --reads 100000 --lim 2000
