@@ -274,7 +274,8 @@ class ApproxCounter:
         return int(self._L.ac_exact_path(self._h))
 
     def stage_mode(self) -> int:
-        """ac_stage_mode: 1 zero-copy, 0 DMA, -1 not decided yet (count_jobs probes both first)."""
+        """ac_stage_mode: the last jobs call's stage -- 2 early launch (the count kernel copies each
+        job in as the host flags it), 0 copy kernel / copy engine ahead of the launch, -1 no call yet."""
         return int(self._L.ac_stage_mode(self._h))
 
     # ---- multi-process data parallelism: the count all-reduce over RCCL (ac_comm_*) ----

@@ -95,7 +95,7 @@ struct ac_ctx {
     struct Slot {
         void* h = nullptr;
         void* d = nullptr;
-        void* hd = nullptr;  // device address of the pinned block (zero-copy stage)
+        void* hd = nullptr;  // device address of the pinned block (staging reads, counts written back)
         size_t h_cap = 0, d_cap = 0;
         hipEvent_t ev = nullptr;
         bool pending = false;
@@ -108,7 +108,6 @@ struct ac_ctx {
     uint32_t gen = 0;                // generation of the last early-launch call (never 0 once used)
     uint32_t early_flip = 0;         // early-launch calls alternate between staging slots 0 and 1
     int exact_path = -1;             // the last exact count's path: 1 partitioned, 0 hash table
-    // zero-copy vs DMA choice of the host-buffer stage (ac_stage_mode)
     int last_mode = -1;  // ac_stage_mode: 2 the last jobs call was an early launch, 0 the DMA path
 };
 
@@ -1326,7 +1325,7 @@ struct JobPlan {
 // windows, four from 2^19.  Same box, interleaved (profiles/r02_stage_parts_ab2.log):
 // cfg4 (2M windows) step p50 10.26-10.31 ms in four parts, 10.42-10.49 in three,
 // 11.27 in two (13.3 in one, r02_stage_parts_ab.log); cfg3 (200k windows)
-// 3.27-3.29 ms in two vs 3.24-3.40 one-part with the zero-copy / DMA chooser
+// 3.27-3.29 ms in two vs 3.24-3.40 one-part with round 2's (since removed) zero-copy / DMA chooser
 // and 3.42 one-part DMA.
 constexpr uint64_t STAGE_PARTS2_MIN_WINDOWS = 1ull << 17, STAGE_PARTS4_MIN_WINDOWS = 1ull << 19;
 int stage_parts(uint64_t total_w) {
@@ -1426,13 +1425,15 @@ ac_status check_jobs(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint32_t n_job
 
 // Packs the jobs' window ranges p.lo/p.hi into a staging slot of ctx (the
 // host worker pool writes the 2-bit codes, N bitmap and window descriptors
-// straight into pinned memory), sends the inputs with one DMA on `stream`
-// and launches the fused count kernel, whose counts go to d_counts (job j at
-// d_counts + sum of the earlier n_kmers) or, when NULL, to the slot's counts
-// area.  Records the slot's event after the launch.
-// Staging slots: a synchronous call's part q always uses slot q (the same
-// pinned pages every call: with the zero-copy stage the GPU's translations of
-// them stay cached); submits alternate between the last two slots.
+// straight into pinned memory), moves each job's region into device memory
+// (p.early: the count kernel copies it itself once the host flags the job;
+// otherwise the copy kernel on `stream`, or the copy engine for multi-part
+// calls) and launches the fused count kernel, whose counts go to d_counts
+// (job j at d_counts + sum of the earlier n_kmers) or, when NULL, to the
+// slot's pinned counts area.  Records the slot's event after the launch.
+// Staging slots: a synchronous call's part q uses slot q (a one-part early
+// launch alternates between slots 0 and 1); submits alternate between two
+// sets of slots of their own.
 ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan& p, hipStream_t stream,
                            uint32_t* d_counts, int part = 0, uint32_t wave_div = 0, bool zero = true) {
     using acamd::image_span;

@@ -12,16 +12,20 @@
 #ifndef AC_WAVES_PER_BLOCK
 #define AC_WAVES_PER_BLOCK 4  // waves per workgroup, all on one candidate group (shared ~Eq table, counts summed in LDS)
 #endif
-#ifndef AC_WORDS
-#define AC_WORDS 1  // lane words per wave (P candidates each): 2 = two NFAs per lane sharing each base's SALU work
-#endif
-#ifndef AC_WAVES_PER_SIMD
-#if AC_WORDS == 2
-#define AC_WAVES_PER_SIMD 4  // two words: twice the registers, half the waves (the same lane words in flight)
+// Lane words per wave (P candidates each) for pattern pack P: 2 = two NFAs per lane sharing each
+// base's SALU work (LDS table read, M0 set-up) at 4 resident waves per SIMD, 1 = one NFA at 8.
+// Two words for P = 2 (k = 11-16): cfg2 kernel 107-108 -> 102-103 us, cfg3 equal; one word for
+// P = 1, where two were 0.8 % slower at cfg5 (profiles/r03_dual_ab.log).  P = 3-4 (k <= 10) are
+// unmeasured and keep one.  -DAC_WORDS=1 / 2 forces one choice for every P (A/B builds).
+constexpr int words_for(int P) {
+#ifdef AC_WORDS
+    return (void)P, AC_WORDS;
 #else
-#define AC_WAVES_PER_SIMD 8  // resident count-kernel waves per SIMD, set by the LDS allocation (<= 64 VGPRs)
+    return P == 2 ? 2 : 1;
 #endif
-#endif
+}
+// resident count-kernel waves per SIMD, set by the LDS allocation (<= 64 VGPRs with one word)
+constexpr int waves_per_simd(int W) { return W == 2 ? 4 : 8; }
 
 // Device error word bits (ac_check, include/approx_counter_amd.h): a window
 // that is misaligned or reaches past the image was skipped; the kernel found
@@ -124,7 +128,7 @@ struct LaunchArgs {
 };
 
 inline uint32_t pack_factor(uint32_t k) { return (32u / k) < AC_MAX_PACK ? (32u / k) : AC_MAX_PACK; }
-inline uint32_t cands_per_wave(uint32_t P) { return 64u * P * AC_WORDS; }
+inline uint32_t cands_per_wave(uint32_t P) { return 64u * P * (uint32_t)words_for((int)P); }
 
 // Waves of the count kernel for pattern pack P that fit on the device at once.
 hipError_t resident_waves(uint32_t P, int cu_count, uint32_t* waves);

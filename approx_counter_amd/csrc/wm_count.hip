@@ -169,8 +169,9 @@ __device__ __forceinline__ void load_desc_vec(const uint64_t* start, const uint3
 
 // Per-wave ~Eq table: word c*64 + lane = the lane's ~Eq mask for character c
 // (A C G T, then N = all ones), read per base with ds_read_addtid_b32.
+template <int W>
 struct TidTable {
-    uint32_t e[AC_WORDS * 5 * 64];  // lane word w's table at e[w * 320]
+    uint32_t e[W * 5 * 64];  // lane word w's table at e[w * 320]
 };
 
 // Lane `lane`'s word of window bases [sb, sb + 256): lanes 0-15 the 16 code
@@ -238,9 +239,10 @@ constexpr bool TID_EB0 = true;
 
 // Workgroup LDS: the ~Eq table, then the count vector the waves sum into,
 // then the staged launch's verdict for the workgroup's segment.
+template <int W>
 struct BlockLds {
-    TidTable tab;
-    uint32_t cnt[AC_WORDS * AC_MAX_PACK * 64];
+    TidTable<W> tab;
+    uint32_t cnt[W * AC_MAX_PACK * 64];
     uint32_t stage_r;
 };
 
@@ -372,18 +374,25 @@ __device__ __attribute__((noinline)) uint32_t stage_wait(const uint8_t* src, uin
     return load(verdict_w, 0);
 }
 
-// The NFA blocks over the wave's AC_WORDS lane-word states (two words: the
-// generated tid2_* blocks, one base's SALU work and text shared by both words).
-#if AC_WORDS == 2
-#define AC_NFA(nb, s, ...) tid2_block##nb<P, TID_EB0>(s[0], s[1], __VA_ARGS__)
-#define AC_NFA_FIRST(s, ...) tid2_block32_first<P, TID_EB0>(s[0], s[1], __VA_ARGS__)
-#else
-#define AC_NFA(nb, s, ...) tid_block##nb<P, TID_EB0>(s[0], __VA_ARGS__)
-#define AC_NFA_FIRST(s, ...) tid_block32_first<P, TID_EB0>(s[0], __VA_ARGS__)
-#endif
+// The NFA blocks over the wave's W lane-word states (two words: the generated
+// tid2_* blocks, one base's SALU work and text shared by both words).
+#define AC_NFA(nb, s, ...)                                            \
+    do {                                                              \
+        if constexpr (W == 2)                                         \
+            tid2_block##nb<P, TID_EB0>(s[0], s[W - 1], __VA_ARGS__); \
+        else                                                          \
+            tid_block##nb<P, TID_EB0>(s[0], __VA_ARGS__);            \
+    } while (0)
+#define AC_NFA_FIRST(s, ...)                                               \
+    do {                                                                   \
+        if constexpr (W == 2)                                              \
+            tid2_block32_first<P, TID_EB0>(s[0], s[W - 1], __VA_ARGS__); \
+        else                                                               \
+            tid_block32_first<P, TID_EB0>(s[0], __VA_ARGS__);            \
+    } while (0)
 
 // The remainder (< 16 bases) of a segment: blocks of 8, 4, 2, 1 bases.
-template <int P>
+template <int P, int W>
 __device__ __forceinline__ void tid_tail(TidNfa* s, uint32_t code, uint32_t nm, uint32_t rem, uint32_t eb) {
     if (rem & 8u) {
         AC_NFA(8, s, code, nm & 0xffu, eb);
@@ -408,7 +417,8 @@ __device__ __forceinline__ void tid_tail(TidNfa* s, uint32_t code, uint32_t nm, 
 // without any of it: in one kernel the extra live values cost SGPR spills inside
 // the count loop (+2.5 % VALU, +3.4 % SALU instructions, ~5 % time at cfg2).
 template <int P, bool STAGED>
-__device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
+__device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_for(P)>& lds) {
+    constexpr int W = words_for(P);
     const uint32_t lane = threadIdx.x & 63u;
     // Workgroup b serves one block-queue (all its waves on one candidate
     // group); its waves take the block-queue's AC_WAVES_PER_BLOCK sub-queues.
@@ -511,8 +521,8 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
     // first m - 3 bases, whose hit accumulation the first block skips (12 of them).
     const bool skip_first = m >= 15u;
 
-    // Q = AC_WORDS x P candidates per lane: slot q = w * P + p is pattern p of lane word w
-    constexpr int Q = AC_WORDS * P;
+    // Q = W x P candidates per lane: slot q = w * P + p is pattern p of lane word w
+    constexpr int Q = W * P;
     uint32_t cand[Q];
 #pragma unroll
     for (int q = 0; q < Q; ++q) cand[q] = g * (64u * Q) + (uint32_t)q * 64u + lane;
@@ -649,7 +659,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
     // window prefetches.
     if (wib == 0) {
 #pragma unroll
-        for (int w = 0; w < AC_WORDS; ++w) {
+        for (int w = 0; w < W; ++w) {
             uint64_t km[P];
 #pragma unroll
             for (int p = 0; p < P; ++p) {
@@ -693,9 +703,9 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
         if (!ok && lane == 0) atomicOr(a.err, AC_DEVERR_WINDOW);
         const uint32_t nb0 = ok ? min(SEG, len) : 0u;
         const uint32_t nfull0 = nb0 >> 4;
-        TidNfa s[AC_WORDS];
+        TidNfa s[W];
 #pragma unroll
-        for (int w = 0; w < AC_WORDS; ++w)
+        for (int w = 0; w < W; ++w)
             s[w] = TidNfa{~0u, d1_init, d2_init, ~0u >> P, d1_init >> P, d2_init >> P, ~0u, d1_init, d2_init};
         auto block32 = [&](uint32_t f, uint32_t ch) __attribute__((always_inline)) {
             const uint32_t code = __builtin_amdgcn_readlane(f, ch);
@@ -740,7 +750,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
                 if (nb & 15u) {
                     const uint32_t code = __builtin_amdgcn_readlane(f, nfull);
                     const uint32_t nm = (__builtin_amdgcn_readlane(f, 16u + (nfull >> 1)) >> ((nfull & 1u) * 16u)) & 0xffffu;
-                    tid_tail<P>(s, code, nm, nb & 15u, eb);
+                    tid_tail<P, W>(s, code, nm, nb & 15u, eb);
                 }
             };
             segment(f0, 0u, nfull0 >= 4u ? 4u : (nfull0 >= 2u ? 2u : 0u));
@@ -752,7 +762,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
                 segment(f, sb, 0u);
             }
 #pragma unroll
-            for (int w = 0; w < AC_WORDS; ++w)
+            for (int w = 0; w < W; ++w)
 #pragma unroll
                 for (int p = 0; p < P; ++p) {
                     const uint32_t lb = 31u - ((m - 1u) * P + (uint32_t)p);
@@ -867,11 +877,12 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds& lds) {
 }  // namespace
 
 template <int P, bool STAGED>
-__global__ __launch_bounds__(64 * WAVES_PER_BLOCK, AC_WAVES_PER_SIMD) void wm2_count_kernel(LaunchArgs a) {
-    // The LDS allocation also caps residency at AC_WAVES_PER_SIMD waves per
-    // SIMD (8: faster than 6 or 10, profiles/r01_kernel_log.md).
-    constexpr int kBlocksPerCu = 4 * AC_WAVES_PER_SIMD / WAVES_PER_BLOCK;
-    __shared__ BlockLds lds[(160 * 1024 / kBlocksPerCu) / sizeof(BlockLds)];
+__global__ __launch_bounds__(64 * WAVES_PER_BLOCK, waves_per_simd(words_for(P))) void wm2_count_kernel(LaunchArgs a) {
+    // The LDS allocation also caps residency at waves_per_simd waves per SIMD
+    // (one word: 8, faster than 6 or 10, profiles/r01_kernel_log.md; two words: 4).
+    constexpr int W = words_for(P);
+    constexpr int kBlocksPerCu = 4 * waves_per_simd(W) / WAVES_PER_BLOCK;
+    __shared__ BlockLds<W> lds[(160 * 1024 / kBlocksPerCu) / sizeof(BlockLds<W>)];
     count_body<P, STAGED>(a, lds[0]);
 }
 

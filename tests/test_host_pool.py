@@ -24,3 +24,16 @@ def test_every_task_runs_once(stress, threads, spin_us, calls):
     r = subprocess.run([stress, str(threads), str(calls)], env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     assert r.stdout.startswith("ok:")
+
+
+@pytest.mark.parametrize("threads,calls,callers,hogs,pin", [
+    (8, 3000, 3, 0, 0),    # several contexts' threads sharing host_pool() (the run lock)
+    (8, 2000, 2, 8, 1),    # pinned workers under neighbour load: workers descheduled mid-task
+    (16, 1000, 4, 4, 1),
+])
+def test_concurrent_callers_under_load(stress, threads, calls, callers, hogs, pin):
+    env = dict(os.environ, AC_HOST_SPIN_US="50")
+    r = subprocess.run([stress, str(threads), str(calls), str(callers), str(hogs), str(pin)], env=env,
+                       capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.startswith("ok:"), r.stdout

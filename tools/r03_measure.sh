@@ -4,6 +4,7 @@
 # end to end at cfg2-cfg4 sizes.  usage: tools/r03_measure.sh OUTDIR [parts...]
 set -u
 OUT=$1; shift
+case $OUT in /*) ;; *) OUT=${GRAFT_REPO_ROOT:-$(pwd)}/$OUT ;; esac  # absolute: the profiler steps cd to /tmp
 PARTS=${*:-"early pack pool exact cli"}
 mkdir -p "$OUT"
 run() {  # name timeout cmd...
@@ -47,7 +48,7 @@ exactprof)  # kernel traces of the exact count, partitioned vs hash table, at cf
     done
   done ;;
 prof)  # PMC passes + kernel traces of the count kernel (device-resident), and a trace of the bench's stage
-  ( bash tools/pmc_passes.sh cfg2 r03_cfg2 ) > "$OUT/pmc_passes.log" 2>&1 || exit 4
+  ( bash tools/pmc_passes.sh cfg2 "$(basename "$OUT")_cfg2" ) > "$OUT/pmc_passes.log" 2>&1 || exit 4
   ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_bench" -o run -- \
     python3 "$GRAFT_REPO_ROOT/bench.py" --steps 100 --warmup 10 --no-cpu-baseline --no-pipelined --kernel-launches 100 ) \
     > "$OUT/prof_bench.log" 2>&1 || exit 5 ;;
