@@ -18,6 +18,7 @@
 #include <cstring>
 #include <string>
 #include <thread>
+#include <memory>
 #include <vector>
 
 #include "approx_counter_amd.h"
@@ -67,6 +68,9 @@ struct ac_ctx {
         uint32_t* acc = nullptr;
         uint32_t* tickets = nullptr;
         uint32_t acc_cap = 0, ticket_cap = 0;
+        // staged launches: per-chunk "copied" flags (= the launch's generation once in device memory)
+        uint32_t* stage_gen = nullptr;
+        uint32_t stage_gen_cap = 0;
     } sc[2 * AC_STAGE_MAX_PARTS];
     // streams of parts 1.. of a synchronous jobs call (part 0 runs on `stream`)
     // and of a submit (part 0 runs on the caller's stream), with the events that
@@ -257,6 +261,7 @@ struct StageLaunch {
     const uint8_t* src[AC_MAX_SEGS] = {};
     uint8_t* dst[AC_MAX_SEGS] = {};
     uint32_t chunks[AC_MAX_SEGS] = {};
+    uint32_t codes_off[AC_MAX_SEGS] = {};  // bytes of the region before its codes (the k-mers section)
     uint32_t* err_out = nullptr;  // device word the launch's error bits are also or-ed into (submits: ac_check)
 };
 
@@ -330,6 +335,7 @@ ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hi
             d.stage_src = stage->src[i];
             d.stage_dst = stage->dst[i];
             d.stage_chunks = stage->chunks[i];
+            d.stage_codes_off = stage->codes_off[i];
         }
         d.n_kmers = s.n_kmers;
         d.n_windows = s.sample.n_windows;
@@ -412,6 +418,23 @@ ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hi
     a.zero_count = sc.dirty[sc.bank ^ 1u];
     a.n_queues = std::max<uint32_t>(1, n_counters);
     if (stage) {
+        uint32_t total_chunks = 0;
+        for (uint32_t i = 0; i < n; ++i) total_chunks += stage->chunks[i];
+        if (total_chunks > sc.stage_gen_cap) {  // (zeroed once: generations are never 0)
+            if (sc.stage_gen) AC_HIP(ctx, hipFree(sc.stage_gen));
+            sc.stage_gen = nullptr;
+            sc.stage_gen_cap = 0;
+            const uint32_t cap = std::max<uint32_t>(total_chunks, 1024);
+            const size_t bytes = sizeof(uint32_t) * AC_QUEUE_LINE * (size_t)cap;  // one line per chunk flag
+            AC_HIP(ctx, hipMalloc(&sc.stage_gen, bytes));
+            AC_HIP(ctx, hipMemsetAsync(sc.stage_gen, 0, bytes, stream));
+            sc.stage_gen_cap = cap;
+        }
+        uint32_t off = 0;
+        for (uint32_t i = 0; i < n; ++i) {
+            a.seg[i].stage_gen = sc.stage_gen + (size_t)off * AC_QUEUE_LINE;
+            off += stage->chunks[i];
+        }
         a.staged = 1;
         a.gen = stage->gen;
         a.host_hdr = stage->host_hdr;
@@ -586,6 +609,7 @@ void ac_destroy(ac_ctx* ctx) {
         if (sc.queue) (void)hipFree(sc.queue);
         if (sc.acc) (void)hipFree(sc.acc);
         if (sc.tickets) (void)hipFree(sc.tickets);
+        if (sc.stage_gen) (void)hipFree(sc.stage_gen);
     }
     for (hipStream_t ps : ctx->part_stream)
         if (ps) (void)hipStreamDestroy(ps);
@@ -953,7 +977,9 @@ ac_status ac_exact_count_device(ac_ctx* ctx, uint32_t k, const ac_windows* dev, 
         if (ac_status s2 = grow(ctx, &ctx->e_buf[6], &ctx->e_cap[6], key_bytes * key_cap)) return s2;
         if (ac_status s2 = grow(ctx, &ctx->e_buf[7], &ctx->e_cap[7], key_bytes * key_cap)) return s2;
         if (ac_status s2 = grow(ctx, &ctx->e_buf[8], &ctx->e_cap[8], key_bytes * key_cap)) return s2;
-        if (ac_status s2 = grow(ctx, &ctx->e_buf[9], &ctx->e_cap[9], sizeof(uint32_t) * (h1 + h2 + S))) return s2;
+        const size_t slabs = (a.n_chunks + EXACT_SCAN_SLAB - 1) / EXACT_SCAN_SLAB;
+        if (ac_status s2 = grow(ctx, &ctx->e_buf[9], &ctx->e_cap[9], sizeof(uint32_t) * (h1 + h2 + S + slabs * S)))
+            return s2;
         if (ac_status s2 = grow(ctx, &ctx->e_buf[10], &ctx->e_cap[10], sizeof(uint32_t) * (NB + 1))) return s2;
         if (ac_status s2 = grow(ctx, &ctx->e_buf[11], &ctx->e_cap[11], sizeof(uint32_t) * NB * EXACT_PHIST)) return s2;
         a.phist = (uint32_t*)ctx->e_buf[11];
@@ -963,6 +989,7 @@ ac_status ac_exact_count_device(ac_ctx* ctx, uint32_t k, const ac_windows* dev, 
         a.h1 = (uint32_t*)ctx->e_buf[9];
         a.h2 = a.h1 + h1;
         a.stot = a.h2 + h2;
+        a.slab = a.stot + S;
         a.bstart = (uint32_t*)ctx->e_buf[10];
         AC_HIP(ctx, hipMemsetAsync(small, 0, small_bytes, st));
         AC_HIP(ctx, acamd::launch_exact_partitioned(a, st));
@@ -1541,6 +1568,8 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
         }
     }
     *(uint32_t*)(h + p.off_err) = 0u;
+    // (the early launch's header and buffer descriptors count a segment's bytes in 31 bits)
+    if (p.early && p.total >= (size_t(1) << 31)) p.early = false;
     // early launch: flags and the completion word cleared before the launch (the slot's last
     // launch has finished: its event was waited for above)
     const size_t hdr_bytes = sizeof(uint32_t) * AC_QUEUE_LINE * AC_HDR_LINES;
@@ -1622,6 +1651,7 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
             stg.src[j] = (const uint8_t*)(hd + p.off_kmers[j]);
             stg.dst[j] = (uint8_t*)(d + p.off_kmers[j]);
             stg.chunks[j] = j < pre ? 0u : (uint32_t)((region[j] + AC_STAGE_CHUNK - 1) / AC_STAGE_CHUNK);
+            stg.codes_off[j] = (uint32_t)(p.off_codes[j] - p.off_kmers[j]);
         }
         auto go = [&]() -> ac_status {
             ac_segment segs[AC_MAX_JOBS];
@@ -1633,13 +1663,27 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
             mark(4);
             return AC_OK;
         };
-        std::atomic<uint32_t> left[AC_MAX_JOBS];
-        for (uint32_t j = 0; j < AC_MAX_JOBS; ++j) left[j].store(0, std::memory_order_relaxed);
-        for (const Task& x : tasks) left[x.job].fetch_add(1, std::memory_order_relaxed);
+        // Progress records: the packed N-free prefix of each job's region (its k-mers, then the
+        // codes of its first tasks up to the first task holding an N), so the kernel moves chunks
+        // over PCIe -- and counts their windows -- while the rest of the job is packed.  Tasks are
+        // claimed in order but finish out of order; this thread alone publishes (a plain 8-byte
+        // store, read whole by the kernel's 16-byte header load): between the tasks it packs
+        // itself, it advances over the tasks the workers have finished.  (Publishing from the
+        // workers -- CAS on the one header line the GPU polls -- cost ~7 us of packing per call.)
+        struct alignas(64) Done {
+            std::atomic<uint32_t> v;
+        };
+        std::unique_ptr<Done[]> t_done(new Done[tasks.size() + 1]);
+        for (size_t t = 0; t < tasks.size(); ++t) t_done[t].v.store(0, std::memory_order_relaxed);
+        auto publish = [&](uint32_t j, uint64_t ready) {
+            __atomic_store_n((uint64_t*)(hdr + j * AC_QUEUE_LINE + AC_HDR_PGEN), (ready << 32) | p.gen, __ATOMIC_RELEASE);
+        };
         const std::function<void(uint32_t)> pack_counted = [&](uint32_t t) {
             pack(t);
-            left[tasks[t].job].fetch_sub(1, std::memory_order_release);
+            t_done[t].v.store(1, std::memory_order_release);
         };
+        // the k-mers are in place already (copied with the layout)
+        for (uint32_t j = 0; j < p.n; ++j) publish(j, p.off_codes[j] - p.off_kmers[j]);
         // the workers start packing job 0 while this thread launches the kernel
         pool.begin((uint32_t)tasks.size(), pack_counted);
         if (pre == 0)
@@ -1647,12 +1691,28 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
                 pool.finish();
                 return st;
             }
+        constexpr uint64_t PUBLISH_STEP = 16384;  // bytes of new prefix worth a header store
         uint32_t t0 = 0;
         for (uint32_t j = 0; j < p.n; ++j) {
             uint32_t t1 = t0;
             while (t1 < (uint32_t)tasks.size() && tasks[t1].job == j) ++t1;
-            pool.help(t1);
-            while (left[j].load(std::memory_order_acquire) != 0u) __builtin_ia32_pause();
+            const uint64_t base_off = p.off_codes[j] - p.off_kmers[j];
+            uint64_t ready = base_off, published = base_off;
+            bool n_seen = false;
+            uint32_t nt = t0, helped = t0;  // tasks [t0, nt) seen finished; [t0, helped) offered to this thread
+            while (nt < t1) {
+                if (helped < t1) pool.help(++helped);  // packs task helped - 1 unless a worker has it
+                while (nt < t1 && t_done[nt].v.load(std::memory_order_acquire)) {
+                    n_seen = n_seen || task_n[nt];
+                    if (!n_seen) ready = base_off + (tasks[nt].bases + tasks[nt].span) / 4;
+                    ++nt;
+                }
+                if (ready >= published + PUBLISH_STEP || (nt == t1 && ready > published)) {
+                    publish(j, ready);
+                    published = ready;
+                }
+                if (helped >= t1 && nt < t1) __builtin_ia32_pause();
+            }
             const bool nn = job_no_n(j);
             const size_t bytes = nn && ulen[j] != AC_NO_ULEN ? p.off_nmask[j] - p.off_kmers[j] : region[j];
             if (j < pre) {  // sent ahead of the launch, which follows it on the stream
@@ -1666,9 +1726,10 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
                 }
             } else {
                 uint32_t* line = hdr + j * AC_QUEUE_LINE;
-                line[AC_HDR_BYTES] = (uint32_t)bytes;
-                line[AC_HDR_HAS_N] = nn ? 0u : 1u;
-                line[AC_HDR_ABORT] = 0u;
+                // no N: the whole region is N-free (never below a prefix: the codes end inside the
+                // bytes sent); with N the published prefix stays where the first N stopped it
+                if (nn) publish(j, bytes);
+                line[AC_HDR_INFO] = (uint32_t)bytes | (nn ? 0u : AC_HDR_INFO_HAS_N);
                 // (test hook: AC_STAGE_TEST_UNFLAGGED=1 leaves the last job unflagged, so the kernel's bounded
                 // wait runs out and the call must fail cleanly: tests/test_gpu_jobs.py)
                 static const bool unflag = std::getenv("AC_STAGE_TEST_UNFLAGGED") != nullptr;

@@ -78,6 +78,7 @@ struct ExactArgs {
     uint32_t* h1;
     uint32_t* h2;
     uint32_t* stot;
+    uint32_t* slab;    // [slab][super]: h1's column sums over EXACT_SCAN_SLAB rows (the level-1 scan)
     uint32_t* bstart;  // nb + 1
     uint32_t nb_log2;
     uint32_t s_log2;    // super-buckets: nb_log2 - s_log2 <= 6
@@ -92,6 +93,7 @@ struct ExactArgs {
 
 #define EXACT_PHIST 32  // per-bucket partial histogram bins (counts 1..32; larger counts go straight to hist)
 
+#define EXACT_SCAN_SLAB 128   // level-1 histogram rows (chunks) per workgroup of the column scan
 #define EXACT_MAX_SUPER 1024  // level-1 super-buckets (at most): 2^16 buckets of <= 64 sub-buckets each
 #define EXACT_MAX_SUB 64     // buckets per super-bucket (at most)
 #define EXACT_BUCKET_SLOTS 4096  // LDS counting table of the per-bucket kernel (32 KB of keys + counts)

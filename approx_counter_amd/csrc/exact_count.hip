@@ -713,24 +713,62 @@ __global__ __launch_bounds__(EXACT_THREADS) void part_hist1_kernel(ExactArgs a) 
     for (uint32_t i = t; i < S; i += EXACT_THREADS) a.h1[(uint64_t)blockIdx.x * S + i] = h[i];
 }
 
-// Level 1, per super-bucket (one workgroup each): h1[.][s] -> each chunk's
-// offset inside super-bucket s; stot[s] = the super-bucket's size.
-__global__ __launch_bounds__(EXACT_THREADS) void part_scan1_kernel(ExactArgs a) {
-    __shared__ uint32_t wsum[EXACT_THREADS / 64];
-    const uint32_t S = 1u << a.s_log2, s = blockIdx.x, t = threadIdx.x;
-    const uint32_t per = (a.n_chunks + EXACT_THREADS - 1) / EXACT_THREADS;
-    const uint32_t r0 = min(a.n_chunks, t * per), r1 = min(a.n_chunks, r0 + per);
-    uint32_t local = 0;
-    for (uint32_t r = r0; r < r1; ++r) local += a.h1[(uint64_t)r * S + s];
-    uint32_t run;
-    const uint32_t total = block_excl_scan(local, run, wsum);
-    for (uint32_t r = r0; r < r1; ++r) {
-        uint32_t* c = &a.h1[(uint64_t)r * S + s];
-        const uint32_t x = *c;
-        *c = run;
-        run += x;
+// Level 1 column scan: h1[.][s] -> each chunk's offset inside super-bucket s,
+// stot[s] = the super-bucket's size.  A workgroup takes 32 super-buckets x one
+// slab of EXACT_SCAN_SLAB rows, so each row it reads is one 128-B line read by
+// one workgroup (one workgroup per column read every line 32 times: 487 us of a
+// 3.7 ms cfg4 exact count, profiles/r03_final/exact_cfg4_hash0.md).  Step 1: the
+// slabs' column sums.
+constexpr uint32_t SCAN_G = EXACT_THREADS / 32;              // row groups per workgroup
+constexpr uint32_t SCAN_RPG = EXACT_SCAN_SLAB / SCAN_G;      // rows per row group
+__global__ __launch_bounds__(EXACT_THREADS) void part_scan1a_kernel(ExactArgs a) {
+    __shared__ uint32_t part[SCAN_G][32];
+    const uint32_t S = 1u << a.s_log2, t = threadIdx.x, c = t & 31u, g = t >> 5;
+    const uint32_t s = blockIdx.x * 32u + c, slab = blockIdx.y;
+    const uint32_t r0 = slab * EXACT_SCAN_SLAB + g * SCAN_RPG;
+    uint32_t sum = 0;
+#pragma unroll 8
+    for (uint32_t i = 0; i < SCAN_RPG; ++i)
+        if (r0 + i < a.n_chunks) sum += a.h1[(uint64_t)(r0 + i) * S + s];
+    part[g][c] = sum;
+    __syncthreads();
+    if (g == 0) {
+        uint32_t tot = 0;
+        for (uint32_t q = 0; q < SCAN_G; ++q) tot += part[q][c];
+        a.slab[(uint64_t)slab * S + s] = tot;
     }
-    if (t == 0) a.stot[s] = total;
+}
+
+// Step 2: each slab's base (the earlier slabs' sums), then the exclusive scan of its rows.
+__global__ __launch_bounds__(EXACT_THREADS) void part_scan1b_kernel(ExactArgs a) {
+    __shared__ uint32_t part[SCAN_G][32];
+    const uint32_t S = 1u << a.s_log2, t = threadIdx.x, c = t & 31u, g = t >> 5;
+    const uint32_t s = blockIdx.x * 32u + c, slab = blockIdx.y;
+    uint32_t b = 0;
+    for (uint32_t q = g; q < slab; q += SCAN_G) b += a.slab[(uint64_t)q * S + s];
+    part[g][c] = b;
+    __syncthreads();
+    uint32_t base = 0;
+    for (uint32_t q = 0; q < SCAN_G; ++q) base += part[q][c];
+    const uint32_t r0 = slab * EXACT_SCAN_SLAB + g * SCAN_RPG;
+    uint32_t v[SCAN_RPG];
+    uint32_t local = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < SCAN_RPG; ++i) {
+        v[i] = r0 + i < a.n_chunks ? a.h1[(uint64_t)(r0 + i) * S + s] : 0u;
+        local += v[i];
+    }
+    __syncthreads();  // (part is reused)
+    part[g][c] = local;
+    __syncthreads();
+    uint32_t run = base;
+    for (uint32_t q = 0; q < g; ++q) run += part[q][c];
+#pragma unroll
+    for (uint32_t i = 0; i < SCAN_RPG; ++i) {
+        if (r0 + i < a.n_chunks) a.h1[(uint64_t)(r0 + i) * S + s] = run;
+        run += v[i];
+    }
+    if (slab + 1u == gridDim.y && g == SCAN_G - 1u) a.stot[s] = run;
 }
 
 // Every workgroup of the later steps rebuilds, from stot, the super-buckets'
@@ -1102,13 +1140,15 @@ hipError_t partitioned(const ExactArgs& a, hipStream_t stream) {
     if (a.nb_log2 < 6 || a.nb_log2 > MAX_NB_LOG2) return hipErrorInvalidValue;
     const uint32_t NB = 1u << a.nb_log2;
     const uint32_t S = 1u << a.s_log2;
-    if (a.s_log2 > a.nb_log2 || S > EXACT_MAX_SUPER || (NB >> a.s_log2) > EXACT_MAX_SUB || !a.n_chunks ||
+    if (a.s_log2 > a.nb_log2 || S > EXACT_MAX_SUPER || S < 32 || (NB >> a.s_log2) > EXACT_MAX_SUB || !a.n_chunks ||
         (uint64_t)a.n_chunks * CHUNK < a.key_cap || a.n_chunks2 < a.n_chunks + S)
         return hipErrorInvalidValue;
     const uint32_t wblocks = (a.n_windows + KEYS_WINDOWS - 1) / KEYS_WINDOWS;
     if (wblocks) hipLaunchKernelGGL(part_keys_kernel<K>, dim3(wblocks), dim3(EXACT_THREADS), 0, stream, a);
     hipLaunchKernelGGL(part_hist1_kernel<K>, dim3(a.n_chunks), dim3(EXACT_THREADS), 0, stream, a);
-    hipLaunchKernelGGL(part_scan1_kernel, dim3(S), dim3(EXACT_THREADS), 0, stream, a);
+    const uint32_t slabs = (a.n_chunks + EXACT_SCAN_SLAB - 1) / EXACT_SCAN_SLAB;
+    hipLaunchKernelGGL(part_scan1a_kernel, dim3(S / 32, slabs), dim3(EXACT_THREADS), 0, stream, a);
+    hipLaunchKernelGGL(part_scan1b_kernel, dim3(S / 32, slabs), dim3(EXACT_THREADS), 0, stream, a);
     hipLaunchKernelGGL(part_scatter1_kernel<K>, dim3(a.n_chunks), dim3(EXACT_THREADS), 0, stream, a);
     hipLaunchKernelGGL(part_hist2_kernel<K>, dim3(a.n_chunks2), dim3(EXACT_THREADS), 0, stream, a);
     hipLaunchKernelGGL(part_scan2_kernel<K>, dim3((S + EXACT_THREADS / 64 - 1) / (EXACT_THREADS / 64)),

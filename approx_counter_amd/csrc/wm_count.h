@@ -37,12 +37,16 @@ constexpr int waves_per_simd(int W) { return W == 2 ? 4 : 8; }
 
 // Staged launches ("early launch"): the count kernel is launched
 // before the host has packed its inputs and stages them itself.  Per segment,
-// the host writes one header line of the pinned staging block when the
-// segment's packed inputs are complete:
-#define AC_HDR_FLAG 0    // = the launch's generation once the rest is valid
-#define AC_HDR_BYTES 1   // bytes of the segment's region to copy (<= the launch's chunks x AC_STAGE_CHUNK)
-#define AC_HDR_HAS_N 2   // 0: the segment holds no N (its N bitmap was not copied)
-#define AC_HDR_ABORT 3   // nonzero: the host gave up on the call; the waves skip the segment
+// one header line of pinned host memory, read by the kernel with ONE 16-byte
+// load (words 0-3):
+#define AC_HDR_PGEN 0    // progress record, one 8-byte store {PGEN, READY}: valid when PGEN = the launch's generation
+#define AC_HDR_READY 1   //   bytes of the segment's region packed and free of N (a prefix: k-mers, then codes)
+#define AC_HDR_FLAG 2    // = generation once the segment is complete and INFO holds
+#define AC_HDR_INFO 3    //   its final byte count (<= the launch's chunks x AC_STAGE_CHUNK, a multiple of 256)
+                         //   | AC_HDR_INFO_HAS_N when it holds an N (its N bitmap sent), or AC_HDR_INFO_ABORT:
+                         //   the host gave up on the call (the waves skip the segment)
+#define AC_HDR_INFO_HAS_N 0x80000000u
+#define AC_HDR_INFO_ABORT 0xffffffffu
 // and the kernel's last workgroup writes the launch's result line (line AC_MAX_SEGS):
 #define AC_HDR_DONE 0    // = generation once every count of the launch is in host memory
 #define AC_HDR_ERR 1     // AC_DEVERR_* bits of the launch
@@ -53,12 +57,15 @@ constexpr int waves_per_simd(int W) { return W == 2 ? 4 : 8; }
 // launch's sub-queue counters in its queue bank (zeroed with them for the next
 // launch on that bank; only word 0 of a line is ever used, as the next launch
 // zeroes word 0 of each): groups done, error bits, then per segment: chunk
-// claims, the segment's header copy (verdict, bytes, seen: a line each),
-// AC_STAGE_REPL done replicas.
+// claims, the segment's final header (verdict, bytes, final seen),
+// AC_STAGE_REPL replicas of the N-free bytes available so far, AC_STAGE_REPL
+// done replicas (every workgroup polls one replica of each: ~1000 waves
+// polling one line slowed the chunk copies).
 #define AC_STAGE_L_GROUPS 0
 #define AC_STAGE_L_ERR 1
-#define AC_STAGE_L_SEG(s) (2 + (s) * (4 + AC_STAGE_REPL))
-#define AC_STAGE_LINES (2 + AC_MAX_SEGS * (4 + AC_STAGE_REPL))
+#define AC_STAGE_SEG_LINES (4 + 2 * AC_STAGE_REPL)
+#define AC_STAGE_L_SEG(s) (2 + (s) * AC_STAGE_SEG_LINES)
+#define AC_STAGE_LINES (2 + AC_MAX_SEGS * AC_STAGE_SEG_LINES)
 #define AC_STAGE_TIMEOUT_TICKS 50000000ull  // 0.5 s of s_memrealtime (100 MHz): every wait is bounded
 
 namespace acamd {
@@ -88,6 +95,8 @@ struct SegDev {
     const uint8_t* stage_src;
     uint8_t* stage_dst;
     uint32_t stage_chunks;
+    uint32_t stage_codes_off;  // bytes of the region before the codes (k-mers)
+    uint32_t* stage_gen;       // per chunk, one line each: = the launch's generation once copied (early counting)
 };
 
 struct LaunchArgs {

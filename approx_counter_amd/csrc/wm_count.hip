@@ -57,7 +57,7 @@ constexpr int WAVES_PER_BLOCK = AC_WAVES_PER_BLOCK;
 // computed from them.
 }  // namespace
 __device__ uint64_t g_stamps[1 << 21];
-__device__ uint64_t g_stage_stamps[64];  // per segment: [s*4] host flag seen by the poller, [s*4+1] its copy done
+__device__ uint64_t g_stage_stamps[64];  // per segment: [s*4] final header seen by the poller, [s*4+1] its first progress record, [s*4+2] last chunk in
 namespace {
 __device__ __forceinline__ void stamp(uint64_t wave, int i) {
     if ((threadIdx.x & 63u) == 0 && wave < (1u << 18)) {
@@ -211,8 +211,16 @@ __device__ __forceinline__ uint32_t tid_word(const Fetch& f, uint32_t lane) { re
 // start % 32 == 0 && length <= n_bases && start <= n_bases - length, on the
 // scalar unit (hipcc compares 64-bit values with VALU ops), written so that no
 // sum wraps: a start near 2^64 must not pass.
+template <bool RFL>
 __device__ __forceinline__ uint32_t window_valid(uint64_t base, uint32_t len, uint64_t nb) {
 #ifndef AC_VALU_VALID
+    // (RFL, the staged kernel: its early-counting gate leaves hipcc holding some of these
+    // wave-uniform values in VGPRs; readfirstlane puts them back in SGPRs for the asm)
+    const uint32_t nbl = RFL ? __builtin_amdgcn_readfirstlane((uint32_t)nb) : (uint32_t)nb;
+    const uint32_t nbh = RFL ? __builtin_amdgcn_readfirstlane((uint32_t)(nb >> 32)) : (uint32_t)(nb >> 32);
+    const uint32_t ln = RFL ? __builtin_amdgcn_readfirstlane(len) : len;
+    const uint32_t bl = RFL ? __builtin_amdgcn_readfirstlane((uint32_t)base) : (uint32_t)base;
+    const uint32_t bh = RFL ? __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32)) : (uint32_t)(base >> 32);
     uint32_t bad, t0, t1;
     asm("s_sub_u32 %[t0], %[nbl], %[len]\n\t"
         "s_subb_u32 %[t1], %[nbh], 0\n\t"  // scc: n_bases < length
@@ -223,8 +231,7 @@ __device__ __forceinline__ uint32_t window_valid(uint64_t base, uint32_t len, ui
         "s_and_b32 %[t0], %[bl], 31\n\t"  // scc: misaligned start
         "s_cselect_b32 %[bad], 1, %[bad]"
         : [bad] "=&s"(bad), [t0] "=&s"(t0), [t1] "=&s"(t1)
-        : [nbl] "s"((uint32_t)nb), [nbh] "s"((uint32_t)(nb >> 32)), [len] "s"(len), [bl] "s"((uint32_t)base),
-          [bh] "s"((uint32_t)(base >> 32))
+        : [nbl] "s"(nbl), [nbh] "s"(nbh), [len] "s"(ln), [bl] "s"(bl), [bh] "s"(bh)
         : "scc");
     return bad ^ 1u;
 #else
@@ -251,91 +258,141 @@ struct BlockLds {
 #endif
 
 // Staged launch ("early launch"): the kernel is launched before
-// the host has packed its inputs.  Wave 0 of every workgroup runs this before
-// anything reads the segment.  It claims AC_STAGE_CHUNK-byte chunks of the
-// segment's region (an agent-scope counter).  The wave that wins chunk 0 is the
-// segment's only host poller: it polls the host's flag (= gen, in the pinned
-// header line; system-scope loads, ~0.2 us apart), copies the header's size and
-// N verdict into the segment's device words and raises a device flag; the other
-// chunk winners wait on that device flag.  Each copies its chunks from the
-// pinned block to device memory with write-through (sc1) stores, waits for them
-// and adds 1 to every replica of the segment's done counter.  Every workgroup
-// then polls one replica until all chunks are in, and acquires.  The copied
-// lines were not in any L2 at launch start and are touched by no one before the
-// counter says so, so the readers' plain loads fetch them fresh (the hand-off
-// form of MI355X_MICROARCH.md's visibility section).  Every wait is bounded
+// the host has packed its inputs.  Wave 0 of every workgroup runs stage_copy
+// before the workgroup reads the segment.  It claims tickets of the segment (an
+// agent-scope counter): ticket 0 makes it the segment's only host poller,
+// ticket c >= 1 the copier of AC_STAGE_CHUNK-byte chunk c - 1 of the region.
+// The host packs the region front to back and publishes the packed N-free
+// prefix (progress record) as it grows, then the final byte count and N verdict
+// (flag).  The poller reads the header with one 16-byte system-scope load per
+// poll (~2 us apart: one PCIe round trip) and republishes it in device words:
+// the N-free bytes so far, then the final verdict, bytes and a final-seen word.
+// A copier waits (polling the device words) until its chunk lies inside the
+// N-free prefix -- so chunks cross PCIe while later ones are still being packed
+// -- or the final header is out; it copies the chunk from the pinned block to
+// device memory with write-through (sc1) stores, waits for them, stores the
+// launch's generation into the chunk's flag and adds 1 to every replica of the
+// segment's done counter.  Readers either wait for the done counter (the whole
+// segment, then its N verdict), or -- equal-window segments -- count a window
+// as soon as the chunks its fetches touch are flagged and lie in the N-free
+// prefix (stage_gate).  No acquire: the copied lines were not in any L2 at
+// launch start and are touched by no one before their flag says so (a fetch
+// never reaches past the chunks checked for it, and 128-B lines never straddle
+// chunks), so the readers' plain loads fetch them fresh (the hand-off form of
+// MI355X_MICROARCH.md's visibility section).  Every wait is bounded
 // (AC_STAGE_TIMEOUT_TICKS): a host that never flags makes the waves report
-// AC_DEVERR_STAGE and skip, never hang.  Returns the segment's has_n, or ~0u when
-// the segment is skipped (timeout, or the host's abort flag).
-__device__ __attribute__((noinline)) uint32_t stage_wait(const uint8_t* src, uint8_t* dst, uint32_t chunks,
-                                                         uint32_t* hdr, uint32_t* words, uint32_t gen, uint32_t* err,
-                                                         uint32_t replica, uint32_t si) {
-    const uint32_t lane = threadIdx.x & 63u;
+// AC_DEVERR_STAGE and skip, never hang.  (The chunk count covers the region's
+// largest layout, N bitmap included, so the last chunk always waits for the
+// final header: once the done counter is complete, the verdict words are written.)
+struct StageWords {
+    uint32_t* claim;
+    uint32_t* verdict;  // ~0u: skip; else 1 = has N
+    uint32_t* bytes;
+    uint32_t* fin;      // 1 once verdict / bytes are written
+    uint32_t* avail;    // N-free bytes of the region published so far: AC_STAGE_REPL replicas, one per line
+    uint32_t* done;     // chunks copied: AC_STAGE_REPL replicas, one per line
+};
+__device__ __forceinline__ StageWords stage_words(uint32_t* words) {
     // (one word per line: a launch zeroes only word 0 of each line of the next launch's bank)
-    uint32_t* claim = words;
-    uint32_t* verdict_w = words + AC_QUEUE_LINE;
-    uint32_t* bytes_w = words + 2 * AC_QUEUE_LINE;
-    uint32_t* seen_w = words + 3 * AC_QUEUE_LINE;
-    uint32_t* done = words + 4 * AC_QUEUE_LINE;
+    return StageWords{words, words + AC_QUEUE_LINE, words + 2 * AC_QUEUE_LINE, words + 3 * AC_QUEUE_LINE,
+                      words + 4 * AC_QUEUE_LINE, words + (4 + AC_STAGE_REPL) * AC_QUEUE_LINE};
+}
+// per chunk flag: one line each (a chunk's readers poll only its own line)
+__device__ __forceinline__ uint32_t* chunk_flag(uint32_t* chunk_gen, uint32_t x) { return chunk_gen + x * AC_QUEUE_LINE; }
+__device__ __forceinline__ const uint32_t* chunk_flag(const uint32_t* chunk_gen, uint32_t x) {
+    return chunk_gen + x * AC_QUEUE_LINE;
+}
+__device__ __forceinline__ uint32_t wave_load(const uint32_t* p) {  // lane 0's agent-scope load, wave-uniform
+    uint32_t v = 0;
+    if ((threadIdx.x & 63u) == 0) v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __builtin_amdgcn_readfirstlane(v);
+}
+__device__ __forceinline__ void wave_store(uint32_t* p, uint32_t v) {
+    if ((threadIdx.x & 63u) == 0) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool stage_late(uint64_t t0) {
+    return __builtin_amdgcn_s_memrealtime() - t0 > AC_STAGE_TIMEOUT_TICKS;
+}
+
+// Claims and serves tickets until none is left; false on timeout.
+__device__ __attribute__((noinline)) bool stage_copy(const uint8_t* src, uint8_t* dst, uint32_t chunks, uint32_t* hdr,
+                                                     uint32_t* words, uint32_t* chunk_gen, uint32_t gen, uint32_t si) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const StageWords sw = stage_words(words);
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    auto late = [&]() { return __builtin_amdgcn_s_memrealtime() - t0 > AC_STAGE_TIMEOUT_TICKS; };
-    auto load = [&](uint32_t* p, int scope) {
-        uint32_t v = 0;
-        if (lane == 0)
-            v = scope ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
-                      : __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return __builtin_amdgcn_readfirstlane(v);
-    };
-    bool ok = true, seen = false;
-    uint32_t bytes = 0, verdict = 0;
-    __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)src, 0, 0, 0x00020000);
-    __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)dst, 0, 0, 0x00020000);
     for (;;) {
         uint32_t c = 0;
-        if (lane == 0) c = __hip_atomic_fetch_add(claim, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) c = __hip_atomic_fetch_add(sw.claim, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         c = __builtin_amdgcn_readfirstlane(c);
-        if (c >= chunks) break;
-        if (!seen) {
-            if (c == 0) {  // the segment's host poller
-                while (load(hdr + AC_HDR_FLAG, 1) != gen) {
-                    if (late()) {
-                        ok = false;
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(8);
+        if (c > chunks) return true;
+        if (c == 0) {  // the segment's host poller
+            // The header's four words in ONE 16-byte system-scope load (one PCIe read): the host
+            // stores the progress record as one 8-byte store and the flag after INFO, so a read
+            // that returns the flag returns the INFO stored before it.
+            typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+            static_assert(AC_HDR_PGEN == 0 && AC_HDR_READY == 1 && AC_HDR_FLAG == 2 && AC_HDR_INFO == 3,
+                          "header layout");
+            const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc((void*)hdr, 0, 16, 0x00020000);
+            uint32_t published = 0;
+            for (;;) {
+                const v4u hv = __builtin_amdgcn_raw_buffer_load_b128(rh, 0, 0, 17);  // sc0 sc1: system scope
+                uint32_t ready = __builtin_amdgcn_readfirstlane(hv.x) == gen ? __builtin_amdgcn_readfirstlane(hv.y) : 0u;
+                const bool fin = __builtin_amdgcn_readfirstlane(hv.z) == gen;
+                uint32_t verdict = 0, bytes = 0;
+                if (fin) {
+                    const uint32_t info = __builtin_amdgcn_readfirstlane(hv.w);
+                    bytes = info & ~AC_HDR_INFO_HAS_N;
+                    verdict = (info == AC_HDR_INFO_ABORT || bytes > chunks * AC_STAGE_CHUNK || ready > bytes)
+                                  ? ~0u
+                                  : (info & AC_HDR_INFO_HAS_N ? 1u : 0u);
+                    if (verdict == 0u) ready = bytes;  // no N anywhere: the whole region is N-free
                 }
-                if (!ok) break;
-                stage_stamp(si, 0);
-                bytes = load(hdr + AC_HDR_BYTES, 1);
-                verdict = load(hdr + AC_HDR_ABORT, 1) ? ~0u : (load(hdr + AC_HDR_HAS_N, 1) ? 1u : 0u);
-                if (bytes > chunks * AC_STAGE_CHUNK) verdict = ~0u;  // a header the launch cannot hold: skip
-                if (lane == 0) {
-                    __hip_atomic_store(verdict_w, verdict, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(bytes_w, bytes, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (verdict != ~0u && ready > published && ready <= chunks * AC_STAGE_CHUNK) {
+                    if (published == 0) stage_stamp(si, 1);
+                    if (lane < AC_STAGE_REPL)  // every replica in one wave instruction
+                        __hip_atomic_store(sw.avail + lane * AC_QUEUE_LINE, ready, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                    published = ready;
                 }
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                if (lane == 0) __hip_atomic_store(seen_w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            } else {  // the other chunk winners wait for the poller's device flag
-                while (load(seen_w, 0) == 0u) {
-                    if (late()) {
-                        ok = false;
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(4);
+                if (fin) {
+                    stage_stamp(si, 0);
+                    wave_store(sw.verdict, verdict);
+                    wave_store(sw.bytes, verdict == ~0u ? 0u : bytes);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    wave_store(sw.fin, 1u);
+                    break;
                 }
-                if (!ok) break;
-                verdict = load(verdict_w, 0);
-                bytes = load(bytes_w, 0);
+                if (stage_late(t0)) return false;
+                __builtin_amdgcn_s_sleep(8);
             }
-            // range-checked descriptors: bytes past the region read as 0 and are not stored
-            rs = __builtin_amdgcn_make_buffer_rsrc((void*)src, 0, (int)bytes, 0x00020000);
-            rd = __builtin_amdgcn_make_buffer_rsrc((void*)dst, 0, (int)bytes, 0x00020000);
-            seen = true;
+            continue;
         }
-        if (verdict != ~0u) {
+        // copier of chunk c - 1: wait until it lies inside the N-free prefix or the segment is final
+        const uint32_t x = c - 1u, lo = x * AC_STAGE_CHUNK, hi = lo + AC_STAGE_CHUNK;
+        uint32_t* my_avail = sw.avail + (x % AC_STAGE_REPL) * AC_QUEUE_LINE;
+        uint32_t limit = 0;  // bytes of the region known to be valid
+        for (;;) {
+            // both words in one wave instruction (lane 0: N-free bytes, lane 1: final seen)
+            uint32_t v = 0;
+            if (lane < 2u) v = __hip_atomic_load(lane ? sw.fin : my_avail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (__builtin_amdgcn_readlane(v, 0) >= hi) {
+                limit = hi;
+                break;
+            }
+            if (__builtin_amdgcn_readlane(v, 1)) {
+                limit = wave_load(sw.verdict) == ~0u ? 0u : wave_load(sw.bytes);
+                break;
+            }
+            if (stage_late(t0)) return false;
+            __builtin_amdgcn_s_sleep(8);
+        }
+        if (limit > lo) {
+            // range-checked descriptors: bytes past the valid prefix read as 0 and are not stored
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)src, 0, (int)limit, 0x00020000);
+            const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)dst, 0, (int)limit, 0x00020000);
             typedef uint32_t v4u __attribute__((ext_vector_type(4)));
             v4u v[4];
-            const uint32_t o = c * AC_STAGE_CHUNK + lane * 16u;
+            const uint32_t o = lo + lane * 16u;
 #pragma unroll
             // (nontemporal, like the copy kernel's loads of the same pinned block: nothing read these
             // lines before the flag in this launch, so no cache holds them; system-scope loads
@@ -345,22 +402,25 @@ __device__ __attribute__((noinline)) uint32_t stage_wait(const uint8_t* src, uin
             for (int u = 0; u < 4; ++u) __builtin_amdgcn_raw_buffer_store_b128(v[u], rd, o + u * 1024u, 0, 16);  // sc1
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (c == 0) stage_stamp(si, 1);
+        wave_store(chunk_flag(chunk_gen, x), gen);
         uint32_t prev = 0;
         if (lane < AC_STAGE_REPL)
-            prev = __hip_atomic_fetch_add(done + lane * AC_QUEUE_LINE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            prev = __hip_atomic_fetch_add(sw.done + lane * AC_QUEUE_LINE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (__builtin_amdgcn_readfirstlane(prev) + 1u == chunks) stage_stamp(si, 2);  // (diagnostic builds) last chunk in
     }
-    while (ok && load(done + replica * AC_QUEUE_LINE, 0) < chunks) {
-        if (late()) {
-            ok = false;
-            break;
+}
+
+// Waits for the whole segment (every chunk copied): its N verdict (0 / 1), or ~0u to skip it.
+__device__ __attribute__((noinline)) uint32_t stage_wait_all(uint32_t* words, uint32_t chunks, uint32_t replica,
+                                                             uint32_t* err) {
+    const StageWords sw = stage_words(words);
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (wave_load(sw.done + replica * AC_QUEUE_LINE) < chunks) {
+        if (stage_late(t0)) {
+            if ((threadIdx.x & 63u) == 0) atomicOr(err, AC_DEVERR_STAGE);
+            return ~0u;
         }
-        __builtin_amdgcn_s_sleep(8);
-    }
-    if (!ok) {
-        if (lane == 0) atomicOr(err, AC_DEVERR_STAGE);
-        return ~0u;
+        __builtin_amdgcn_s_sleep(16);
     }
     // No acquire fence: it would only invalidate this CU's L1, and no CU can hold a line of the
     // region (nothing reads it before the counter says it is complete, and a launch starts with
@@ -371,7 +431,44 @@ __device__ __attribute__((noinline)) uint32_t stage_wait(const uint8_t* src, uin
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
-    return load(verdict_w, 0);
+    return wave_load(sw.verdict);
+}
+
+#ifndef AC_GATE_SLEEP
+#define AC_GATE_SLEEP 12  // s_sleep units (64 clocks) between a gate's polls
+#endif
+// Early counting: waits until region bytes [r0, r1) are in device memory (their chunks flagged)
+// and inside the N-free prefix, or until the whole segment is in.  Low word: 2 for "count it
+// with an all-zero N bitmap" (high word: the end of the chunks checked, in chunks), the
+// segment's verdict (0 / 1) once it is complete, ~0u to skip (timeout: error bit set).
+__device__ __forceinline__ uint64_t stage_gate(uint32_t* words, const uint32_t* chunk_gen, uint32_t chunks,
+                                                         uint32_t replica, uint32_t gen, uint32_t r0, uint32_t r1,
+                                                         uint32_t* err) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const StageWords sw = stage_words(words);
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    const uint32_t x0 = r0 / AC_STAGE_CHUNK, x1 = (r1 - 1u) / AC_STAGE_CHUNK;
+    // (more chunks than lanes, or past the launch's chunks: wait for the whole segment)
+    const uint32_t nx = (x1 < chunks && x1 - x0 < 62u) ? x1 - x0 + 1u : 0u;
+    bool in_prefix = false;  // the N-free prefix covers [r0, r1) (it only grows)
+    for (;;) {
+        // one wave instruction: lane 0 the done count, lane 1 the N-free bytes (this workgroup's
+        // replicas), lanes 2.. the chunks' flags once the prefix covers them
+        const uint32_t* p = lane == 0u ? sw.done + replica * AC_QUEUE_LINE
+                          : lane == 1u ? sw.avail + replica * AC_QUEUE_LINE
+                                       : (in_prefix && lane - 2u < nx ? chunk_flag(chunk_gen, x0 + (lane - 2u)) : nullptr);
+        uint32_t v = 0;
+        if (p) v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__builtin_amdgcn_readlane(v, 0) >= chunks) return wave_load(sw.verdict);
+        const uint64_t miss = __ballot(lane >= 2u && lane - 2u < nx && v != gen);
+        if (in_prefix && miss == 0) return ((uint64_t)(x1 + 1u) << 32) | 2u;
+        in_prefix = nx && __builtin_amdgcn_readlane(v, 1) >= r1;
+        if (stage_late(t0)) {
+            if (lane == 0) atomicOr(err, AC_DEVERR_STAGE);
+            return ~0u;
+        }
+        if (!in_prefix) __builtin_amdgcn_s_sleep(AC_GATE_SLEEP);
+    }
 }
 
 // The NFA blocks over the wave's W lane-word states (two words: the generated
@@ -472,19 +569,37 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
     // workgroup's other waves wait at a barrier, then everyone reads the verdict from LDS.
     uint32_t has_n = sg.has_n;
     bool skip = false;
+    // Early counting (staged, equal windows): `partial` while the segment is not known complete;
+    // a window is then fetched only once stage_gate has seen the chunks its fetches touch in
+    // device memory and inside the N-free prefix ([v_lo, v_hi): chunks already checked), and
+    // counted with an all-zero N bitmap.
+    bool partial = false;
+    uint32_t v_lo = 0, v_hi = 0;
+    uint32_t* st_words = nullptr;
     if (STAGED && sg.stage_chunks) {  // (a segment sent ahead of a staged launch has no chunks)
+        st_words = a.stage + AC_STAGE_L_SEG(si) * AC_QUEUE_LINE;
         if (wib == 0) {
-            const uint32_t r = stage_wait(sg.stage_src, sg.stage_dst, sg.stage_chunks,
-                                          a.host_hdr + (uint32_t)si * AC_QUEUE_LINE,
-                                          a.stage + AC_STAGE_L_SEG(si) * AC_QUEUE_LINE, a.gen, a.err,
-                                          blockIdx.x % AC_STAGE_REPL, (uint32_t)si);
+            uint32_t r = ~0u;
+            if (!__builtin_amdgcn_readfirstlane(
+                    (uint32_t)stage_copy(sg.stage_src, sg.stage_dst, sg.stage_chunks,
+                                         a.host_hdr + (uint32_t)si * AC_QUEUE_LINE, st_words, sg.stage_gen, a.gen,
+                                         (uint32_t)si))) {
+                if (lane == 0) atomicOr(a.err, AC_DEVERR_STAGE);
+            } else if (sg.ulen != AC_NO_ULEN && sg.n_kmers) {
+                // only the k-mers (the ~Eq table) are needed before counting starts
+                r = (uint32_t)stage_gate(st_words, sg.stage_gen, sg.stage_chunks, blockIdx.x % AC_STAGE_REPL, a.gen, 0u,
+                                         8u * sg.n_kmers, a.err);
+            } else {
+                r = stage_wait_all(st_words, sg.stage_chunks, blockIdx.x % AC_STAGE_REPL, a.err);
+            }
             if (lane == 0) lds.stage_r = r;
             stamp(wave, 7);  // diagnostic builds (staged): the staging wait is over
         }
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         const uint32_t r = __builtin_amdgcn_readfirstlane(lds.stage_r);
         skip = r == ~0u;
-        has_n = skip ? 0u : r;
+        partial = r == 2u;
+        has_n = (skip || partial) ? 0u : r;
     }
     const uint32_t* codes_p = sg.codes;
     const uint32_t* nmask_p = sg.nmask;
@@ -574,27 +689,33 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
         const uint32_t qb = qq / WAVES_PER_BLOCK;  // one wave of every workgroup dealt to block-queue qb
         return wgs_of(qb);
     };
-#ifndef AC_STRIDED_ITEMS
     // Sub-queue jj holds the contiguous items [first(jj), first(jj) + n_in(jj)):
     // a workgroup's sub-queues are consecutive and its XCD is fixed, so each
     // XCD's L2 fetches a slice of the sample instead of all of it, and
     // neighbouring windows (which share cache lines) are counted together.
-    const uint32_t q_items = n_items / S, r_items = n_items % S;
-    auto n_in = [&](uint32_t jj) { return q_items + (jj < r_items ? 1u : 0u); };
-    auto first_of = [&](uint32_t jj) { return jj * q_items + min(jj, r_items); };
-#else  // A/B: item jj + c*S in sub-queue jj
-    auto n_in = [&](uint32_t jj) { return jj < n_items ? (n_items - jj + S - 1u) / S : 0u; };
+    // Staged launches (early counting) stride instead -- item jj + c*S in
+    // sub-queue jj -- so the waves' first items are the image's first windows,
+    // the ones that arrive first, and the waves move through the image as it
+    // arrives (AC_STRIDED_ITEMS / AC_CONTIG_ITEMS: one form for every launch, A/B switches).
+    constexpr bool STRIDED =
+#if defined(AC_STRIDED_ITEMS)
+        true;
+#elif defined(AC_CONTIG_ITEMS)  // A/B: contiguous for every launch
+        false;
+#else
+        STAGED;
 #endif
+    const uint32_t q_items = n_items / S, r_items = n_items % S;
+    auto n_in = [&](uint32_t jj) {
+        return STRIDED ? (jj < n_items ? (n_items - jj + S - 1u) / S : 0u) : q_items + (jj < r_items ? 1u : 0u);
+    };
+    auto first_of = [&](uint32_t jj) { return STRIDED ? 0u : jj * q_items + min(jj, r_items); };
     // Per-sub-queue constants of the served sub-queue, recomputed only when a
     // steal changes it (their divisions are SALU sequences; with 1-window items
     // they ran once per window).
     uint32_t jc_waves = waves_in(jc), jc_items = n_in(jc);
-#ifndef AC_STRIDED_ITEMS
     uint32_t jc_first = first_of(jc);
-    auto item_of = [&](uint32_t c) { return c < jc_items ? jc_first + c : n_items; };
-#else
-    auto item_of = [&](uint32_t c) { return c < jc_items ? jc + c * S : n_items; };
-#endif
+    auto item_of = [&](uint32_t c) { return c < jc_items ? (STRIDED ? jc + c * S : jc_first + c) : n_items; };
     auto dequeue_issue = [&]() -> uint32_t {  // lane 0 holds the result; read with readfirstlane
         uint32_t v = 0;
         if (lane == 0) v = __hip_atomic_fetch_add(counter(jc), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -625,9 +746,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
             jc = jj;
             jc_waves = waves_in(jj);
             jc_items = n_in(jj);
-#ifndef AC_STRIDED_ITEMS
             jc_first = first_of(jj);
-#endif
             const uint32_t c = jc_waves + __builtin_amdgcn_readfirstlane(dequeue_issue());
             if (c < jc_items) return item_of(c);
         }
@@ -638,16 +757,50 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
 
     // Window pipeline: the next window's first segment is fetched while the current one is counted.
     // (written so that no sum wraps: a start near 2^64 must not pass)
-    auto valid = [&](uint64_t base, uint32_t len) { return window_valid(base, len, g_nbases) != 0u; };
+    auto valid = [&](uint64_t base, uint32_t len) { return window_valid<STAGED>(base, len, g_nbases) != 0u; };
     // an empty window reads no word (its start may be the image's end)
     auto fetchable = [&](uint64_t base, uint32_t len) { return len != 0u && valid(base, len); };
+    // Staged early counting: before a window's first fetch, make sure every byte its fetches read
+    // (256 bases per fetch from `base`, up to the image end) is in; false = skip the segment.
+    auto gate = [&](uint64_t base, uint32_t len) __attribute__((always_inline)) {
+        if constexpr (STAGED) {
+            if (!partial) return true;
+            const uint64_t end = min(base + (((uint64_t)len + 255u) & ~255ull), g_nbases);
+            const uint32_t r0 = sg.stage_codes_off + (uint32_t)(base >> 2);
+            const uint32_t r1 = sg.stage_codes_off + (uint32_t)(end >> 2);
+            if (r0 >= v_lo && r1 <= v_hi) return true;
+            // (a call's results come back in VGPRs: made wave-uniform again, or everything they
+            // touch -- the item cursor, window bases -- would turn divergent)
+            const uint64_t g = stage_gate(st_words, sg.stage_gen, sg.stage_chunks, blockIdx.x % AC_STAGE_REPL, a.gen,
+                                          r0, r1, a.err);
+            const uint32_t r = __builtin_amdgcn_readfirstlane((uint32_t)g);
+            if (r == 2u) {
+                v_lo = (r0 / AC_STAGE_CHUNK) * AC_STAGE_CHUNK;
+                v_hi = __builtin_amdgcn_readfirstlane((uint32_t)(g >> 32)) * AC_STAGE_CHUNK;
+                return true;
+            }
+            partial = false;
+            if (r == ~0u) return false;
+            // complete: from here on the segment's own N bitmap (if it has one)
+            has_n = r;
+            nmask_bytes = has_n ? (uint32_t)(g_nbases >> 3) : 0u;
+            im.nmask = __builtin_amdgcn_make_buffer_rsrc((void*)nmask_p, 0, (int)nmask_bytes, 0x00020000);
+            return true;
+        } else {
+            (void)base;
+            (void)len;
+            return true;
+        }
+    };
     uint64_t nbase = 0;
     uint32_t nlen = 0;
     Fetch nf = {0u, 0u};
     const uint32_t lane_off = (lane < 16u ? lane : (lane - 16u) & 7u) << 2;  // this lane's word of a segment, in bytes
     if (item < n_items) {
         desc(w, nbase, nlen);
-        if (fetchable(nbase, nlen)) tid_fetch(nf, im, nbase, lane, lane_off);
+        // (staged: after the table barrier -- a wave waiting for its first window must not hold
+        // its workgroup's other waves at the barrier)
+        if (!STAGED && fetchable(nbase, nlen)) tid_fetch(nf, im, nbase, lane, lane_off);
     }
 
     // ~Eq table, built by wave 0 of the workgroup (the waves share the
@@ -679,6 +832,12 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
     if (!STAGED) stamp(wave, 7);  // diagnostic builds: the wave's own prologue done, before the barrier
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     stamp(wave, 1);
+    bool stage_ok = true;
+    if (STAGED && item < n_items && fetchable(nbase, nlen)) {
+        stage_ok = gate(nbase, nlen);
+        if (stage_ok) tid_fetch(nf, im, nbase, lane, lane_off);
+    }
+    if (!stage_ok) item = n_items;
 
     // Per window, the next window's three dependent global accesses (for an
     // item's last window: claim -> descriptor -> first words; otherwise
@@ -731,12 +890,15 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
                 desc(nitem * chunk, nbase, nlen);
             }
         } else if (fetchable(nbase, nlen)) {
-            tid_fetch(nf, im, nbase, lane, lane_off);
+            if (gate(nbase, nlen)) tid_fetch(nf, im, nbase, lane, lane_off);
+            else stage_ok = false;
         }
         // step 2 (after block 1): the next item's first words
         if (nfull0 >= 4u) block32(f0, 2u);
-        if (last && nitem < n_items && fetchable(nbase, nlen))
-            tid_fetch(nf, im, nbase, lane, lane_off);
+        if (last && nitem < n_items && fetchable(nbase, nlen)) {
+            if (gate(nbase, nlen)) tid_fetch(nf, im, nbase, lane, lane_off);
+            else stage_ok = false;
+        }
         if (ok) {
             auto segment = [&](uint32_t f, uint32_t sb, uint32_t ch) __attribute__((always_inline)) {
                 const uint32_t nb = min(SEG, len - sb);
@@ -777,8 +939,10 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
                 item = __builtin_amdgcn_readfirstlane(steal());
                 if (item < n_items) {
                     desc(item * chunk, nbase, nlen);
-                    if (fetchable(nbase, nlen))
-                        tid_fetch(nf, im, nbase, lane, lane_off);
+                    if (fetchable(nbase, nlen)) {
+                        if (gate(nbase, nlen)) tid_fetch(nf, im, nbase, lane, lane_off);
+                        else stage_ok = false;
+                    }
                 }
             }
             if (item < n_items) {
@@ -786,6 +950,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
                 item_end = min(sg.n_windows, w + chunk);
             }
         }
+        if (STAGED && !stage_ok) break;  // the segment is skipped (the error word says so)
     }
 
     stamp(wave, 2);

@@ -222,24 +222,45 @@ def test_multi_context_shuffled_overlapping_windows():
             assert np.array_equal(multi.count(16, kmers, shuffled), exp), shards
 
 
+def _late_n(wins, frac):
+    """The windows with N only in the last `frac` of them (the early-counting prefix stops there)."""
+    out = [w.replace("N", "A") for w in wins]
+    for i in range(int(len(out) * (1 - frac)), len(out)):
+        if len(out[i]) > 3:
+            out[i] = out[i][:2] + "N" + out[i][3:]
+    return out
+
+
 def early_rotation(calls=30):
-    """Rotates three different workloads (different sizes, N / no N, equal / ragged windows,
-    1-3 jobs) through one context's early-launch stage; every call checked."""
+    """Rotates different workloads (sizes, N / no N, equal / ragged windows, 1-3 jobs) through
+    one context's early-launch stage; every call checked.  Equal-window jobs are counted while
+    they arrive (windows gated chunk by chunk): among them jobs whose N sit only in the last
+    windows or only in the first, windows longer than one 256-base fetch, and k-mer sets that
+    span several staging chunks."""
     rng = np.random.default_rng(5)
     work = []
-    for seed, (nw, lens, p_n, n_jobs) in enumerate([(900, (100, 100), 0.0, 2), (2500, (0, 150), 0.02, 3),
-                                                      (400, (101, 101), 0.01, 1)]):
+    for seed, (nw, lens, p_n, n_jobs, n_k, shape) in enumerate([
+            (900, (100, 100), 0.0, 2, None, None), (2500, (0, 150), 0.02, 3, None, None),
+            (400, (101, 101), 0.01, 1, None, None), (6000, (100, 100), 0.0, 2, 1500, "late_n"),
+            (3000, (101, 101), 0.0, 1, None, "first_n"), (700, (600, 600), 0.0, 2, 700, None)]):
         jobs, exp = [], []
         for j in range(n_jobs):
-            km, wins = cases.planted_case(300 + 10 * seed + j, 16, int(rng.integers(60, 400)), nw, win_len=lens,
-                                          p_n=p_n)
+            km, wins = cases.planted_case(300 + 10 * seed + j, 16, n_k or int(rng.integers(60, 400)), nw,
+                                          win_len=lens, p_n=p_n)
+            if lens[0] == lens[1]:  # truly equal windows (a planted candidate may have grown one)
+                wins = [(w + "A" * lens[0])[: lens[0]] for w in wins]
+            if shape == "late_n":
+                wins = _late_n(wins, 0.02)
+            elif shape == "first_n":
+                wins = list(wins)
+                wins[0] = "N" + wins[0][1:]
             jobs.append((km, ac.Dna5Sample.from_windows(wins)))
             exp.append(oracle.count_myers(16, km, wins))
         work.append((ac.Jobs(jobs), exp))
     c = ac.ApproxCounter(0)
     try:
         for i in range(calls):
-            jobs, exp = work[i % 3]
+            jobs, exp = work[i % len(work)]
             got = c.count_jobs(16, jobs)
             assert c.stage_mode() == 2, c.stage_mode()
             for g, e in zip(got, exp):
@@ -258,7 +279,7 @@ def test_early_launch_rotating_inputs_bit_exact(mode):
     that last held other data: any stale line read or early completion shows up as a wrong
     count.  In a child process per mode (AC_STAGE_EARLY is read once per process)."""
     env = dict(os.environ, AC_STAGE_EARLY=mode, PYTHONPATH=ROOT)
-    code = "from tests.test_gpu_jobs import early_rotation; early_rotation(45); print('OK')"
+    code = "from tests.test_gpu_jobs import early_rotation; early_rotation(48); print('OK')"
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=200, cwd=ROOT)
     assert r.returncode == 0 and "OK" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])
 

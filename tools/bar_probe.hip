@@ -12,6 +12,7 @@
 #include <signal.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -37,12 +38,15 @@ static void on_segv(int) {
     _exit(3);
 }
 
-// mode 0: plain loads; 1: system-scope acquire fence after the flag; 2: nontemporal loads
+// mode 0: plain loads; 1: system-scope acquire fence after the flag; 2: nontemporal loads (modes 0-2
+// read the region before waiting, so their L2 holds the old lines); 3: plain loads, no read of the
+// region in this launch before the flag (an earlier launch read it) -- the early-launch stage's case
 __global__ void check_kernel(const uint32_t* buf, uint32_t n, const uint32_t* flag, uint32_t want, uint32_t* bad,
                              uint32_t* seen_ticks, int mode) {
     const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
     uint32_t sink = 0;
-    for (uint32_t i = i0; i < n; i += stride) sink += buf[i];  // pull the old lines into L2 / L1
+    if (mode != 3)
+        for (uint32_t i = i0; i < n; i += stride) sink += buf[i];  // pull the old lines into L2 / L1
     if (sink == 0xfffffffeu) bad[1] = sink;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     uint32_t f = 0;
@@ -119,6 +123,39 @@ int main() {
         std::printf("host write %zu KB into device memory, %d thread(s): p50 %.1f us (%.1f GB/s), p10 %.1f us\n",
                     WORDS * 4 / 1024, threads, t[t.size() / 2], WORDS * 4 / t[t.size() / 2] / 1e3, t[t.size() / 10]);
     }
+    {  // persistent threads (no spawn inside the timed region), 1-16 writers, 64-B streaming stores
+        for (int threads : {1, 2, 4, 8, 12}) {
+            std::atomic<int> go{0}, done{0};
+            std::atomic<bool> quit{false};
+            std::vector<std::thread> th;
+            for (int q = 0; q < threads; ++q)
+                th.emplace_back([&, q] {
+                    int seen = 0;
+                    for (;;) {
+                        int g;
+                        while ((g = go.load(std::memory_order_acquire)) == seen)
+                            if (quit.load(std::memory_order_relaxed)) return;
+                        seen = g;
+                        host_fill(fg, (uint32_t)g, WORDS * q / threads, WORDS * (q + 1) / threads);
+                        done.fetch_add(1, std::memory_order_acq_rel);
+                    }
+                });
+            std::vector<double> t;
+            for (int r = 1; r <= 60; ++r) {
+                done.store(0);
+                const double a = now_us();
+                go.store(r, std::memory_order_release);
+                while (done.load(std::memory_order_acquire) != threads) {}
+                t.push_back(now_us() - a);
+            }
+            quit.store(true);
+            for (auto& x : th) x.join();
+            std::sort(t.begin() + 10, t.end());
+            const double p50 = t[10 + (t.size() - 10) / 2];
+            std::printf("persistent writers: %2d thread(s), %zu KB into device memory: p50 %.1f us (%.1f GB/s), best %.1f us\n",
+                        threads, WORDS * 4 / 1024, p50, WORDS * 4 / p50 / 1e3, t[10]);
+        }
+    }
     {  // the same into pinned host memory, for scale
         uint32_t* hp = nullptr;
         CK(hipHostMalloc((void**)&hp, WORDS * 4, hipHostMallocDefault));
@@ -137,15 +174,17 @@ int main() {
     hipStream_t s;
     CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     uint32_t* ticks = bad + 16;
-    for (int mode = 0; mode < 3; ++mode) {
+    for (int mode = 0; mode < 4; ++mode) {
         uint32_t total_bad = 0, timeouts = 0;
         double tick_sum = 0;
-        const int iters = 200;
+        const int iters = mode == 3 ? 1000 : 200;
         for (int it = 1; it <= iters; ++it) {
             const uint32_t want = (uint32_t)(mode * 100000 + it * 1000);
             __atomic_store_n(bad, 0u, __ATOMIC_RELEASE);
             __atomic_store_n(bad + 2, 0u, __ATOMIC_RELEASE);
             __atomic_store_n(flag, 0u, __ATOMIC_RELEASE);
+            if (mode == 3)  // the lines pulled into L2 by an earlier launch; the checking launch reads only after the flag
+                hipLaunchKernelGGL(read_kernel, dim3(512), dim3(256), 0, s, fg, (uint32_t)WORDS, 2u, bad_d + 32);
             hipLaunchKernelGGL(check_kernel, dim3(512), dim3(256), 0, s, fg, (uint32_t)WORDS, flag_d, want, bad_d,
                                ticks, mode);
             CK(hipGetLastError());
@@ -161,7 +200,7 @@ int main() {
             tick_sum += __atomic_load_n(ticks, __ATOMIC_ACQUIRE);
         }
         std::printf("visibility mode %d (%s): %u stale words over %d iterations, %u timeouts, flag wait %.1f us avg\n",
-                    mode, mode == 0 ? "plain loads" : mode == 1 ? "system acquire" : "nontemporal loads", total_bad,
+                    mode, mode == 0 ? "plain loads" : mode == 1 ? "system acquire" : mode == 2 ? "nontemporal loads" : "no read before the flag in this launch, plain loads", total_bad,
                     iters, timeouts, tick_sum / iters / 100.0);
     }
 

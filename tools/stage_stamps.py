@@ -5,7 +5,8 @@
     APPROX_COUNTER_AMD_LIB=build/var/stamps/libapprox_counter_amd.so python tools/stage_stamps.py [--sn N]
 
 Per segment (read end), in us relative to the first wave's entry: when the segment's
-host poller saw the host's flag, when its own chunk was copied, and the spread of wave
+host poller saw the host's first progress record and its final header, when the last
+chunk was in device memory, and the spread of wave
 entry, counting start (after the staging wait and the table barrier), counting end and
 exit.  No output value is computed from the stamps."""
 import argparse
@@ -53,8 +54,8 @@ def main():
         print("                          p0      p10     p50     p90    p100  (us)")
         for s in np.unique(seg):
             m = seg == s
-            print(f" seg {s}: flag seen {(stage[4 * s] - t0) / 100:7.1f}, poller's copy done "
-                  f"{(stage[4 * s + 1] - t0) / 100:7.1f}, last chunk in {(stage[4 * s + 2] - t0) / 100:7.1f}")
+            print(f" seg {s}: first progress seen {(stage[4 * s + 1] - t0) / 100:7.1f}, final header seen "
+                  f"{(stage[4 * s] - t0) / 100:7.1f}, last chunk in {(stage[4 * s + 2] - t0) / 100:7.1f}")
             print("   entry           ", pct(us[m, 0]))
             wait_end = (raw[:, 7] - t0) / 100.0
             w0 = m & (np.arange(n) % 4 == 0)
