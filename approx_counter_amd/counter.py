@@ -56,6 +56,21 @@ class PackedSample:
                          _ptr(self.start, ctypes.c_uint64), _ptr(self.length, ctypes.c_uint32),
                          self.n_windows, self.n_bases)
 
+    def equal_window_len(self):
+        """The common window length when every window has it and window w starts at base
+        w * ceil32(length) (the layout ac_error_count_device_equal reads without descriptors),
+        else None."""
+        n = self.n_windows
+        if n == 0:
+            return None
+        ln = int(self.length[0])
+        stride = (ln + 31) // 32 * 32
+        if not np.all(self.length == ln):
+            return None
+        if not np.array_equal(self.start, np.arange(n, dtype=np.uint64) * np.uint64(stride)):
+            return None
+        return ln
+
 
 def pack_windows(windows) -> PackedSample:
     """Pack Dna5 windows into the 2-bit + N-mask image with ac_pack_windows.
@@ -329,12 +344,23 @@ class ApproxCounter:
         count_device (saves the per-call ctypes marshalling in launch loops)."""
         return (ACSegment * len(segments))(*[s.as_struct() for s in segments])
 
-    def count_device(self, k: int, segments, stream=None, accumulate: bool = False) -> None:
+    def count_device(self, k: int, segments, stream=None, accumulate: bool = False, window_len=None) -> None:
         """ac_error_count_device over DeviceSegment objects, or an array from
-        segment_array (asynchronous)."""
+        segment_array (asynchronous).  window_len (one per segment): the samples'
+        windows all have that length and sit back to back at ceil32 strides
+        (ac_error_count_device_equal; start / length are not read)."""
         arr = segments if isinstance(segments, ctypes.Array) else self.segment_array(segments)
-        fn = self._L.ac_error_count_device_accumulate if accumulate else self._L.ac_error_count_device
-        st = fn(self._h, int(k), arr, len(arr), ctypes.c_void_p(stream or 0))
+        if window_len is not None:
+            if accumulate:
+                raise ValueError("window_len: no accumulate form")
+            wl = np.ascontiguousarray(window_len, dtype=np.uint32)
+            if wl.size != len(arr):
+                raise ValueError("one window_len per segment")
+            st = self._L.ac_error_count_device_equal(self._h, int(k), arr, _ptr(wl, ctypes.c_uint32), len(arr),
+                                                     ctypes.c_void_p(stream or 0))
+        else:
+            fn = self._L.ac_error_count_device_accumulate if accumulate else self._L.ac_error_count_device
+            st = fn(self._h, int(k), arr, len(arr), ctypes.c_void_p(stream or 0))
         if st:
             check(st, self._h)
 

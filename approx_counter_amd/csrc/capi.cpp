@@ -283,9 +283,12 @@ ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hi
     for (uint32_t i = 0; i < n; ++i) {
         const ac_segment& s = segs[i];
         if (s.n_kmers && (!s.kmers || !s.counts)) return fail(ctx, AC_ERR_INVALID, "segment kmers/counts is NULL");
+        const bool equal = ulen && ulen[i] != AC_NO_ULEN;  // windows back to back at ceil32(ulen[i])
         if (s.n_kmers && s.sample.n_windows &&
-            (!s.sample.codes || !s.sample.nmask || !s.sample.start || !s.sample.length))
+            (!s.sample.codes || !s.sample.nmask || (!equal && (!s.sample.start || !s.sample.length))))
             return fail(ctx, AC_ERR_INVALID, "segment sample has a NULL array");
+        if (equal && (uint64_t)s.sample.n_windows * ((ulen[i] + 31ull) & ~31ull) > s.sample.n_bases)
+            return fail(ctx, AC_ERR_INVALID, "equal windows reach past n_bases");
         if (s.sample.n_bases % 32 || s.sample.n_bases >= AC_MAX_IMAGE_BASES)
             return fail(ctx, AC_ERR_INVALID, "sample n_bases must be a multiple of 32 below 2^34");
         const uint32_t groups = (s.n_kmers + cpw - 1) / cpw;
@@ -647,6 +650,20 @@ ac_status ac_error_count_device_accumulate(ac_ctx* ctx, uint32_t k, const ac_seg
     if (!ctx) return fail(nullptr, AC_ERR_INVALID, "ctx is NULL");
     AC_HIP(ctx, hipSetDevice(ctx->device));
     return launch(ctx, k, segments, n_segments, (hipStream_t)hip_stream, false);
+}
+
+ac_status ac_error_count_device_equal(ac_ctx* ctx, uint32_t k, const ac_segment* segments,
+                                      const uint32_t* window_len, uint32_t n_segments, void* hip_stream) {
+    if (!ctx) return fail(nullptr, AC_ERR_INVALID, "ctx is NULL");
+    if (n_segments && !window_len) return fail(ctx, AC_ERR_INVALID, "window_len is NULL");
+    if (n_segments > AC_MAX_SEGS) return fail(ctx, AC_ERR_INVALID, "too many segments in one launch (max 4)");
+    uint32_t ul[AC_MAX_SEGS];
+    for (uint32_t i = 0; i < n_segments; ++i) {
+        if (window_len[i] == AC_NO_ULEN) return fail(ctx, AC_ERR_INVALID, "window_len out of range");
+        ul[i] = window_len[i];
+    }
+    AC_HIP(ctx, hipSetDevice(ctx->device));
+    return launch(ctx, k, segments, n_segments, (hipStream_t)hip_stream, true, nullptr, 0, 0, nullptr, ul);
 }
 
 }  // extern "C"
@@ -1401,12 +1418,12 @@ hipError_t stage_blit_launch(const void* src_dev, void* dst, size_t bytes, hipSt
 // The early-launch stage for calls counted in one part on one device, synchronous calls and
 // submits alike (default: AC_STAGE_EARLY=1).  0 = the pack -> copy kernel -> launch order of
 // round 2; 2 = the first job sent ahead of the launch by the copy kernel, the others staged by
-// the count kernel.  Same box, interleaved (profiles/r03_m2/summary.log): cfg2 step 0.141-0.143
+// the count kernel; 3 (diagnostic) = every job sent ahead.  Same box, interleaved (profiles/r03_m2/summary.log): cfg2 step 0.141-0.143
 // vs 0.148-0.149 ms.
 int stage_early() {
     static const int v = [] {
         const char* e = std::getenv("AC_STAGE_EARLY");
-        return e ? std::max(0, std::min(2, std::atoi(e))) : 1;
+        return e ? std::max(0, std::min(3, std::atoi(e))) : 1;
     }();
     return v;
 }
@@ -1638,7 +1655,12 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
         // codes, then the N bitmap unless the job holds no N, and the window descriptors unless
         // its windows have one length.  The first `pre` jobs (AC_STAGE_EARLY=2: the first) are
         // sent before the launch by the copy kernel instead, stream-ordered ahead of it.
-        const uint32_t pre = (stage_early() == 2 && p.n > 1) ? 1u : 0u;
+        // (AC_STAGE_EARLY=3, diagnostic: every job sent ahead, so the staged kernel runs on resident
+        // input -- its own cost against the plain kernel's)
+        const uint32_t pre = stage_early() == 3 ? p.n : (stage_early() == 2 && p.n > 1) ? 1u : 0u;
+        // (Packing the jobs' tasks interleaved, so both ends arrive together, was slower:
+        // 0.144 vs 0.134 ms per cfg2 step -- each end's last chunk waits for its final header,
+        // which then came ~27 us into the kernel for both; profiles/r03_stage/r03_early12_step3.log.)
         size_t region[AC_MAX_JOBS] = {};
         StageLaunch stg;
         if (++ctx->gen == 0) ++ctx->gen;
@@ -1692,27 +1714,21 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
                 return st;
             }
         constexpr uint64_t PUBLISH_STEP = 16384;  // bytes of new prefix worth a header store
-        uint32_t t0 = 0;
+        // per job: its tasks in claim order
+        std::vector<uint32_t> jt[AC_MAX_JOBS];
+        for (uint32_t t = 0; t < (uint32_t)tasks.size(); ++t) jt[tasks[t].job].push_back(t);
+        uint64_t ready[AC_MAX_JOBS], published[AC_MAX_JOBS];
+        uint32_t nt[AC_MAX_JOBS];  // jt[j][0, nt[j]) seen finished
+        bool n_seen[AC_MAX_JOBS] = {}, flagged[AC_MAX_JOBS] = {};
         for (uint32_t j = 0; j < p.n; ++j) {
-            uint32_t t1 = t0;
-            while (t1 < (uint32_t)tasks.size() && tasks[t1].job == j) ++t1;
-            const uint64_t base_off = p.off_codes[j] - p.off_kmers[j];
-            uint64_t ready = base_off, published = base_off;
-            bool n_seen = false;
-            uint32_t nt = t0, helped = t0;  // tasks [t0, nt) seen finished; [t0, helped) offered to this thread
-            while (nt < t1) {
-                if (helped < t1) pool.help(++helped);  // packs task helped - 1 unless a worker has it
-                while (nt < t1 && t_done[nt].v.load(std::memory_order_acquire)) {
-                    n_seen = n_seen || task_n[nt];
-                    if (!n_seen) ready = base_off + (tasks[nt].bases + tasks[nt].span) / 4;
-                    ++nt;
-                }
-                if (ready >= published + PUBLISH_STEP || (nt == t1 && ready > published)) {
-                    publish(j, ready);
-                    published = ready;
-                }
-                if (helped >= t1 && nt < t1) __builtin_ia32_pause();
-            }
+            ready[j] = published[j] = p.off_codes[j] - p.off_kmers[j];
+            nt[j] = 0;
+        }
+        uint32_t helped = 0, left_jobs = p.n;
+        bool first_flag = true;
+        // Job j is finished: its final byte count and N verdict, then its flag (or, jobs below
+        // `pre`, the copy kernel sends it ahead of the launch; those finish in job order).
+        auto finalize = [&](uint32_t j) -> ac_status {
             const bool nn = job_no_n(j);
             const size_t bytes = nn && ulen[j] != AC_NO_ULEN ? p.off_nmask[j] - p.off_kmers[j] : region[j];
             if (j < pre) {  // sent ahead of the launch, which follows it on the stream
@@ -1720,24 +1736,48 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
                 hipError_t e = stage_blit_launch(hd + p.off_kmers[j], d + p.off_kmers[j], bytes, stream);
                 ac_status st = e == hipSuccess ? AC_OK : hip_fail(ctx, e, "stage transfer");
                 if (st == AC_OK && j + 1 == pre) st = go();
-                if (st != AC_OK) {
-                    pool.finish();
-                    return st;
-                }
-            } else {
-                uint32_t* line = hdr + j * AC_QUEUE_LINE;
-                // no N: the whole region is N-free (never below a prefix: the codes end inside the
-                // bytes sent); with N the published prefix stays where the first N stopped it
-                if (nn) publish(j, bytes);
-                line[AC_HDR_INFO] = (uint32_t)bytes | (nn ? 0u : AC_HDR_INFO_HAS_N);
-                // (test hook: AC_STAGE_TEST_UNFLAGGED=1 leaves the last job unflagged, so the kernel's bounded
-                // wait runs out and the call must fail cleanly: tests/test_gpu_jobs.py)
-                static const bool unflag = std::getenv("AC_STAGE_TEST_UNFLAGGED") != nullptr;
-                if (!(unflag && j + 1 == p.n))
-                    __atomic_store_n(&line[AC_HDR_FLAG], p.gen, __ATOMIC_RELEASE);  // the kernel's waves may go
-                if (j == 0) mark(3);  // (AC_STAGE_TRACE: launch -> first job flagged, in "h2d_enq")
+                return st;
             }
-            t0 = t1;
+            uint32_t* line = hdr + j * AC_QUEUE_LINE;
+            // no N: the whole region is N-free (never below a prefix: the codes end inside the
+            // bytes sent); with N the published prefix stays where the first N stopped it
+            if (nn) publish(j, bytes);
+            line[AC_HDR_INFO] = (uint32_t)bytes | (nn ? 0u : AC_HDR_INFO_HAS_N);
+            // (test hook: AC_STAGE_TEST_UNFLAGGED=1 leaves the last job unflagged, so the kernel's bounded
+            // wait runs out and the call must fail cleanly: tests/test_gpu_jobs.py)
+            static const bool unflag = std::getenv("AC_STAGE_TEST_UNFLAGGED") != nullptr;
+            if (!(unflag && j + 1 == p.n))
+                __atomic_store_n(&line[AC_HDR_FLAG], p.gen, __ATOMIC_RELEASE);  // the kernel's waves may go
+            if (first_flag) mark(3);  // (AC_STAGE_TRACE: launch -> first job flagged, in "h2d_enq")
+            first_flag = false;
+            return AC_OK;
+        };
+        while (left_jobs) {
+            if (helped < (uint32_t)tasks.size()) pool.help(++helped);  // packs task helped - 1 unless a worker has it
+            for (uint32_t j = 0; j < p.n; ++j) {
+                if (flagged[j] || (j > 0 && j <= pre && !flagged[j - 1])) continue;  // (pre: in job order)
+                const uint64_t base_off = p.off_codes[j] - p.off_kmers[j];
+                const uint32_t nj = (uint32_t)jt[j].size();
+                while (nt[j] < nj && t_done[jt[j][nt[j]]].v.load(std::memory_order_acquire)) {
+                    const Task& x = tasks[jt[j][nt[j]]];
+                    n_seen[j] = n_seen[j] || task_n[jt[j][nt[j]]];
+                    if (!n_seen[j]) ready[j] = base_off + (x.bases + x.span) / 4;
+                    ++nt[j];
+                }
+                if (ready[j] >= published[j] + PUBLISH_STEP || (nt[j] == nj && ready[j] > published[j])) {
+                    publish(j, ready[j]);
+                    published[j] = ready[j];
+                }
+                if (nt[j] == nj) {
+                    if (ac_status st = finalize(j)) {
+                        pool.finish();
+                        return st;
+                    }
+                    flagged[j] = true;
+                    --left_jobs;
+                }
+            }
+            if (helped >= (uint32_t)tasks.size() && left_jobs) __builtin_ia32_pause();
         }
         pool.finish();
         mark(2);

@@ -668,7 +668,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
     // with a static split the first waves finish early and the last ones run
     // with few partners (profiles/r01_kernel_log.md).  Instead each candidate
     // group's items (`chunk` windows each) are spread over `subq` sub-queues
-    // (contiguous ranges, see `first_of` below), each a counter on its own
+    // (strided, see `n_in` below), each a counter on its own
     // 128-B line; a wave's first item is assigned statically, further ones
     // are claimed one at a time (below).  Waves are dealt to sub-queues
     // round-robin, so every sub-queue serves a mix of old and young waves;
@@ -689,33 +689,20 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
         const uint32_t qb = qq / WAVES_PER_BLOCK;  // one wave of every workgroup dealt to block-queue qb
         return wgs_of(qb);
     };
-    // Sub-queue jj holds the contiguous items [first(jj), first(jj) + n_in(jj)):
-    // a workgroup's sub-queues are consecutive and its XCD is fixed, so each
-    // XCD's L2 fetches a slice of the sample instead of all of it, and
-    // neighbouring windows (which share cache lines) are counted together.
-    // Staged launches (early counting) stride instead -- item jj + c*S in
-    // sub-queue jj -- so the waves' first items are the image's first windows,
-    // the ones that arrive first, and the waves move through the image as it
-    // arrives (AC_STRIDED_ITEMS / AC_CONTIG_ITEMS: one form for every launch, A/B switches).
-    constexpr bool STRIDED =
-#if defined(AC_STRIDED_ITEMS)
-        true;
-#elif defined(AC_CONTIG_ITEMS)  // A/B: contiguous for every launch
-        false;
-#else
-        STAGED;
-#endif
-    const uint32_t q_items = n_items / S, r_items = n_items % S;
-    auto n_in = [&](uint32_t jj) {
-        return STRIDED ? (jj < n_items ? (n_items - jj + S - 1u) / S : 0u) : q_items + (jj < r_items ? 1u : 0u);
-    };
-    auto first_of = [&](uint32_t jj) { return STRIDED ? 0u : jj * q_items + min(jj, r_items); };
+    // Sub-queue jj holds items jj, jj + S, jj + 2S, ... (strided): the waves'
+    // first items are the image's first windows, so a staged launch's waves
+    // start on the windows that arrive first and move through the image as it
+    // arrives.  Round 3 measured strided against contiguous ranges (sub-queue jj
+    // = one slice of the image, so each XCD's L2 fetched a slice): cfg2 kernel
+    // 104.8 -> 101.1 us, cfg3 equal, cfg5 -0.5 % (profiles/r03_strided_ab.log);
+    // contiguous ranges had been worth 1.5-2 % at cfg5 before two lane words per
+    // wave and the rotated workgroup deal.
+    auto n_in = [&](uint32_t jj) { return jj < n_items ? (n_items - jj + S - 1u) / S : 0u; };
     // Per-sub-queue constants of the served sub-queue, recomputed only when a
     // steal changes it (their divisions are SALU sequences; with 1-window items
     // they ran once per window).
     uint32_t jc_waves = waves_in(jc), jc_items = n_in(jc);
-    uint32_t jc_first = first_of(jc);
-    auto item_of = [&](uint32_t c) { return c < jc_items ? (STRIDED ? jc + c * S : jc_first + c) : n_items; };
+    auto item_of = [&](uint32_t c) { return c < jc_items ? jc + c * S : n_items; };
     auto dequeue_issue = [&]() -> uint32_t {  // lane 0 holds the result; read with readfirstlane
         uint32_t v = 0;
         if (lane == 0) v = __hip_atomic_fetch_add(counter(jc), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -746,7 +733,6 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
             jc = jj;
             jc_waves = waves_in(jj);
             jc_items = n_in(jj);
-            jc_first = first_of(jj);
             const uint32_t c = jc_waves + __builtin_amdgcn_readfirstlane(dequeue_issue());
             if (c < jc_items) return item_of(c);
         }

@@ -287,12 +287,21 @@ def main():
     # (profiles/r02_trace_percall.log), so the stage's warmup then starts at the sustained clock.
     kern_ms = None
     geo = None
+    wlen = None
     if not args.no_kernel_leg:
-        segs = [ac.DeviceSegment.upload(wl[e]["kmers"], ac.pack_windows(wl[e]["windows"]), device=dev) for e in ends]
+        packed = [ac.pack_windows(wl[e]["windows"]) for e in ends]
+        segs = [ac.DeviceSegment.upload(wl[e]["kmers"], packed[i], device=dev) for i, e in enumerate(ends)]
         arr = ac.ApproxCounter.segment_array(segs)
+        # equal windows (every start window sl bases, every end window sl + 1): the launch form the
+        # stage's kernel uses (window places computed, not loaded; ac_error_count_device_equal)
+        eq = [p.equal_window_len() for p in packed]
+        wlen = eq if all(x is not None for x in eq) else None
         kc = ac.ApproxCounter(local)
-        for _ in range(args.warmup):
-            kc.count_device(args.k, arr, stream=stream.cuda_stream)
+        # >= 150 untimed launches (>= 15 ms of load at cfg2): the timed ones then run at the
+        # sustained clock, like the stage's steps after them (last 50 of 210 launches:
+        # 94.6 us against 98.2 for all 210, profiles/r03_staged_cost_early3.md)
+        for _ in range(max(args.warmup, 150)):
+            kc.count_device(args.k, arr, stream=stream.cuda_stream, window_len=wlen)
         every = max(1, args.event_every)
         n_kernel = max(args.steps, args.kernel_launches)
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -300,7 +309,7 @@ def main():
         for i in range(n_kernel):
             if i % every == 0:
                 evs[i // every][0].record(stream)
-            kc.count_device(args.k, arr, stream=stream.cuda_stream)
+            kc.count_device(args.k, arr, stream=stream.cuda_stream, window_len=wlen)
             if i % every == 0:
                 evs[i // every][1].record(stream)
         torch.cuda.synchronize(dev)
@@ -476,6 +485,8 @@ def main():
                                          "ratio": pmc["sq_insts_valu_per_launch"] / model}
             out["kernel_ms"] = kern_ms
             out["kernel_kmer_bp_per_s"] = units_rank / (kern_ms * 1e-3)
+            out["kernel_leg"] = ("ac_error_count_device_equal (equal windows: places computed, as in the stage)"
+                                 if wlen else "ac_error_count_device (window descriptors loaded)")
             out["launch"] = geo
             out["roofline"] = roof
             out["roofline_hbm"] = {"bound": "hbm (informational)",

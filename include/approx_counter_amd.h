@@ -143,6 +143,18 @@ ac_status ac_error_count_device_accumulate(ac_ctx* ctx, uint32_t k, const ac_seg
                                            uint32_t n_segments, void* hip_stream);
 
 /*
+ * ac_error_count_device for samples whose windows all have one length -- the
+ * reference's own sample: every start window holds sl bases and every end
+ * window sl + 1 (sampleSequences, approx_counter.cpp:415-476).  Segment i's
+ * window w starts at base w * ceil32(window_len[i]) and holds window_len[i]
+ * bases, n_windows * ceil32(window_len[i]) <= n_bases; segments[i].sample.start
+ * and .length are not read (may be NULL): the kernel computes each window's
+ * place instead of loading its descriptor, as the host-buffer stage does.
+ */
+ac_status ac_error_count_device_equal(ac_ctx* ctx, uint32_t k, const ac_segment* segments,
+                                      const uint32_t* window_len, uint32_t n_segments, void* hip_stream);
+
+/*
  * Device copy of a packed sample, owned by the context (valid until the next
  * ac_sample_upload on ctx or ac_destroy).  Lets one upload serve both the
  * exact count and the approximate count of one read end.  The closest

@@ -96,6 +96,29 @@ def test_fused_segments_one_launch(counter):
         assert np.array_equal(seg.counts_numpy(), oracle.count_myers(16, km, w))
 
 
+@pytest.mark.parametrize("k,lens", [(16, (100, 101)), (22, (151, 151)), (9, (300, 37))])
+def test_device_equal_windows(counter, k, lens):
+    """ac_error_count_device_equal: windows back to back at ceil32 strides, places computed
+    instead of loaded (start / length not read) -- both ends fused, bit-exact."""
+    import torch
+
+    parts = []
+    for s, L in enumerate(lens):
+        km, w = cases.planted_case(700 + s + k, k, 300, 900, win_len=(L, L), p_n=0.01)
+        parts.append((km, [(x + "A" * L)[:L] for x in w]))  # truly equal (a plant may grow one)
+    packed = [ac.pack_windows(w) for _, w in parts]
+    assert [p.equal_window_len() for p in packed] == list(lens)
+    segs = [ac.DeviceSegment.upload(km, p) for (km, _), p in zip(parts, packed)]
+    counter.count_device(k, segs, window_len=list(lens))
+    torch.cuda.synchronize()
+    counter.check()
+    for (km, w), seg in zip(parts, segs):
+        assert np.array_equal(seg.counts_numpy(), oracle.count_myers(k, km, w))
+    # windows that would reach past n_bases are refused on the host
+    with pytest.raises(ac.ApproxCounterError):
+        counter.count_device(k, segs[:1], window_len=[lens[0] + 64])
+
+
 def test_sharded_accumulate_equals_whole(counter):
     """Windows split into shards and accumulated == one launch (multi-GPU identity)."""
     import torch

@@ -19,6 +19,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="cfg2")
     ap.add_argument("--launches", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=0,
+                    help="launches before the counted ones (a cold GPU runs its first ~10 ms below the "
+                         "sustained clock; kernel traces then leave them out: prof_summary.py --skip)")
+    ap.add_argument("--descriptors", action="store_true",
+                    help="load every window's start / length (ac_error_count_device) even for equal windows")
     a = ap.parse_args()
     import torch
 
@@ -28,14 +33,18 @@ def main():
     sys.argv = ["bench.py", "--config", a.config]
     args = bench.parse()
     wl, _ = bench.build_workload(args, 0, 1)
-    segs = [ac.DeviceSegment.upload(wl[e]["kmers"], ac.pack_windows(wl[e]["windows"])) for e in ("start", "end")]
+    packed = [ac.pack_windows(wl[e]["windows"]) for e in ("start", "end")]
+    segs = [ac.DeviceSegment.upload(wl[e]["kmers"], packed[i]) for i, e in enumerate(("start", "end"))]
     arr = ac.ApproxCounter.segment_array(segs)
+    eq = [p.equal_window_len() for p in packed]
+    wlen = eq if all(x is not None for x in eq) and not a.descriptors else None
     with ac.ApproxCounter(0) as c:
-        for _ in range(a.launches):
-            c.count_device(args.k, arr)
+        for _ in range(a.warmup + a.launches):
+            c.count_device(args.k, arr, window_len=wlen)
         torch.cuda.synchronize()
         c.check()
-        print(f"{a.launches} launches of {a.config}; geometry {c.last_launch()}")
+        print(f"{a.launches} launches of {a.config} ({'equal windows' if wlen else 'descriptors'}); "
+              f"geometry {c.last_launch()}")
 
 
 if __name__ == "__main__":

@@ -8,4 +8,5 @@ for c in FETCH_SIZE WRITE_SIZE "SQ_INSTS_VALU SQ_WAVES SQ_INSTS_SALU SQ_INSTS_LD
   d=gpurun_out/${tag}_$(echo $c | cut -d' ' -f1)
   timeout -s KILL 90 rocprofv3 --pmc $c -d $d -o run -- python3 tools/kernel_run.py --config $cfg --launches 20
 done
-timeout -s KILL 90 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_trace -o run -- python3 tools/kernel_run.py --config $cfg --launches 50
+# (trace: 150 warm-up launches first; summarise with tools/prof_summary.py --skip 150)
+timeout -s KILL 90 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_trace -o run -- python3 tools/kernel_run.py --config $cfg --launches 50 --warmup 150

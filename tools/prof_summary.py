@@ -28,11 +28,13 @@ def short(name: str, n: int = 70) -> str:
     return name if len(name) <= n else name[: n - 3] + "..."
 
 
-def kernel_rows(con):
+def kernel_rows(con, skip=0):
+    """Durations per kernel name in dispatch order, the first `skip` of each left out (a cold
+    GPU runs its first ~10 ms of dense load below the sustained clock)."""
     dur = defaultdict(list)
-    for name, d in con.execute("select name, duration from kernels"):
+    for name, d in con.execute("select name, duration from kernels order by start"):
         dur[name].append(d)
-    return dur
+    return {k: v[skip:] for k, v in dur.items() if len(v) > skip}
 
 
 def pmc_rows(con):
@@ -52,12 +54,12 @@ def pmc_rows(con):
     return vals
 
 
-def summarise(dbs):
+def summarise(dbs, skip=0):
     dur = defaultdict(list)
     pmc = defaultdict(lambda: defaultdict(list))
     for db in dbs:
         con = sqlite3.connect(db)
-        for k, v in kernel_rows(con).items():
+        for k, v in kernel_rows(con, skip).items():
             dur[k] += v
         for k, cs in pmc_rows(con).items():
             for c, v in cs.items():
@@ -86,11 +88,14 @@ def main():
     ap.add_argument("path")
     ap.add_argument("--out")
     ap.add_argument("--title", default="")
+    ap.add_argument("--skip", type=int, default=0, help="leave out each kernel's first N dispatches (warm-up)")
     a = ap.parse_args()
     dbs = find_dbs(a.path)
     if not dbs:
         raise SystemExit(f"no rocprofv3 .db under {a.path}")
-    text = summarise(dbs)
+    text = summarise(dbs, a.skip)
+    if a.skip:
+        text = f"(each kernel's first {a.skip} dispatches left out: warm-up)\n\n" + text
     if a.title:
         text = f"## {a.title}\n\n" + text
     if a.out:
