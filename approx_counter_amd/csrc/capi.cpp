@@ -252,6 +252,7 @@ ac_status check_layout(ac_ctx* ctx, const ac_windows& s) {
 // `no_n` (optional, per segment): the segment's image is known to hold no N.
 // `ulen` (optional, per segment): AC_NO_ULEN, or all windows have this length
 // and sit back to back at ceil32(ulen)-base strides (start / length unread).
+// `nrec` (optional, per equal-window segment): its windows carry inline N records (nrec.h).
 // Staged launch (the early-launch stage): the kernel copies each
 // segment's region from src (the pinned block) to dst once the host flags it in
 // host_hdr, and reports its completion there.
@@ -267,7 +268,8 @@ struct StageLaunch {
 
 ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hipStream_t stream,
                  bool zero, uint32_t* err = nullptr, int scratch = 0, uint64_t wave_cap = 0,
-                 const bool* no_n = nullptr, const uint32_t* ulen = nullptr, const StageLaunch* stage = nullptr) {
+                 const bool* no_n = nullptr, const uint32_t* ulen = nullptr, const StageLaunch* stage = nullptr,
+                 const bool* nrec = nullptr) {
     ac_ctx::Scratch& sc = ctx->sc[scratch];
     if (ac_status st = check_k(ctx, k)) return st;
     if (n > AC_MAX_SEGS) return fail(ctx, AC_ERR_INVALID, "too many segments in one launch (max 4)");
@@ -330,6 +332,7 @@ ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hi
         d.nmask = s.sample.nmask;
         d.has_n = (no_n && no_n[i]) ? 0u : 1u;
         d.ulen = ulen ? ulen[i] : AC_NO_ULEN;
+        d.nrec = (nrec && nrec[i] && d.ulen != AC_NO_ULEN) ? acamd::nrec_bits(d.ulen) : 0u;
         d.start = s.sample.start;
         d.length = s.sample.length;
         d.n_bases = s.sample.n_bases;
@@ -1428,6 +1431,15 @@ int stage_early() {
     return v;
 }
 
+// AC_STAGE_NREC=0 (A/B only): no inline N records; every job holding an N sends its N bitmap.
+bool records_off() {
+    static const bool v = [] {
+        const char* e = std::getenv("AC_STAGE_NREC");
+        return e && std::atoi(e) == 0;
+    }();
+    return v;
+}
+
 // Some job has candidates and windows (a launch with work, so a completion word to wait for).
 bool live_work(const ac_job* jobs, uint32_t n_jobs) {
     for (uint32_t j = 0; j < n_jobs; ++j)
@@ -1597,27 +1609,11 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
     uint32_t* hdr = sl.hdr;
     if (p.early) std::memset(hdr, 0, hdr_bytes);
     mark(1);
-    // per task: did its windows hold an N (its N-bitmap words, or-ed after packing; still in cache)
-    std::vector<uint8_t> task_n(tasks.size(), 0);
-    const std::function<void(uint32_t)> pack = [&](uint32_t t) {
-        const Task& x = tasks[t];
-        const ac_dna5_windows& w = jobs[x.job].sample;
-        const uint32_t j = x.job, r = x.w0 - p.lo[j];
-        uint32_t* nm = (uint32_t*)(h + p.off_nmask[j]);
-        acamd::pack_dna5_range(w.bases, w.offset, w.length, x.w0, x.w1, x.bases, (uint32_t*)(h + p.off_codes[j]), nm,
-                               (uint64_t*)(h + p.off_start[j]) + r, (uint32_t*)(h + p.off_len[j]) + r);
-        uint32_t any = 0;
-        for (uint64_t i = x.bases / 32, e = (x.bases + x.span) / 32; i < e; ++i) any |= nm[i];
-        task_n[t] = any != 0u;
-    };
-    bool no_n[AC_MAX_JOBS] = {};
-    auto job_no_n = [&](uint32_t j) {
-        for (size_t t = 0; t < tasks.size(); ++t)
-            if (tasks[t].job == j && task_n[t]) return false;
-        return true;
-    };
     // equal windows (the common case: every start window sl bases, every end window sl + 1)
     uint32_t ulen[AC_MAX_JOBS];
+    // inline N records (nrec.h): equal windows whose slots leave room carry their N positions, so
+    // the job's N bitmap is needed (and sent) only if some window overflowed its record
+    bool nrec[AC_MAX_JOBS] = {};
     for (uint32_t j = 0; j < p.n; ++j) {
         bool any = false, equal = true;
         uint32_t l0 = 0;
@@ -1628,7 +1624,27 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
                 equal = equal && x.len_diff == 0u && x.first_len == l0;
             }
         ulen[j] = (any && equal) ? l0 : AC_NO_ULEN;
+        nrec[j] = ulen[j] != AC_NO_ULEN && acamd::nrec_bits(ulen[j]) != 0u && !records_off();
     }
+    // per task: does the job need its N bitmap for these windows (an N, or with records an
+    // overflowed record)
+    std::vector<uint8_t> task_n(tasks.size(), 0);
+    const std::function<void(uint32_t)> pack = [&](uint32_t t) {
+        const Task& x = tasks[t];
+        const ac_dna5_windows& w = jobs[x.job].sample;
+        const uint32_t j = x.job, r = x.w0 - p.lo[j];
+        const uint32_t f = acamd::pack_dna5_range(w.bases, w.offset, w.length, x.w0, x.w1, x.bases,
+                                                  (uint32_t*)(h + p.off_codes[j]), (uint32_t*)(h + p.off_nmask[j]),
+                                                  (uint64_t*)(h + p.off_start[j]) + r,
+                                                  (uint32_t*)(h + p.off_len[j]) + r, nrec[j]);
+        task_n[t] = (f & (nrec[j] ? acamd::PACK_OVERFLOW : acamd::PACK_HAS_N)) != 0u;
+    };
+    bool no_n[AC_MAX_JOBS] = {};
+    auto job_no_n = [&](uint32_t j) {
+        for (size_t t = 0; t < tasks.size(); ++t)
+            if (tasks[t].job == j && task_n[t]) return false;
+        return true;
+    };
     char* d = (char*)sl.d;
     // The kernel writes the error word and the counts straight into the pinned block (hd), so
     // no copy comes back (profiles/r02_stage_dma_back_ab.log).
@@ -1678,7 +1694,7 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
         auto go = [&]() -> ac_status {
             ac_segment segs[AC_MAX_JOBS];
             make_segs(segs);
-            if (ac_status st = launch(ctx, k, segs, p.n, stream, zero, nullptr, p.scratch, 0, no_n, ulen, &stg))
+            if (ac_status st = launch(ctx, k, segs, p.n, stream, zero, nullptr, p.scratch, 0, no_n, ulen, &stg, nrec))
                 return st;
             AC_HIP(ctx, hipEventRecord(sl.ev, stream));
             sl.pending = true;
@@ -1760,7 +1776,9 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
                 const uint32_t nj = (uint32_t)jt[j].size();
                 while (nt[j] < nj && t_done[jt[j][nt[j]]].v.load(std::memory_order_acquire)) {
                     const Task& x = tasks[jt[j][nt[j]]];
-                    n_seen[j] = n_seen[j] || task_n[jt[j][nt[j]]];
+                    // (with records the kernel counts any packed window; one that overflowed its
+                    // record waits for the job's N bitmap by itself)
+                    n_seen[j] = n_seen[j] || (task_n[jt[j][nt[j]]] && !nrec[j]);
                     if (!n_seen[j]) ready[j] = base_off + (x.bases + x.span) / 4;
                     ++nt[j];
                 }
@@ -1841,7 +1859,7 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
         cap = ctx->resident[P] / wave_div;
     }
     if (ac_status st = launch(ctx, k, segs, p.n, stream, zero, d_counts ? nullptr : (uint32_t*)(hd + p.off_err),
-                              p.scratch, cap, no_n, ulen))
+                              p.scratch, cap, no_n, ulen, nullptr, nrec))
         return st;
     mark(4);
     mark(5);

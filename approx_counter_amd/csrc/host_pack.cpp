@@ -314,14 +314,37 @@ inline void pack32_scalar(const uint8_t* src, uint32_t* code2, uint32_t* nm) {
     *nm = n;
 }
 
+// The inline N record of one window (nrec.h), built from its N-mask bits as they are packed:
+// add(bits, b) takes the N bits of window bases [b, b + 64); finish(slot) writes the record
+// into the top bits of the slot's last code word (padding, zero until then) and returns the
+// window's PACK_* flags.  len = 0: no record (PACK_HAS_N only).
+struct NRecord {
+    uint32_t R, pb, cap, n = 0, pos = 0;
+    uint32_t len;
+    explicit NRecord(uint32_t l) : R(nrec_bits(l)), pb(nrec_pos_bits(l)), cap(nrec_cap(l)), len(l) {}
+    inline void add(uint64_t bits, uint32_t b) {
+        for (; bits; bits &= bits - 1) {
+            if (n < cap) pos |= (b + (uint32_t)__builtin_ctzll(bits)) << nrec_pos_shift(pb, n);
+            ++n;
+        }
+    }
+    inline uint32_t finish(uint32_t* slot) const {
+        if (!n) return 0u;
+        if (!R) return PACK_HAS_N;
+        slot[nrec_word(len)] |= n <= cap ? (pos | n << 29) : NREC_OVERFLOW << 29;
+        return PACK_HAS_N | (n > cap ? PACK_OVERFLOW : 0u);
+    }
+};
+
 // AVX-512BW: 64 bases per step, the tail through a byte-masked load (no
 // access past the window, so no over-read of the caller's buffer).  Codes: the
 // 2-bit values multiply-added into one byte per 4 bases, vpmovdb narrows 16
 // such dwords to the 16 bytes of four code words; N: one compare to a k-mask.
-__attribute__((target("avx512f,avx512bw,avx512vl"))) void pack_range_avx512(
+__attribute__((target("avx512f,avx512bw,avx512vl"))) uint32_t pack_range_avx512(
     const uint8_t* bases, const uint64_t* offset, const uint32_t* length, uint32_t w0, uint32_t w1, uint64_t first,
-    uint32_t* codes, uint32_t* nmask, uint64_t* start_out, uint32_t* len_out) {
+    uint32_t* codes, uint32_t* nmask, uint64_t* start_out, uint32_t* len_out, bool rec) {
     const __m512i three = _mm512_set1_epi8(3);
+    uint32_t flags = 0;
     const __m512i pair = _mm512_set1_epi16(0x0401);
     const __m512i quad = _mm512_set1_epi32(0x00100001);
     uint64_t pos = first;
@@ -333,11 +356,13 @@ __attribute__((target("avx512f,avx512bw,avx512vl"))) void pack_range_avx512(
         const uint64_t span = image_span(len);
         uint8_t* cw = (uint8_t*)(codes + pos / 16);
         uint8_t* nw = (uint8_t*)(nmask + pos / 32);
+        NRecord nr(rec ? len : 0u);
         for (uint32_t b = 0; b < span; b += 64) {
             const uint32_t left = len > b ? len - b : 0u;
             const __mmask64 m = left >= 64 ? ~0ull : ((1ull << left) - 1ull);
             const __m512i v = _mm512_maskz_loadu_epi8(m, src + b);
             const uint64_t isn = _mm512_mask_cmpgt_epu8_mask(m, v, three);
+            if (isn) nr.add(isn, b);
             __m512i t = _mm512_maddubs_epi16(_mm512_and_si512(v, three), pair);
             t = _mm512_madd_epi16(t, quad);
             const __m128i c = _mm512_cvtepi32_epi8(t);
@@ -350,13 +375,17 @@ __attribute__((target("avx512f,avx512bw,avx512vl"))) void pack_range_avx512(
                 std::memcpy(nw + b / 8, &lo, 4);
             }
         }
+        flags |= nr.finish(codes + pos / 16);
         pos += span;
     }
+    return flags;
 }
 
 template <bool AVX2>
-void pack_range_impl(const uint8_t* bases, const uint64_t* offset, const uint32_t* length, uint32_t w0, uint32_t w1,
-                     uint64_t first, uint32_t* codes, uint32_t* nmask, uint64_t* start_out, uint32_t* len_out) {
+uint32_t pack_range_impl(const uint8_t* bases, const uint64_t* offset, const uint32_t* length, uint32_t w0,
+                         uint32_t w1, uint64_t first, uint32_t* codes, uint32_t* nmask, uint64_t* start_out,
+                         uint32_t* len_out, bool rec) {
+    uint32_t flags = 0;
     uint64_t pos = first;
     alignas(32) uint8_t tail[32];
     for (uint32_t w = w0; w < w1; ++w) {
@@ -377,8 +406,13 @@ void pack_range_impl(const uint8_t* bases, const uint64_t* offset, const uint32_
             if (AVX2) pack32_avx2(tail, cw + 2 * full, nw + full);
             else pack32_scalar(tail, cw + 2 * full, nw + full);
         }
+        NRecord nr(rec ? len : 0u);
+        for (uint32_t b = 0; b < (len + 31u) / 32u; ++b)
+            if (nw[b]) nr.add(nw[b], 32u * b);
+        flags |= nr.finish(cw);
         pos += image_span(len);
     }
+    return flags;
 }
 
 bool have_avx2() {
@@ -393,14 +427,14 @@ bool have_avx512() {
 
 }  // namespace
 
-void pack_dna5_range(const uint8_t* bases, const uint64_t* offset, const uint32_t* length, uint32_t w0, uint32_t w1,
-                     uint64_t first, uint32_t* codes, uint32_t* nmask, uint64_t* start_out, uint32_t* len_out) {
+uint32_t pack_dna5_range(const uint8_t* bases, const uint64_t* offset, const uint32_t* length, uint32_t w0,
+                         uint32_t w1, uint64_t first, uint32_t* codes, uint32_t* nmask, uint64_t* start_out,
+                         uint32_t* len_out, bool records) {
     if (have_avx512())
-        pack_range_avx512(bases, offset, length, w0, w1, first, codes, nmask, start_out, len_out);
-    else if (have_avx2())
-        pack_range_impl<true>(bases, offset, length, w0, w1, first, codes, nmask, start_out, len_out);
-    else
-        pack_range_impl<false>(bases, offset, length, w0, w1, first, codes, nmask, start_out, len_out);
+        return pack_range_avx512(bases, offset, length, w0, w1, first, codes, nmask, start_out, len_out, records);
+    if (have_avx2())
+        return pack_range_impl<true>(bases, offset, length, w0, w1, first, codes, nmask, start_out, len_out, records);
+    return pack_range_impl<false>(bases, offset, length, w0, w1, first, codes, nmask, start_out, len_out, records);
 }
 
 }  // namespace acamd

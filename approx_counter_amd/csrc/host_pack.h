@@ -13,6 +13,8 @@
 #include <thread>
 #include <vector>
 
+#include "nrec.h"
+
 namespace acamd {
 
 // A fixed set of worker threads that run the tasks [0, n) of one job
@@ -117,7 +119,13 @@ inline uint64_t image_span(uint32_t len) { return ((uint64_t)len + 31u) / 32u * 
 // the image start / length of each window into start_out[w - w0] /
 // len_out[w - w0].  `codes` / `nmask` are the image's word arrays (indexed by
 // absolute image base).  Dna5 ordinals: 0..3 = A C G T, anything else = N.
-void pack_dna5_range(const uint8_t* bases, const uint64_t* offset, const uint32_t* length, uint32_t w0, uint32_t w1,
-                     uint64_t first, uint32_t* codes, uint32_t* nmask, uint64_t* start_out, uint32_t* len_out);
+// `records`: the windows are equal (one length) and each gets its inline N
+// record (nrec.h; windows whose length leaves no room get none).  Returns the
+// PACK_* bits of the range: PACK_HAS_N = some window holds an N, PACK_OVERFLOW =
+// some window's N bases did not fit its record (its N-bitmap words are needed).
+constexpr uint32_t PACK_HAS_N = 1u, PACK_OVERFLOW = 2u;
+uint32_t pack_dna5_range(const uint8_t* bases, const uint64_t* offset, const uint32_t* length, uint32_t w0,
+                         uint32_t w1, uint64_t first, uint32_t* codes, uint32_t* nmask, uint64_t* start_out,
+                         uint32_t* len_out, bool records = false);
 
 }  // namespace acamd

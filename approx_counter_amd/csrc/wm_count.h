@@ -89,6 +89,8 @@ struct SegDev {
     uint32_t has_n;       // 0: the image holds no N (its N bitmap is not read; every word reads as 0)
     uint32_t ulen;        // AC_NO_ULEN, or every window has this length and window w starts at base
                           // w * ceil32(ulen) (start / length are not read)
+    uint32_t nrec;        // equal windows with inline N records (nrec.h): the record's bits R, else 0;
+                          // has_n then says whether the N bitmap is there (some record overflowed)
     // staged launches: the segment's packed region (k-mers first) is copied from stage_src (the
     // pinned block, device-visible address) to stage_dst (device memory; kmers / codes / ... point
     // into it) in stage_chunks chunks of AC_STAGE_CHUNK bytes once the host flags it

@@ -44,6 +44,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "nrec.h"
 #include "wm_count.h"
 
 namespace acamd {
@@ -621,6 +622,9 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
     uint32_t ulen = sg.ulen;
     asm volatile("" : "+s"(ulen));
     const uint32_t ustride = ulen == AC_NO_ULEN ? 0u : (ulen + 31u) & ~31u;
+    // inline N records (nrec.h): the lane of the fetch holding a window's record word, ~0u: none
+    uint32_t rec_lane = sg.nrec ? nrec_word(ulen) : ~0u;
+    asm volatile("" : "+s"(rec_lane));
     auto desc = [&](uint32_t ww, uint64_t& base_out, uint32_t& len_out) __attribute__((always_inline)) {
         if (ulen != AC_NO_ULEN) {
             base_out = (uint64_t)ww * ustride;
@@ -748,6 +752,16 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
     auto fetchable = [&](uint64_t base, uint32_t len) { return len != 0u && valid(base, len); };
     // Staged early counting: before a window's first fetch, make sure every byte its fetches read
     // (256 bases per fetch from `base`, up to the image end) is in; false = skip the segment.
+    // The segment is complete (verdict r: 0 / 1) or skipped (~0u): from here on its own N bitmap,
+    // if it has one.
+    auto completed = [&](uint32_t r) __attribute__((always_inline)) {
+        partial = false;
+        if (r == ~0u) return false;
+        has_n = r;
+        nmask_bytes = has_n ? (uint32_t)(g_nbases >> 3) : 0u;
+        im.nmask = __builtin_amdgcn_make_buffer_rsrc((void*)nmask_p, 0, (int)nmask_bytes, 0x00020000);
+        return true;
+    };
     auto gate = [&](uint64_t base, uint32_t len) __attribute__((always_inline)) {
         if constexpr (STAGED) {
             if (!partial) return true;
@@ -765,13 +779,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
                 v_hi = __builtin_amdgcn_readfirstlane((uint32_t)(g >> 32)) * AC_STAGE_CHUNK;
                 return true;
             }
-            partial = false;
-            if (r == ~0u) return false;
-            // complete: from here on the segment's own N bitmap (if it has one)
-            has_n = r;
-            nmask_bytes = has_n ? (uint32_t)(g_nbases >> 3) : 0u;
-            im.nmask = __builtin_amdgcn_make_buffer_rsrc((void*)nmask_p, 0, (int)nmask_bytes, 0x00020000);
-            return true;
+            return completed(r);
         } else {
             (void)base;
             (void)len;
@@ -782,11 +790,18 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
     uint32_t nlen = 0;
     Fetch nf = {0u, 0u};
     const uint32_t lane_off = (lane < 16u ? lane : (lane - 16u) & 7u) << 2;  // this lane's word of a segment, in bytes
+    // (staged: did the next window's fetch read the N bitmap -- the descriptor changes when the
+    // segment completes; a window whose record overflowed needs its bitmap words)
+    bool nf_full = false;
+    auto fetch_next = [&](uint64_t b) __attribute__((always_inline)) {
+        tid_fetch(nf, im, b, lane, lane_off);
+        if constexpr (STAGED) nf_full = nmask_bytes != 0u;
+    };
     if (item < n_items) {
         desc(w, nbase, nlen);
         // (staged: after the table barrier -- a wave waiting for its first window must not hold
         // its workgroup's other waves at the barrier)
-        if (!STAGED && fetchable(nbase, nlen)) tid_fetch(nf, im, nbase, lane, lane_off);
+        if (!STAGED && fetchable(nbase, nlen)) fetch_next(nbase);
     }
 
     // ~Eq table, built by wave 0 of the workgroup (the waves share the
@@ -821,7 +836,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
     bool stage_ok = true;
     if (STAGED && item < n_items && fetchable(nbase, nlen)) {
         stage_ok = gate(nbase, nlen);
-        if (stage_ok) tid_fetch(nf, im, nbase, lane, lane_off);
+        if (stage_ok) fetch_next(nbase);
     }
     if (!stage_ok) item = n_items;
 
@@ -836,6 +851,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
         // issued: inside the chunk loop hipcc would otherwise wait for both.
         uint32_t f0 = tid_word(nf, lane);
         asm volatile("" : "+v"(f0));
+        const bool f0_full = STAGED ? nf_full : has_n != 0u;
         const uint32_t wn = w + 1;
         const bool last = wn >= item_end;  // the item's last window: claim the next item
         uint32_t nitem = n_items;
@@ -844,8 +860,48 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
         } else {
             pending = dequeue_issue();
         }
-        const bool ok = valid(base, len);  // a malformed window is skipped: never read outside the image
+        bool ok = valid(base, len);  // a malformed window is skipped: never read outside the image
         if (!ok && lane == 0) atomicOr(a.err, AC_DEVERR_WINDOW);
+        // Inline N record (nrec.h): the window's N-mask words (lanes 16-23) built from its N
+        // positions; an overflowed record takes the N bitmap's words instead.
+        if (rec_lane != ~0u && ok) {
+            const uint32_t rw = __builtin_amdgcn_readlane(f0, rec_lane);
+            const uint32_t c = rw >> 29;
+            if (c == NREC_OVERFLOW) {
+                bool have = f0_full;
+                if constexpr (STAGED) {
+                    if (!have && partial) {  // wait for the whole segment (its N bitmap)
+                        const uint64_t g = stage_gate(st_words, sg.stage_gen, sg.stage_chunks, blockIdx.x % AC_STAGE_REPL,
+                                                      a.gen, 0u, ~0u, a.err);
+                        if (!completed(__builtin_amdgcn_readfirstlane((uint32_t)g))) stage_ok = false;
+                    }
+                }
+                if (!have && has_n && stage_ok) {
+                    Fetch ff = {0u, 0u};
+                    tid_fetch(ff, im, base, lane, lane_off);
+                    uint32_t v = tid_word(ff, lane);
+                    asm volatile("" : "+v"(v));
+                    if (lane >= 16u) f0 = v;
+                    have = true;
+                }
+                if (!have) {  // no bitmap for an overflowed record: skipped, reported
+                    if (stage_ok && lane == 0) atomicOr(a.err, AC_DEVERR_WINDOW);
+                    ok = false;
+                }
+            } else if (c) {
+                const uint32_t pb = ustride <= 128u ? 7u : 8u, pm = (1u << pb) - 1u;
+                const uint32_t wi = lane - 16u;  // this lane's N-mask word (lanes 16-23)
+                uint32_t add = 0;
+                for (uint32_t i = 0; i < c; ++i) {
+                    const uint32_t pos = (rw >> nrec_pos_shift(pb, i)) & pm;
+                    if (wi == (pos >> 5)) add |= 1u << (pos & 31u);
+                }
+                f0 |= add;
+            }
+            // (made wave-uniform again: set under the error atomic's lane-0 branch, hipcc would
+            // treat it -- and every window size derived from it -- as divergent)
+            ok = __builtin_amdgcn_readfirstlane((uint32_t)ok) != 0u;
+        }
         const uint32_t nb0 = ok ? min(SEG, len) : 0u;
         const uint32_t nfull0 = nb0 >> 4;
         TidNfa s[W];
@@ -876,13 +932,13 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
                 desc(nitem * chunk, nbase, nlen);
             }
         } else if (fetchable(nbase, nlen)) {
-            if (gate(nbase, nlen)) tid_fetch(nf, im, nbase, lane, lane_off);
+            if (gate(nbase, nlen)) fetch_next(nbase);
             else stage_ok = false;
         }
         // step 2 (after block 1): the next item's first words
         if (nfull0 >= 4u) block32(f0, 2u);
         if (last && nitem < n_items && fetchable(nbase, nlen)) {
-            if (gate(nbase, nlen)) tid_fetch(nf, im, nbase, lane, lane_off);
+            if (gate(nbase, nlen)) fetch_next(nbase);
             else stage_ok = false;
         }
         if (ok) {
@@ -926,7 +982,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
                 if (item < n_items) {
                     desc(item * chunk, nbase, nlen);
                     if (fetchable(nbase, nlen)) {
-                        if (gate(nbase, nlen)) tid_fetch(nf, im, nbase, lane, lane_off);
+                        if (gate(nbase, nlen)) fetch_next(nbase);
                         else stage_ok = false;
                     }
                 }

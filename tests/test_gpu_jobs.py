@@ -102,6 +102,67 @@ def test_single_n_anywhere_is_seen(counter):
             assert got[0][0] < exp_clean[0]
 
 
+def _kmers_from(wins, n, seed, k=16):
+    """n k-mers cut from random places of random windows (N bases read as random bases)."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        w = wins[int(rng.integers(len(wins)))]
+        s0 = int(rng.integers(0, max(1, len(w) - k + 1)))
+        v = 0
+        for b in w[s0:s0 + k]:
+            v = (v << 2) | (int(b) if b < 4 else int(rng.integers(4)))
+        out.append(v)
+    return np.array(out, np.uint64)
+
+
+def _n_record_windows(seed, n, L, counts, spots=()):
+    """n equal windows of L random bases; window i holds counts[i % len(counts)] N bases,
+    the first ones at `spots` (window-relative, clipped to L), the rest at random places."""
+    rng = np.random.default_rng(seed)
+    w = rng.integers(0, 4, size=(n, L), dtype=np.uint8)
+    for i in range(n):
+        c = counts[i % len(counts)]
+        pos = [p for p in spots if p < L][:c]
+        free = np.setdiff1d(np.arange(L), pos)
+        pos += list(rng.choice(free, size=c - len(pos), replace=False))
+        w[i, pos] = 4 if i % 3 else 9  # (any ordinal > 3 is N)
+    return w
+
+
+@pytest.mark.parametrize("L", [100, 101, 150, 151, 128, 16, 40])
+def test_inline_n_records(counter, L):
+    """Equal windows carry their N positions in the slot's padding (nrec.h): 4 positions
+    at L = 100/101, 2 at 150, 1 at 151, none at 128 (no room: the N bitmap path), 4 at 16 / 40.
+    Windows with 0..6 N bases -- records that hold them all and records that overflow (their
+    N-bitmap words are used) -- with N on word edges (0, 15, 16, 31, 32, 63, 64, L - 1), in
+    one job beside an N-free job and a job whose only N-holders overflow."""
+    ws = _n_record_windows(L, 3000, L, [0, 1, 0, 2, 0, 3, 4, 0, 5, 6, 1], spots=(0, 15, 16, 31, 32, 63, 64, L - 1))
+    over = _n_record_windows(L + 1, 900, L, [0, 0, 7])
+    clean = _n_record_windows(L + 2, 700, L, [0])
+    kmers = _kmers_from(ws, 300, seed=L)  # occurrences in the windows, many across an N
+    km2 = np.concatenate([_kmers_from(over, 100, seed=L + 1), kmers[:20]])
+    jobs = [(kmers, ac.Dna5Sample.from_windows(ws)), (km2, ac.Dna5Sample.from_windows(over)),
+            (kmers[:64], ac.Dna5Sample.from_windows(clean))]
+    for rep in range(2):  # (both staging slots)
+        got = counter.count_jobs(16, jobs)
+        assert np.array_equal(got[0], oracle.count_myers(16, kmers, np.minimum(ws, 4), 16)), rep
+        assert np.array_equal(got[1], oracle.count_myers(16, km2, np.minimum(over, 4), 16)), rep
+        assert np.array_equal(got[2], oracle.count_myers(16, kmers[:64], clean, 16)), rep
+
+
+def test_inline_n_records_large_call(counter):
+    """The multi-part DMA path (>= 2^17 windows) with inline N records: N-bitmap sent only
+    for the part whose records overflowed."""
+    L = 101
+    a = _n_record_windows(7, 90_000, L, [0] * 20 + [1, 2, 3, 4])
+    b = _n_record_windows(8, 60_000, L, [0] * 50 + [1, 5])
+    kmers = _kmers_from(a, 40, seed=77)
+    got = counter.count_jobs(16, [(kmers, ac.Dna5Sample.from_windows(a)), (kmers, ac.Dna5Sample.from_windows(b))])
+    assert np.array_equal(got[0], oracle.count_myers(16, kmers, np.minimum(a, 4), 16))
+    assert np.array_equal(got[1], oracle.count_myers(16, kmers, np.minimum(b, 4), 16))
+
+
 def test_jobs_equal_image_path_and_repeat(counter):
     """Calls alternating between the two staging slots, growing and shrinking."""
     for trial, (n_k, n_w, wl) in enumerate([(500, 2000, (100, 101)), (37, 50, (0, 300)), (1000, 5000, (150, 151)),
