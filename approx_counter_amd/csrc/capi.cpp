@@ -1431,15 +1431,6 @@ int stage_early() {
     return v;
 }
 
-// AC_STAGE_NREC=0 (A/B only): no inline N records; every job holding an N sends its N bitmap.
-bool records_off() {
-    static const bool v = [] {
-        const char* e = std::getenv("AC_STAGE_NREC");
-        return e && std::atoi(e) == 0;
-    }();
-    return v;
-}
-
 // Some job has candidates and windows (a launch with work, so a completion word to wait for).
 bool live_work(const ac_job* jobs, uint32_t n_jobs) {
     for (uint32_t j = 0; j < n_jobs; ++j)
@@ -1553,7 +1544,10 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
         // the N bitmap, then the window descriptors: a job without N / with equal windows is
         // sent without them (job by job, below)
         p.off_kmers[j] = off;
-        off = align256(off + sizeof(uint64_t) * jobs[j].n_kmers);
+        // (early launch: the k-mer section fills whole staging chunks, which the kernel copies
+        // without waiting for the host -- the k-mers are in place before the launch)
+        off = p.early ? off + (sizeof(uint64_t) * jobs[j].n_kmers + AC_STAGE_CHUNK - 1) / AC_STAGE_CHUNK * AC_STAGE_CHUNK
+                      : align256(off + sizeof(uint64_t) * jobs[j].n_kmers);
         p.off_codes[j] = off;
         off = align256(off + sizeof(uint32_t) * (p.n_bases[j] / 16));
         p.off_nmask[j] = off;
@@ -1624,7 +1618,7 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
                 equal = equal && x.len_diff == 0u && x.first_len == l0;
             }
         ulen[j] = (any && equal) ? l0 : AC_NO_ULEN;
-        nrec[j] = ulen[j] != AC_NO_ULEN && acamd::nrec_bits(ulen[j]) != 0u && !records_off();
+        nrec[j] = ulen[j] != AC_NO_ULEN && acamd::nrec_bits(ulen[j]) != 0u;
     }
     // per task: does the job need its N bitmap for these windows (an N, or with records an
     // overflowed record)

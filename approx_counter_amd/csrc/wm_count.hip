@@ -315,9 +315,11 @@ __device__ __forceinline__ bool stage_late(uint64_t t0) {
     return __builtin_amdgcn_s_memrealtime() - t0 > AC_STAGE_TIMEOUT_TICKS;
 }
 
-// Claims and serves tickets until none is left; false on timeout.
-__device__ __attribute__((noinline)) bool stage_copy(const uint8_t* src, uint8_t* dst, uint32_t chunks, uint32_t* hdr,
-                                                     uint32_t* words, uint32_t* chunk_gen, uint32_t gen, uint32_t si) {
+// Claims and serves tickets until none is left; false on timeout.  Chunks below `pre_chunks` (the
+// k-mer section, in place in the pinned block before the launch) are copied without waiting.
+__device__ __attribute__((noinline)) bool stage_copy(const uint8_t* src, uint8_t* dst, uint32_t chunks,
+                                                     uint32_t pre_chunks, uint32_t* hdr, uint32_t* words,
+                                                     uint32_t* chunk_gen, uint32_t gen, uint32_t si) {
     const uint32_t lane = threadIdx.x & 63u;
     const StageWords sw = stage_words(words);
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -371,8 +373,8 @@ __device__ __attribute__((noinline)) bool stage_copy(const uint8_t* src, uint8_t
         // copier of chunk c - 1: wait until it lies inside the N-free prefix or the segment is final
         const uint32_t x = c - 1u, lo = x * AC_STAGE_CHUNK, hi = lo + AC_STAGE_CHUNK;
         uint32_t* my_avail = sw.avail + (x % AC_STAGE_REPL) * AC_QUEUE_LINE;
-        uint32_t limit = 0;  // bytes of the region known to be valid
-        for (;;) {
+        uint32_t limit = x < pre_chunks ? hi : 0u;  // bytes of the region known to be valid
+        while (limit == 0u) {
             // both words in one wave instruction (lane 0: N-free bytes, lane 1: final seen)
             uint32_t v = 0;
             if (lane < 2u) v = __hip_atomic_load(lane ? sw.fin : my_avail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -444,14 +446,14 @@ __device__ __attribute__((noinline)) uint32_t stage_wait_all(uint32_t* words, ui
 // segment's verdict (0 / 1) once it is complete, ~0u to skip (timeout: error bit set).
 __device__ __forceinline__ uint64_t stage_gate(uint32_t* words, const uint32_t* chunk_gen, uint32_t chunks,
                                                          uint32_t replica, uint32_t gen, uint32_t r0, uint32_t r1,
-                                                         uint32_t* err) {
+                                                         uint32_t* err, uint32_t pre = 0u) {
     const uint32_t lane = threadIdx.x & 63u;
     const StageWords sw = stage_words(words);
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     const uint32_t x0 = r0 / AC_STAGE_CHUNK, x1 = (r1 - 1u) / AC_STAGE_CHUNK;
     // (more chunks than lanes, or past the launch's chunks: wait for the whole segment)
     const uint32_t nx = (x1 < chunks && x1 - x0 < 62u) ? x1 - x0 + 1u : 0u;
-    bool in_prefix = false;  // the N-free prefix covers [r0, r1) (it only grows)
+    bool in_prefix = nx && r1 <= pre;  // the N-free prefix covers [r0, r1) (it only grows; `pre`: at launch)
     for (;;) {
         // one wave instruction: lane 0 the done count, lane 1 the N-free bytes (this workgroup's
         // replicas), lanes 2.. the chunks' flags once the prefix covers them
@@ -463,7 +465,7 @@ __device__ __forceinline__ uint64_t stage_gate(uint32_t* words, const uint32_t* 
         if (__builtin_amdgcn_readlane(v, 0) >= chunks) return wave_load(sw.verdict);
         const uint64_t miss = __ballot(lane >= 2u && lane - 2u < nx && v != gen);
         if (in_prefix && miss == 0) return ((uint64_t)(x1 + 1u) << 32) | 2u;
-        in_prefix = nx && __builtin_amdgcn_readlane(v, 1) >= r1;
+        in_prefix = nx && (r1 <= pre || __builtin_amdgcn_readlane(v, 1) >= r1);
         if (stage_late(t0)) {
             if (lane == 0) atomicOr(err, AC_DEVERR_STAGE);
             return ~0u;
@@ -579,17 +581,23 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
     uint32_t* st_words = nullptr;
     if (STAGED && sg.stage_chunks) {  // (a segment sent ahead of a staged launch has no chunks)
         st_words = a.stage + AC_STAGE_L_SEG(si) * AC_QUEUE_LINE;
+        // the k-mer section fills whole chunks and is in the pinned block before the launch
+        const uint32_t pre_chunks = sg.stage_codes_off / AC_STAGE_CHUNK;
         if (wib == 0) {
             uint32_t r = ~0u;
+            const bool equal = sg.ulen != AC_NO_ULEN && sg.n_kmers;
+            // (serving a chunk that has to wait for the host after the table barrier instead, so the
+            // workgroup's other waves start counting, measured slower: its copy starts later,
+            // profiles/r03_stage2/defer_ab.log)
             if (!__builtin_amdgcn_readfirstlane(
-                    (uint32_t)stage_copy(sg.stage_src, sg.stage_dst, sg.stage_chunks,
+                    (uint32_t)stage_copy(sg.stage_src, sg.stage_dst, sg.stage_chunks, pre_chunks,
                                          a.host_hdr + (uint32_t)si * AC_QUEUE_LINE, st_words, sg.stage_gen, a.gen,
                                          (uint32_t)si))) {
                 if (lane == 0) atomicOr(a.err, AC_DEVERR_STAGE);
-            } else if (sg.ulen != AC_NO_ULEN && sg.n_kmers) {
+            } else if (equal) {
                 // only the k-mers (the ~Eq table) are needed before counting starts
                 r = (uint32_t)stage_gate(st_words, sg.stage_gen, sg.stage_chunks, blockIdx.x % AC_STAGE_REPL, a.gen, 0u,
-                                         8u * sg.n_kmers, a.err);
+                                         8u * sg.n_kmers, a.err, sg.stage_codes_off);
             } else {
                 r = stage_wait_all(st_words, sg.stage_chunks, blockIdx.x % AC_STAGE_REPL, a.err);
             }
@@ -752,6 +760,9 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
     auto fetchable = [&](uint64_t base, uint32_t len) { return len != 0u && valid(base, len); };
     // Staged early counting: before a window's first fetch, make sure every byte its fetches read
     // (256 bases per fetch from `base`, up to the image end) is in; false = skip the segment.
+#ifdef AC_STAMPS
+    uint64_t gate_ticks = 0, gate_calls = 0;  // (diagnostic: time in the early-counting gate's slow path)
+#endif
     // The segment is complete (verdict r: 0 / 1) or skipped (~0u): from here on its own N bitmap,
     // if it has one.
     auto completed = [&](uint32_t r) __attribute__((always_inline)) {
@@ -771,8 +782,15 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
             if (r0 >= v_lo && r1 <= v_hi) return true;
             // (a call's results come back in VGPRs: made wave-uniform again, or everything they
             // touch -- the item cursor, window bases -- would turn divergent)
+#ifdef AC_STAMPS
+            const uint64_t tg = __builtin_amdgcn_s_memrealtime();
+#endif
             const uint64_t g = stage_gate(st_words, sg.stage_gen, sg.stage_chunks, blockIdx.x % AC_STAGE_REPL, a.gen,
                                           r0, r1, a.err);
+#ifdef AC_STAMPS
+            gate_ticks += __builtin_amdgcn_s_memrealtime() - tg;
+            ++gate_calls;
+#endif
             const uint32_t r = __builtin_amdgcn_readfirstlane((uint32_t)g);
             if (r == 2u) {
                 v_lo = (r0 / AC_STAGE_CHUNK) * AC_STAGE_CHUNK;
@@ -997,6 +1015,12 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
 
     stamp(wave, 2);
     stamp_val(wave, 6, ((uint64_t)si << 32) | ((uint64_t)g << 16) | j);
+#ifdef AC_STAMPS
+    if (STAGED) {  // (staged diagnostic builds: slots 4 / 5 hold the gate's time and calls, not the HW ids)
+        stamp_val(wave, 4, gate_ticks);
+        stamp_val(wave, 5, gate_calls);
+    }
+#endif
     // The workgroup's waves sum their counts in LDS; one wave adds the sums to
     // the group's slots in `acc`, so each slot takes 1/AC_WAVES_PER_BLOCK of the
     // same-address atomics (they serialise at the L2: ~10 us of launch tail at

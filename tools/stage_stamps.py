@@ -63,6 +63,7 @@ def main():
             print("   counting starts ", pct(us[m, 1]))
             print("   counting ends   ", pct(us[m, 2]))
             print("   exit            ", pct(us[m, 3]))
+            print("   gate slow path us", pct(raw[m, 4] / 100.0), " calls", pct(raw[m, 5]))
 
 
 if __name__ == "__main__":
