@@ -264,6 +264,8 @@ struct StageLaunch {
     uint32_t chunks[AC_MAX_SEGS] = {};
     uint32_t codes_off[AC_MAX_SEGS] = {};  // bytes of the region before its codes (the k-mers section)
     uint32_t* err_out = nullptr;  // device word the launch's error bits are also or-ed into (submits: ac_check)
+    uint32_t tag = 0;              // tagged completion (wm_count.h LaunchArgs::tag)
+    uint64_t* grp_err = nullptr;   // its per-group error words (device-visible pinned address)
 };
 
 ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hipStream_t stream,
@@ -448,7 +450,14 @@ ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hi
         a.err = a.stage + AC_STAGE_L_ERR * AC_QUEUE_LINE;
         a.total_groups = groups_total;
         a.err_out = stage->err_out;
+        a.tag = stage->tag;
+        a.grp_err = stage->grp_err;
     }
+    // the equal-window instantiation when every live segment has equal windows (their fit in the
+    // image checked above)
+    a.eq = 1u;
+    for (uint32_t i = 0; i < n; ++i)
+        if (a.seg[i].queue_begin != ~0u && a.seg[i].ulen == AC_NO_ULEN) a.eq = 0u;
     // Live segments' queue_begin values are increasing; the kernel picks the
     // last live segment whose queue_begin <= its sub-queue.
     a.total_waves = wave;
@@ -1360,6 +1369,11 @@ struct JobPlan {
     size_t off_start[AC_MAX_JOBS] = {}, off_len[AC_MAX_JOBS] = {}, off_counts[AC_MAX_JOBS] = {};
     size_t off_err = 0, total = 0;
     bool early = false;  // the early-launch stage (the kernel stages its own inputs, host-polled completion)
+    // early launch with host counts (synchronous calls): tagged completion -- u64 counts (generation << 32 |
+    // count) and one tagged error word per candidate group at off_gerr (n_gerr of them)
+    bool tag = false;
+    size_t off_gerr = 0;
+    uint32_t n_gerr = 0;
     uint32_t gen = 0;    // its generation (the header flags and completion word carry it)
     int slot = 0;     // staging slot (set by the caller: a synchronous part q uses slot q, a submit part its set's)
     int scratch = 0;  // count-kernel scratch set (ac_ctx::sc)
@@ -1452,6 +1466,38 @@ ac_status wait_early(ac_ctx* ctx, const uint32_t* done, uint32_t gen, hipStream_
             if (__atomic_load_n(done, __ATOMIC_ACQUIRE) == gen) break;
             return fail(ctx, AC_ERR_INTERNAL, "early launch finished without writing its completion word");
         }
+    }
+    return AC_OK;
+}
+
+// Spin until every count of the live jobs and every group error word of a tagged early launch
+// carries the launch's generation (high half); hipStreamQuery every 1024 spins catches a launch that
+// failed or finished without writing them.
+ac_status wait_tagged(ac_ctx* ctx, const ac_job* jobs, uint32_t n_jobs, const JobPlan& p, const char* h,
+                      hipStream_t stream) {
+    uint32_t spins = 0;
+    auto await = [&](const uint64_t* w) -> ac_status {
+        while ((uint32_t)(__atomic_load_n(w, __ATOMIC_ACQUIRE) >> 32) != p.gen) {
+            __builtin_ia32_pause();
+            if ((++spins & 1023u) == 0u) {
+                const hipError_t q = hipStreamQuery(stream);
+                if (q == hipErrorNotReady) continue;
+                if (q != hipSuccess) return hip_fail(ctx, q, "early launch");
+                if ((uint32_t)(__atomic_load_n(w, __ATOMIC_ACQUIRE) >> 32) == p.gen) break;
+                return fail(ctx, AC_ERR_INTERNAL, "early launch finished without writing its counts");
+            }
+        }
+        return AC_OK;
+    };
+    // the group error words first (one per candidate group: each arrives with its group's counts)
+    const uint64_t* ge = (const uint64_t*)(h + p.off_gerr);
+    for (uint32_t i = 0; i < p.n_gerr; ++i)
+        if (ac_status st = await(ge + i)) return st;
+    for (uint32_t j = 0; j < n_jobs && j < p.n; ++j) {
+        if (!jobs[j].n_kmers || p.hi[j] <= p.lo[j]) continue;
+        const uint64_t* hc = (const uint64_t*)(h + p.off_counts[j]);
+        for (uint32_t i = 0; i < jobs[j].n_kmers; ++i)
+            if (ac_status st = await(hc + i)) return st;
     }
     return AC_OK;
 }
@@ -1559,9 +1605,18 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
     }
     p.off_err = off;
     off = align256(off + sizeof(uint32_t));
+    p.tag = p.early && !d_counts;
     for (uint32_t j = 0; j < p.n; ++j) {
         p.off_counts[j] = off;
-        off = align256(off + sizeof(uint32_t) * jobs[j].n_kmers);
+        off = align256(off + (p.tag ? sizeof(uint64_t) : sizeof(uint32_t)) * jobs[j].n_kmers);
+    }
+    p.off_gerr = off;
+    p.n_gerr = 0;
+    if (p.tag) {
+        const uint32_t cpw = acamd::cands_per_wave(acamd::pack_factor(k));
+        for (uint32_t j = 0; j < p.n; ++j)
+            if (jobs[j].n_kmers && p.hi[j] > p.lo[j]) p.n_gerr += (jobs[j].n_kmers + cpw - 1) / cpw;
+        off = align256(off + sizeof(uint64_t) * p.n_gerr);
     }
     p.total = off;
     // The slot: wait until the launch that last read it has finished, grow it.
@@ -1592,7 +1647,10 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
     }
     *(uint32_t*)(h + p.off_err) = 0u;
     // (the early launch's header and buffer descriptors count a segment's bytes in 31 bits)
-    if (p.early && p.total >= (size_t(1) << 31)) p.early = false;
+    if (p.early && p.total >= (size_t(1) << 31)) p.early = p.tag = false;
+    // tagged completion: no count or error word may carry this call's generation before the kernel
+    // writes it (the slot last held other data)
+    if (p.tag) std::memset(h + p.off_counts[0], 0, p.total - p.off_counts[0]);
     // early launch: flags and the completion word cleared before the launch (the slot's last
     // launch has finished: its event was waited for above)
     const size_t hdr_bytes = sizeof(uint32_t) * AC_QUEUE_LINE * AC_HDR_LINES;
@@ -1677,6 +1735,8 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
         p.gen = stg.gen = ctx->gen;
         stg.host_hdr = sl.hdr_d;
         stg.err_out = d_counts ? ctx->d_err : nullptr;  // a submit reports through ac_check
+        stg.tag = p.tag ? 1u : 0u;
+        stg.grp_err = p.tag ? (uint64_t*)(hd + p.off_gerr) : nullptr;
         for (uint32_t j = 0; j < p.n; ++j) {
             const size_t end = ulen[j] != AC_NO_ULEN ? p.off_start[j] : (j + 1 < p.n ? p.off_kmers[j + 1] : p.off_err);
             region[j] = end - p.off_kmers[j];
@@ -1762,8 +1822,28 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
             first_flag = false;
             return AC_OK;
         };
+        // With workers, this thread only publishes: packing a task of its own (~8 us at cfg2's
+        // 312-window tasks) held every progress record back until it was done.  It still packs when
+        // no worker has finished a task for 20 us (workers asleep or descheduled).
+        const bool serial = pool.serial();
+        uint32_t seen_done = 0, idle_polls = 0;
+        auto last_seen = std::chrono::steady_clock::now();
         while (left_jobs) {
-            if (helped < (uint32_t)tasks.size()) pool.help(++helped);  // packs task helped - 1 unless a worker has it
+            bool help_now = false;
+            if (!serial && (++idle_polls & 63u) == 0u) {
+                uint32_t d = 0;
+                for (uint32_t j = 0; j < p.n; ++j) d += nt[j];
+                const auto now = std::chrono::steady_clock::now();
+                if (d != seen_done) {
+                    seen_done = d;
+                    last_seen = now;
+                } else if (now - last_seen > std::chrono::microseconds(20)) {
+                    help_now = true;
+                    last_seen = now;
+                }
+            }
+            if (serial && helped < (uint32_t)tasks.size()) pool.help(++helped);  // packs task helped - 1
+            else if (help_now) pool.help_one();
             for (uint32_t j = 0; j < p.n; ++j) {
                 if (flagged[j] || (j > 0 && j <= pre && !flagged[j - 1])) continue;  // (pre: in job order)
                 const uint64_t base_off = p.off_codes[j] - p.off_kmers[j];
@@ -1789,7 +1869,7 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
                     --left_jobs;
                 }
             }
-            if (helped >= (uint32_t)tasks.size() && left_jobs) __builtin_ia32_pause();
+            if (!(serial && helped < (uint32_t)tasks.size()) && left_jobs) __builtin_ia32_pause();
         }
         pool.finish();
         mark(2);
@@ -1990,7 +2070,14 @@ ac_status ac_error_count_jobs(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint3
         ac_ctx::Slot& sl = u.c->slot[u.plan.slot];
         const char* h = (const char*)sl.h;
         uint32_t err_word;
-        if (u.plan.early) {
+        if (u.plan.tag) {
+            // every count and every group's error word is tagged with the launch's generation: poll
+            // them instead of the stream (the launch's event is waited for when the slot is next used)
+            if (ac_status st = wait_tagged(u.c, jobs, n_jobs, u.plan, h, u.stream)) return st;
+            err_word = 0;
+            const uint64_t* ge = (const uint64_t*)(h + u.plan.off_gerr);
+            for (uint32_t i = 0; i < u.plan.n_gerr; ++i) err_word |= (uint32_t)ge[i];
+        } else if (u.plan.early) {
             // the kernel's last workgroup writes the completion word after every count: poll it
             // instead of waiting for the stream (the launch's event is waited for when the slot is
             // next used)
@@ -2014,6 +2101,12 @@ ac_status ac_error_count_jobs(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint3
             continue;
         }
         for (uint32_t j = 0; j < n_jobs; ++j) {
+            if (u.plan.tag) {
+                const uint64_t* hc = (const uint64_t*)(h + u.plan.off_counts[j]);
+                if (u.plan.hi[j] > u.plan.lo[j])  // (a job without windows here: its counts are 0)
+                    for (uint32_t i = 0; i < jobs[j].n_kmers; ++i) jobs[j].counts[i] += (uint32_t)hc[i];
+                continue;
+            }
             const uint32_t* hc = (const uint32_t*)(h + u.plan.off_counts[j]);
             for (uint32_t i = 0; i < jobs[j].n_kmers; ++i) jobs[j].counts[i] += hc[i];
         }

@@ -51,9 +51,9 @@ WorkPool::~WorkPool() {
     for (auto& t : threads_) t.join();
 }
 
-void WorkPool::drain(uint32_t gen, uint32_t upto) {
+void WorkPool::drain(uint32_t gen, uint32_t upto, uint32_t max_tasks) {
     const Job& job = jobs_[gen & 1u];
-    for (;;) {
+    for (uint32_t ran = 0; ran < max_tasks; ++ran) {
         uint64_t s = state_.load(std::memory_order_acquire);
         if ((uint32_t)(s >> 32) != gen) return;  // the job is over (a later one is published)
         const uint32_t i = (uint32_t)s;
@@ -121,6 +121,14 @@ void WorkPool::help(uint32_t upto) {
         return;
     }
     drain(gen_, upto);
+}
+
+void WorkPool::help_one() {
+    if (serial_) {
+        if (serial_next_ < n_) (*serial_fn_)(serial_next_++);
+        return;
+    }
+    drain(gen_, ~0u, 1);
 }
 
 void WorkPool::finish() {

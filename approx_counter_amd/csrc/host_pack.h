@@ -40,11 +40,14 @@ public:
     // below `upto`, finish() runs what is left and waits for every task.
     void begin(uint32_t n, const std::function<void(uint32_t)>& fn);
     void help(uint32_t upto);
+    void help_one();  // runs at most one unclaimed task
     void finish();
+    // (between begin() and finish()) the caller runs every task itself: no workers, or one task
+    bool serial() const { return serial_; }
 
 private:
     void worker();
-    void drain(uint32_t gen, uint32_t upto = ~0u);
+    void drain(uint32_t gen, uint32_t upto = ~0u, uint32_t max_tasks = ~0u);
 
     // A job is published as state_ = gen << 32 | next task; a participant
     // claims task i by a CAS of state_ from (gen, i) to (gen, i + 1), having

@@ -133,7 +133,12 @@ struct LaunchArgs {
     uint32_t* stage;
     uint32_t total_groups;
     uint32_t* err_out;  // staged: the launch's error bits are also or-ed in here when set (submits)
+    // staged, tagged completion (synchronous calls): counts are u64 host words (generation << 32 | count)
+    // and each candidate group stores its error snapshot (generation << 32 | bits) at grp_err[ticket index]
+    uint32_t tag;
+    uint64_t* grp_err;
     uint32_t n_segs;
+    uint32_t eq;  // every live segment has equal windows (ulen), checked on the host to fit its image
     uint32_t m;  // k-mer length
     uint32_t P;  // candidates per lane word
 };

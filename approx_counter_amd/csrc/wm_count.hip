@@ -516,7 +516,10 @@ __device__ __forceinline__ void tid_tail(TidNfa* s, uint32_t code, uint32_t nm, 
 // system-scope count stores, completion word).  The plain launches get a kernel
 // without any of it: in one kernel the extra live values cost SGPR spills inside
 // the count loop (+2.5 % VALU, +3.4 % SALU instructions, ~5 % time at cfg2).
-template <int P, bool STAGED>
+// EQ: every live segment holds equal windows back to back (ulen set; the host has checked that they
+// fit the image): window places by arithmetic, no descriptor arrays or per-window range checks held
+// in registers (the staged kernel spilled SGPRs inside the count loop without this).
+template <int P, bool STAGED, bool EQ>
 __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_for(P)>& lds) {
     constexpr int W = words_for(P);
     const uint32_t lane = threadIdx.x & 63u;
@@ -625,7 +628,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
     // pointer would turn the claim into a flat atomic, which also counts in
     // lgkmcnt and so would be waited for by the NFA blocks' LDS waits)
     uint32_t* g_queue = a.queue + ((uint64_t)a.bank * a.qstride + sg.queue_begin + g * sg.subq) * AC_QUEUE_LINE;
-    asm volatile("" : "+s"(g_start), "+s"(g_length), "+s"(g_nbases));
+    if constexpr (!EQ) asm volatile("" : "+s"(g_start), "+s"(g_length), "+s"(g_nbases));
     // Equal windows packed back to back (the host-buffer stage's image): descriptors by arithmetic.
     uint32_t ulen = sg.ulen;
     asm volatile("" : "+s"(ulen));
@@ -634,7 +637,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
     uint32_t rec_lane = sg.nrec ? nrec_word(ulen) : ~0u;
     asm volatile("" : "+s"(rec_lane));
     auto desc = [&](uint32_t ww, uint64_t& base_out, uint32_t& len_out) __attribute__((always_inline)) {
-        if (ulen != AC_NO_ULEN) {
+        if (EQ || ulen != AC_NO_ULEN) {
             base_out = (uint64_t)ww * ustride;
             len_out = ulen;
         } else if (STAGED) {
@@ -755,7 +758,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
 
     // Window pipeline: the next window's first segment is fetched while the current one is counted.
     // (written so that no sum wraps: a start near 2^64 must not pass)
-    auto valid = [&](uint64_t base, uint32_t len) { return window_valid<STAGED>(base, len, g_nbases) != 0u; };
+    auto valid = [&](uint64_t base, uint32_t len) { return EQ || window_valid<STAGED>(base, len, g_nbases) != 0u; };
     // an empty window reads no word (its start may be the image's end)
     auto fetchable = [&](uint64_t base, uint32_t len) { return len != 0u && valid(base, len); };
     // Staged early counting: before a window's first fetch, make sure every byte its fetches read
@@ -1074,6 +1077,9 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
                 if (cand[q] < sg.n_kmers) {
                     if (a.add_counts) {
                         if (v) atomicAdd(&sg.counts[cand[q]], v);
+                    } else if (STAGED && a.tag) {  // host memory, each count tagged with the launch's generation
+                        __hip_atomic_store((uint64_t*)sg.counts + cand[q], ((uint64_t)a.gen << 32) | v, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_SYSTEM);
                     } else if (STAGED) {  // host memory the host reads before the stream completes
                         __hip_atomic_store(&sg.counts[cand[q]], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     } else {
@@ -1082,7 +1088,18 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
                 }
             }
             if (lane == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (STAGED) {
+            if (STAGED && a.tag) {
+                // Tagged completion (synchronous calls): the host waits until every count and every
+                // group's error word carries this launch's generation, so no completion word, no
+                // wait for the counts' stores and no launch-wide counter sit on the path to the host.
+                // The group's error snapshot holds every bit its waves set (each wave's atomics were
+                // performed before its workgroup's ticket); the host ors all groups' words.
+                uint32_t e = 0;
+                if (lane == 0) e = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (lane == 0)
+                    __hip_atomic_store(a.grp_err + sg.ticket_begin + g, ((uint64_t)a.gen << 32) | e, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_SYSTEM);
+            } else if (STAGED) {
                 // the launch's last group publishes its error bits, then its completion, to the host
                 // (its counts went out as system-scope stores; each group's, drained before its add)
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1107,14 +1124,14 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
 
 }  // namespace
 
-template <int P, bool STAGED>
+template <int P, bool STAGED, bool EQ>
 __global__ __launch_bounds__(64 * WAVES_PER_BLOCK, waves_per_simd(words_for(P))) void wm2_count_kernel(LaunchArgs a) {
     // The LDS allocation also caps residency at waves_per_simd waves per SIMD
     // (one word: 8, faster than 6 or 10, profiles/r01_kernel_log.md; two words: 4).
     constexpr int W = words_for(P);
     constexpr int kBlocksPerCu = 4 * waves_per_simd(W) / WAVES_PER_BLOCK;
     __shared__ BlockLds<W> lds[(160 * 1024 / kBlocksPerCu) / sizeof(BlockLds<W>)];
-    count_body<P, STAGED>(a, lds[0]);
+    count_body<P, STAGED, EQ>(a, lds[0]);
 }
 
 namespace {
@@ -1122,7 +1139,7 @@ template <int P>
 hipError_t occupancy(int cu_count, uint32_t* waves) {
     int blocks = 0;
     hipError_t e =
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, wm2_count_kernel<P, false>, 64 * WAVES_PER_BLOCK, 0);
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, wm2_count_kernel<P, false, false>, 64 * WAVES_PER_BLOCK, 0);
     if (e != hipSuccess) return e;
     if (blocks < 1) blocks = 1;
     *waves = (uint32_t)blocks * WAVES_PER_BLOCK * (uint32_t)cu_count;
@@ -1155,12 +1172,16 @@ hipError_t launch_wm2_count(const LaunchArgs& args, hipStream_t stream) {
     if (args.total_waves == 0) return hipSuccess;
     const uint64_t blocks = (args.total_waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
     const dim3 grid((uint32_t)blocks), block(64 * WAVES_PER_BLOCK);
-#define AC_LAUNCH(PP)                                                                     \
-    case PP:                                                                              \
-        if (args.staged)                                                                  \
-            hipLaunchKernelGGL((wm2_count_kernel<PP, true>), grid, block, 0, stream, args);  \
-        else                                                                              \
-            hipLaunchKernelGGL((wm2_count_kernel<PP, false>), grid, block, 0, stream, args); \
+#define AC_LAUNCH(PP)                                                                            \
+    case PP:                                                                                     \
+        if (args.staged && args.eq)                                                              \
+            hipLaunchKernelGGL((wm2_count_kernel<PP, true, true>), grid, block, 0, stream, args);   \
+        else if (args.staged)                                                                    \
+            hipLaunchKernelGGL((wm2_count_kernel<PP, true, false>), grid, block, 0, stream, args);  \
+        else if (args.eq)                                                                        \
+            hipLaunchKernelGGL((wm2_count_kernel<PP, false, true>), grid, block, 0, stream, args);  \
+        else                                                                                     \
+            hipLaunchKernelGGL((wm2_count_kernel<PP, false, false>), grid, block, 0, stream, args); \
         break;
     switch (args.P) {
         AC_LAUNCH(1)

@@ -64,6 +64,11 @@ def main():
             print("   counting ends   ", pct(us[m, 2]))
             print("   exit            ", pct(us[m, 3]))
             print("   gate slow path us", pct(raw[m, 4] / 100.0), " calls", pct(raw[m, 5]))
+            grp = (raw[:, 6] >> 16) & 0xffff
+            for gv in np.unique(grp[m]):
+                mg = m & (grp == gv)
+                print(f"   group {int(gv)}: {int(mg.sum())} waves; counting ends p0/p50/p100 "
+                      f"{us[mg, 2].min():.1f} {np.median(us[mg, 2]):.1f} {us[mg, 2].max():.1f}; exit max {us[mg, 3].max():.1f}")
 
 
 if __name__ == "__main__":
