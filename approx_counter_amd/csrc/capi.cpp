@@ -376,9 +376,6 @@ ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hi
             if (x.queue_begin == ~0u || y.queue_begin == ~0u) continue;
             alias = x.counts < y.counts + y.n_kmers && y.counts < x.counts + x.n_kmers;
         }
-#ifdef AC_COUNTS_DIRECT  // A/B variant: memset + direct atomics
-    alias = true;
-#endif
     a.add_counts = (!zero || alias) ? 1u : 0u;
     if (zero && alias)
         for (uint32_t i = 0; i < n; ++i)
@@ -1550,16 +1547,7 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
     }
     const std::function<void(uint32_t)> span_of = [&](uint32_t t) {
         Task& x = tasks[t];
-        const uint32_t* len = jobs[x.job].sample.length;
-        uint64_t b = 0;
-        for (uint32_t w = x.w0; w < x.w1; ++w) b += image_span(len[w]);
-        // (a separate OR-reduction: folded into the loop above, min / max stopped it vectorising: +7 us at cfg2)
-        const uint32_t f = x.w1 > x.w0 ? len[x.w0] : 0u;
-        uint32_t diff = 0;
-        for (uint32_t w = x.w0; w < x.w1; ++w) diff |= len[w] ^ f;
-        x.bases = b;
-        x.first_len = f;
-        x.len_diff = diff;
+        x.bases = acamd::span_scan(jobs[x.job].sample.length + x.w0, x.w1 - x.w0, &x.first_len, &x.len_diff);
     };
     double tt = g_trace.on ? now_us() : 0.0;
     auto mark = [&](int i) {
@@ -1745,14 +1733,23 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
             stg.chunks[j] = j < pre ? 0u : (uint32_t)((region[j] + AC_STAGE_CHUNK - 1) / AC_STAGE_CHUNK);
             stg.codes_off[j] = (uint32_t)(p.off_codes[j] - p.off_kmers[j]);
         }
+        // (the slot's event is recorded after the publishing loop, not right after the launch: the
+        // caller's first progress records went out 1.2 us later with it there)
+        bool launched = false;
+        auto record_slot = [&]() -> ac_status {
+            if (!launched) return AC_OK;
+            launched = false;
+            AC_HIP(ctx, hipEventRecord(sl.ev, stream));
+            sl.pending = true;
+            return AC_OK;
+        };
         auto go = [&]() -> ac_status {
             ac_segment segs[AC_MAX_JOBS];
             make_segs(segs);
             if (ac_status st = launch(ctx, k, segs, p.n, stream, zero, nullptr, p.scratch, 0, no_n, ulen, &stg, nrec))
                 return st;
-            AC_HIP(ctx, hipEventRecord(sl.ev, stream));
-            sl.pending = true;
             mark(4);
+            launched = true;
             return AC_OK;
         };
         // Progress records: the packed N-free prefix of each job's region (its k-mers, then the
@@ -1863,6 +1860,7 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
                 if (nt[j] == nj) {
                     if (ac_status st = finalize(j)) {
                         pool.finish();
+                        (void)record_slot();
                         return st;
                     }
                     flagged[j] = true;
@@ -1873,7 +1871,7 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
         }
         pool.finish();
         mark(2);
-        return AC_OK;
+        return record_slot();
     }
     // DMA mode sends the inputs [r0, r1) of the slot (copy engine or blit kernel)
     auto transfer = [&](size_t r0, size_t r1) -> hipError_t {

@@ -433,7 +433,48 @@ bool have_avx512() {
     return v;
 }
 
+__attribute__((target("avx512f"))) uint64_t span_scan_avx512(const uint32_t* len, uint32_t n, uint32_t f,
+                                                              uint32_t* diff) {
+    const __m512i c31 = _mm512_set1_epi32(31), fv = _mm512_set1_epi32((int)f);
+    __m512i sum_lo = _mm512_setzero_si512(), sum_hi = _mm512_setzero_si512(), d = _mm512_setzero_si512();
+    __m512i all = _mm512_setzero_si512();
+    uint32_t i = 0;
+    for (; i + 16 <= n; i += 16) {
+        const __m512i v = _mm512_loadu_si512((const void*)(len + i));
+        all = _mm512_or_si512(all, v);
+        d = _mm512_or_si512(d, _mm512_xor_si512(v, fv));
+        const __m512i blocks = _mm512_srli_epi32(_mm512_add_epi32(v, c31), 5);  // (len + 31) / 32, wraps for len > 2^32 - 32
+        sum_lo = _mm512_add_epi64(sum_lo, _mm512_cvtepu32_epi64(_mm512_castsi512_si256(blocks)));
+        sum_hi = _mm512_add_epi64(sum_hi, _mm512_cvtepu32_epi64(_mm512_extracti64x4_epi64(blocks, 1)));
+    }
+    uint64_t b = (uint64_t)_mm512_reduce_add_epi64(_mm512_add_epi64(sum_lo, sum_hi)) * 32u;
+    uint32_t dd = (uint32_t)_mm512_reduce_or_epi32(d);
+    for (; i < n; ++i) {
+        b += image_span(len[i]);
+        dd |= len[i] ^ f;
+    }
+    // (a window of 2^31 bases or more may have wrapped above: recount exactly)
+    if ((uint32_t)_mm512_reduce_or_epi32(all) >> 31) {
+        b = 0;
+        for (uint32_t j = 0; j < n; ++j) b += image_span(len[j]);
+    }
+    *diff = dd;
+    return b;
+}
+
 }  // namespace
+
+uint64_t span_scan(const uint32_t* len, uint32_t n, uint32_t* first, uint32_t* diff) {
+    const uint32_t f = n ? len[0] : 0u;
+    *first = f;
+    if (have_avx512()) return span_scan_avx512(len, n, f, diff);
+    uint64_t b = 0;
+    for (uint32_t w = 0; w < n; ++w) b += image_span(len[w]);
+    uint32_t d = 0;  // (a separate OR-reduction: folded into the loop above it did not vectorise)
+    for (uint32_t w = 0; w < n; ++w) d |= len[w] ^ f;
+    *diff = d;
+    return b;
+}
 
 uint32_t pack_dna5_range(const uint8_t* bases, const uint64_t* offset, const uint32_t* length, uint32_t w0,
                          uint32_t w1, uint64_t first, uint32_t* codes, uint32_t* nmask, uint64_t* start_out,

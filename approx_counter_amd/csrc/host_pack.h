@@ -116,6 +116,10 @@ double cgroup_cpu_quota();
 // boundaries, include/approx_counter_amd.h).
 inline uint64_t image_span(uint32_t len) { return ((uint64_t)len + 31u) / 32u * 32u; }
 
+// Image bases of windows len[0, n) (sum of image_span), the first length and the OR of
+// (length ^ first) -- zero iff every window has one length.  AVX-512 when the CPU has it.
+uint64_t span_scan(const uint32_t* len, uint32_t n, uint32_t* first, uint32_t* diff);
+
 // Packs windows [w0, w1) of a Dna5 window set into a window image whose window
 // w0 starts at image base `first`: writes the 2-bit codes and the N bitmap of
 // every 32-base block the windows occupy (padding bases as code 0, not N), and

@@ -140,10 +140,7 @@ typedef const __attribute__((address_space(4))) uint64_t* cu64p;
 typedef const __attribute__((address_space(4))) uint32_t* cu32p;
 __device__ __forceinline__ void load_desc(const uint64_t* start, const uint32_t* length, uint32_t w, uint64_t& base,
                                           uint32_t& len) {
-#if defined(AC_TIMING_UNIFORM_DESC)  // timing-only A/B: equal windows at a 128-base stride, no descriptor loads
-    base = (uint64_t)w * 128u;
-    len = __builtin_amdgcn_readfirstlane(((cu32p)length)[0]);
-#elif !defined(AC_VECTOR_DESC)
+#if !defined(AC_VECTOR_DESC)
     base = ((cu64p)start)[w];
     len = ((cu32p)length)[w];
 #else
@@ -214,7 +211,6 @@ __device__ __forceinline__ uint32_t tid_word(const Fetch& f, uint32_t lane) { re
 // sum wraps: a start near 2^64 must not pass.
 template <bool RFL>
 __device__ __forceinline__ uint32_t window_valid(uint64_t base, uint32_t len, uint64_t nb) {
-#ifndef AC_VALU_VALID
     // (RFL, the staged kernel: its early-counting gate leaves hipcc holding some of these
     // wave-uniform values in VGPRs; readfirstlane puts them back in SGPRs for the asm)
     const uint32_t nbl = RFL ? __builtin_amdgcn_readfirstlane((uint32_t)nb) : (uint32_t)nb;
@@ -235,9 +231,6 @@ __device__ __forceinline__ uint32_t window_valid(uint64_t base, uint32_t len, ui
         : [nbl] "s"(nbl), [nbh] "s"(nbh), [len] "s"(ln), [bl] "s"(bl), [bh] "s"(bh)
         : "scc");
     return bad ^ 1u;
-#else
-    return !(base & 31u) && len <= nb && base <= nb - len;
-#endif
 }
 
 // The workgroup's waves serve one candidate group and share one table, the
@@ -535,7 +528,6 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
     // sub-queue is served by waves of every dispatch age (see the work-queue
     // comment below); q -> (segment, candidate group g, sub-queue j of that group).
     const uint32_t rank = blockIdx.x / nqb;
-#ifndef AC_PLAIN_DEAL  // A/B: the plain b mod nqb deal
     // Rank r's workgroups are dealt to the block-queues rotated by shift(r):
     // with a plain b mod nqb deal every workgroup a CU receives belongs to one
     // block-queue, so each candidate group ran on a fixed slice of the chip
@@ -551,10 +543,6 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
     auto wgs_of = [&](uint32_t qb) {
         return blocks / nqb + ((qb + nqb - shift(blocks / nqb)) % nqb < blocks % nqb ? 1u : 0u);
     };
-#else
-    const uint32_t bq = blockIdx.x % nqb;
-    auto wgs_of = [&](uint32_t qb) { return blocks / nqb + (qb < blocks % nqb ? 1u : 0u); };
-#endif
     const uint32_t q = bq * WAVES_PER_BLOCK + wib;
     int si = 0;
 #pragma unroll
@@ -1036,15 +1024,6 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
     // launch's last group reads the word)
     if (STAGED) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-#ifdef AC_COUNTS_DIRECT  // A/B variant: every workgroup adds straight into the (pre-zeroed) counts
-    if (wib == 0) {
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            const uint32_t v = lds.cnt[q * 64 + lane];
-            if (cand[q] < sg.n_kmers && v) atomicAdd(&sg.counts[cand[q]], v);
-        }
-    }
-#else
     if (wib == 0) {
         uint32_t* acc = a.acc + sg.acc_begin + g * (64u * Q);
         // Returning atomics, their results consumed before the ticket: every add
@@ -1055,11 +1034,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
             const uint32_t v = lds.cnt[q * 64 + lane];
-#ifdef AC_TIMING_NO_ATOMICS  // timing-only build: results discarded (kept live by an impossible store)
-            if (v == 0xdeadbeefu) acc[q * 64 + lane] = 1u;
-#else
             if (v) sink |= __hip_atomic_fetch_add(&acc[q * 64 + lane], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
         }
         asm volatile("" ::"v"(sink));
         // Workgroups serving group g: those dealt to its subq / WPB block-queues.
@@ -1118,7 +1093,6 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
             }
         }
     }
-#endif
     stamp(wave, 3);
 }
 
