@@ -445,7 +445,6 @@ ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hi
         a.host_hdr = stage->host_hdr;
         a.stage = sc.queue + ((uint64_t)sc.bank * sc.qcap + n_counters) * AC_QUEUE_LINE;
         a.err = a.stage + AC_STAGE_L_ERR * AC_QUEUE_LINE;
-        a.total_groups = groups_total;
         a.err_out = stage->err_out;
         a.tag = stage->tag;
         a.grp_err = stage->grp_err;
@@ -1371,7 +1370,7 @@ struct JobPlan {
     bool tag = false;
     size_t off_gerr = 0;
     uint32_t n_gerr = 0;
-    uint32_t gen = 0;    // its generation (the header flags and completion word carry it)
+    uint32_t gen = 0;    // its generation (the header flags and the tagged counts carry it)
     int slot = 0;     // staging slot (set by the caller: a synchronous part q uses slot q, a submit part its set's)
     int scratch = 0;  // count-kernel scratch set (ac_ctx::sc)
 
@@ -1442,29 +1441,11 @@ int stage_early() {
     return v;
 }
 
-// Some job has candidates and windows (a launch with work, so a completion word to wait for).
+// Some job has candidates and windows (a launch with work, so tagged counts to wait for).
 bool live_work(const ac_job* jobs, uint32_t n_jobs) {
     for (uint32_t j = 0; j < n_jobs; ++j)
         if (jobs[j].n_kmers && jobs[j].sample.n_windows) return true;
     return false;
-}
-
-// Spin until an early launch's completion word reads `gen`.  The kernel's own waits are
-// bounded (AC_STAGE_TIMEOUT_TICKS), so the stream always completes; if it has completed
-// without the word, the launch failed.
-ac_status wait_early(ac_ctx* ctx, const uint32_t* done, uint32_t gen, hipStream_t stream) {
-    uint32_t spins = 0;
-    while (__atomic_load_n(done, __ATOMIC_ACQUIRE) != gen) {
-        __builtin_ia32_pause();
-        if ((++spins & 1023u) == 0u) {
-            const hipError_t q = hipStreamQuery(stream);
-            if (q == hipErrorNotReady) continue;
-            if (q != hipSuccess) return hip_fail(ctx, q, "early launch");
-            if (__atomic_load_n(done, __ATOMIC_ACQUIRE) == gen) break;
-            return fail(ctx, AC_ERR_INTERNAL, "early launch finished without writing its completion word");
-        }
-    }
-    return AC_OK;
 }
 
 // Spin until every count of the live jobs and every group error word of a tagged early launch
@@ -1639,7 +1620,7 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
     // tagged completion: no count or error word may carry this call's generation before the kernel
     // writes it (the slot last held other data)
     if (p.tag) std::memset(h + p.off_counts[0], 0, p.total - p.off_counts[0]);
-    // early launch: flags and the completion word cleared before the launch (the slot's last
+    // early launch: flags cleared before the launch (the slot's last
     // launch has finished: its event was waited for above)
     const size_t hdr_bytes = sizeof(uint32_t) * AC_QUEUE_LINE * AC_HDR_LINES;
     if (p.early && !sl.hdr) {
@@ -2075,13 +2056,6 @@ ac_status ac_error_count_jobs(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint3
             err_word = 0;
             const uint64_t* ge = (const uint64_t*)(h + u.plan.off_gerr);
             for (uint32_t i = 0; i < u.plan.n_gerr; ++i) err_word |= (uint32_t)ge[i];
-        } else if (u.plan.early) {
-            // the kernel's last workgroup writes the completion word after every count: poll it
-            // instead of waiting for the stream (the launch's event is waited for when the slot is
-            // next used)
-            const uint32_t* res = sl.hdr + AC_MAX_SEGS * AC_QUEUE_LINE;
-            if (ac_status st = wait_early(u.c, res + AC_HDR_DONE, u.plan.gen, u.stream)) return st;
-            err_word = __atomic_load_n(res + AC_HDR_ERR, __ATOMIC_ACQUIRE);
         } else {
             AC_HIP(u.c, hipStreamSynchronize(u.stream));
             sl.pending = false;

@@ -47,25 +47,21 @@ constexpr int waves_per_simd(int W) { return W == 2 ? 4 : 8; }
                          //   the host gave up on the call (the waves skip the segment)
 #define AC_HDR_INFO_HAS_N 0x80000000u
 #define AC_HDR_INFO_ABORT 0xffffffffu
-// and the kernel's last workgroup writes the launch's result line (line AC_MAX_SEGS):
-#define AC_HDR_DONE 0    // = generation once every count of the launch is in host memory
-#define AC_HDR_ERR 1     // AC_DEVERR_* bits of the launch
-#define AC_HDR_LINES (AC_MAX_SEGS + 1)
+#define AC_HDR_LINES AC_MAX_SEGS
 #define AC_STAGE_CHUNK 4096u  // bytes one wave copies per claimed chunk (64 lanes x 16 B x 4)
 #define AC_STAGE_REPL 32      // replicas of a segment's done counter (pollers spread over lines)
 // Device words of a staged launch, one AC_QUEUE_LINE line each, after the
 // launch's sub-queue counters in its queue bank (zeroed with them for the next
 // launch on that bank; only word 0 of a line is ever used, as the next launch
-// zeroes word 0 of each): groups done, error bits, then per segment: chunk
+// zeroes word 0 of each): error bits, then per segment: chunk
 // claims, the segment's final header (verdict, bytes, final seen),
 // AC_STAGE_REPL replicas of the N-free bytes available so far, AC_STAGE_REPL
 // done replicas (every workgroup polls one replica of each: ~1000 waves
 // polling one line slowed the chunk copies).
-#define AC_STAGE_L_GROUPS 0
-#define AC_STAGE_L_ERR 1
+#define AC_STAGE_L_ERR 0
 #define AC_STAGE_SEG_LINES (4 + 2 * AC_STAGE_REPL)
-#define AC_STAGE_L_SEG(s) (2 + (s) * AC_STAGE_SEG_LINES)
-#define AC_STAGE_LINES (2 + AC_MAX_SEGS * AC_STAGE_SEG_LINES)
+#define AC_STAGE_L_SEG(s) (1 + (s) * AC_STAGE_SEG_LINES)
+#define AC_STAGE_LINES (1 + AC_MAX_SEGS * AC_STAGE_SEG_LINES)
 #define AC_STAGE_TIMEOUT_TICKS 50000000ull  // 0.5 s of s_memrealtime (100 MHz): every wait is bounded
 
 namespace acamd {
@@ -126,13 +122,12 @@ struct LaunchArgs {
     // Staged launch (nonzero): inputs copied in by the kernel once the host flags each segment in
     // host_hdr (pinned, AC_HDR_LINES lines of AC_QUEUE_LINE u32); counts stored to host memory at
     // system scope, the launch's completion written to host_hdr's result line.  `stage` = this
-    // launch's AC_STAGE_LINES device lines; total_groups = candidate groups over all segments.
+    // launch's AC_STAGE_LINES device lines.
     uint32_t staged;
     uint32_t gen;
     uint32_t* host_hdr;
     uint32_t* stage;
-    uint32_t total_groups;
-    uint32_t* err_out;  // staged: the launch's error bits are also or-ed in here when set (submits)
+    uint32_t* err_out;  // staged, counts in device memory (submits): each group ors its error bits in here
     // staged, tagged completion (synchronous calls): counts are u64 host words (generation << 32 | count)
     // and each candidate group stores its error snapshot (generation << 32 | bits) at grp_err[ticket index]
     uint32_t tag;

@@ -506,7 +506,7 @@ __device__ __forceinline__ void tid_tail(TidNfa* s, uint32_t code, uint32_t nm, 
 }
 
 // STAGED: the early-launch instantiation (staging wait, vector descriptor loads,
-// system-scope count stores, completion word).  The plain launches get a kernel
+// system-scope count stores, tagged completion).  The plain launches get a kernel
 // without any of it: in one kernel the extra live values cost SGPR spills inside
 // the count loop (+2.5 % VALU, +3.4 % SALU instructions, ~5 % time at cfg2).
 // EQ: every live segment holds equal windows back to back (ulen set; the host has checked that they
@@ -1055,40 +1055,27 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
                     } else if (STAGED && a.tag) {  // host memory, each count tagged with the launch's generation
                         __hip_atomic_store((uint64_t*)sg.counts + cand[q], ((uint64_t)a.gen << 32) | v, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_SYSTEM);
-                    } else if (STAGED) {  // host memory the host reads before the stream completes
-                        __hip_atomic_store(&sg.counts[cand[q]], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    } else {
+                    } else {  // (device memory: read after the stream has completed)
                         sg.counts[cand[q]] = v;
                     }
                 }
             }
             if (lane == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (STAGED && a.tag) {
-                // Tagged completion (synchronous calls): the host waits until every count and every
-                // group's error word carries this launch's generation, so no completion word, no
-                // wait for the counts' stores and no launch-wide counter sit on the path to the host.
+            if (STAGED) {
                 // The group's error snapshot holds every bit its waves set (each wave's atomics were
-                // performed before its workgroup's ticket); the host ors all groups' words.
+                // performed before its workgroup's ticket); all groups' snapshots together hold the
+                // launch's.  Tagged completion (synchronous calls): the host waits until every count
+                // and every group's word carries this launch's generation, so no completion word, no
+                // wait for the counts' stores and no launch-wide counter sit on the path to the host.
+                // Submits (counts in device memory): the bits go to the context's word (ac_check).
                 uint32_t e = 0;
                 if (lane == 0) e = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (lane == 0)
-                    __hip_atomic_store(a.grp_err + sg.ticket_begin + g, ((uint64_t)a.gen << 32) | e, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_SYSTEM);
-            } else if (STAGED) {
-                // the launch's last group publishes its error bits, then its completion, to the host
-                // (its counts went out as system-scope stores; each group's, drained before its add)
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                uint32_t last = 0;
-                if (lane == 0)
-                    last = __hip_atomic_fetch_add(a.stage + AC_STAGE_L_GROUPS * AC_QUEUE_LINE, 1u, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT) == a.total_groups - 1u;
-                if (__builtin_amdgcn_readfirstlane(last) && lane == 0) {
-                    uint32_t* res = a.host_hdr + AC_MAX_SEGS * AC_QUEUE_LINE;
-                    const uint32_t e = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (e && a.err_out) atomicOr(a.err_out, e);
-                    __hip_atomic_store(res + AC_HDR_ERR, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    __hip_atomic_store(res + AC_HDR_DONE, a.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (a.tag) {
+                    if (lane == 0)
+                        __hip_atomic_store(a.grp_err + sg.ticket_begin + g, ((uint64_t)a.gen << 32) | e,
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                } else if (lane == 0 && e && a.err_out) {
+                    atomicOr(a.err_out, e);
                 }
             }
         }

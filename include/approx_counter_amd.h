@@ -367,12 +367,14 @@ int ac_plan_host_cpus(const char* const* rank_cpulists, int n_ranks, int rank, c
  * on one device (default; AC_STAGE_EARLY=0 turns it off): the count kernel is
  * launched before the host packs, the host flags each job in a pinned header as
  * soon as it is packed, the kernel copies the flagged job into device memory
- * itself and counts it while later jobs are still being packed, and its last
- * workgroup stores the counts and a completion word into pinned memory, which
- * the host polls.  0 = the DMA path (calls of >= 2^17 windows, cut into 2-4
- * parts, each packed and copied by the copy engine while the previous part
- * counts; or AC_STAGE_EARLY=0): a job is sent without its N bitmap when it holds
- * no N and without window descriptors when its windows have one length.  -1 = no
+ * itself and counts it while later jobs are still being packed, and each
+ * candidate group's last workgroup stores its counts and error bits, tagged with
+ * the call's generation, into pinned memory, which the host polls.  0 = the DMA
+ * path (calls of >= 2^17 windows, cut into 2-4 parts, each packed and copied by
+ * the copy engine while the previous part counts; or AC_STAGE_EARLY=0).  Either
+ * way a job is sent without its N bitmap when no window needs it (no N, or, for
+ * equal windows, every N inside the window's inline record) and without window
+ * descriptors when its windows have one length.  -1 = no
  * call yet.  ac_error_count_jobs_submit takes the early launch for one-part calls
  * too (its counts and errors go to device memory; ac_check reports the errors).
  */

@@ -334,8 +334,8 @@ def early_rotation(calls=30):
 def test_early_launch_rotating_inputs_bit_exact(mode):
     """The early-launch stage (ac_stage_mode 2): the kernel is launched before the host
     packs (mode 2: after the first job, which the copy kernel sends ahead of it), copies
-    each later job into device memory itself once the host flags it, and the host polls a
-    completion word instead of the stream.  Staging slots alternate between calls, so
+    each later job into device memory itself once the host flags it, and the host polls the
+    generation-tagged counts instead of the stream.  Staging slots alternate between calls, so
     rotating three different workloads through one context makes every call land on a slot
     that last held other data: any stale line read or early completion shows up as a wrong
     count.  In a child process per mode (AC_STAGE_EARLY is read once per process)."""
