@@ -1519,6 +1519,8 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
     uint64_t total_w = 0;
     for (uint32_t j = 0; j < p.n; ++j)
         if (jobs[j].n_kmers) total_w += p.hi[j] - p.lo[j];
+    // (tasks of 128 windows, or the first tasks of every job packed first, were slower: the claims
+    // contend on the pool's one state line, profiles/r03_m8/ab.log)
     const uint64_t per = std::max<uint64_t>(256, std::min<uint64_t>(65536, total_w / (4ull * pool.size()) + 1));
     std::vector<Task> tasks;
     for (uint32_t j = 0; j < p.n; ++j) {
