@@ -350,7 +350,7 @@ struct NRecord {
 // such dwords to the 16 bytes of four code words; N: one compare to a k-mask.
 __attribute__((target("avx512f,avx512bw,avx512vl"))) uint32_t pack_range_avx512(
     const uint8_t* bases, const uint64_t* offset, const uint32_t* length, uint32_t w0, uint32_t w1, uint64_t first,
-    uint32_t* codes, uint32_t* nmask, uint64_t* start_out, uint32_t* len_out, bool rec) {
+    uint32_t* codes, uint32_t* nmask, uint64_t* start_out, uint32_t* len_out, bool records) {
     const __m512i three = _mm512_set1_epi8(3);
     uint32_t flags = 0;
     const __m512i pair = _mm512_set1_epi16(0x0401);
@@ -359,12 +359,16 @@ __attribute__((target("avx512f,avx512bw,avx512vl"))) uint32_t pack_range_avx512(
     for (uint32_t w = w0; w < w1; ++w) {
         const uint8_t* src = bases + offset[w];
         const uint32_t len = length[w];
-        start_out[w - w0] = pos;
-        len_out[w - w0] = len;
+        const bool rec = records && nrec_bits(len) != 0u;  // (no room: a plain window)
+        if (!rec) {  // (equal windows with records: places by arithmetic, no descriptors needed)
+            start_out[w - w0] = pos;
+            len_out[w - w0] = len;
+        }
         const uint64_t span = image_span(len);
         uint8_t* cw = (uint8_t*)(codes + pos / 16);
         uint8_t* nw = (uint8_t*)(nmask + pos / 32);
         NRecord nr(rec ? len : 0u);
+        uint64_t isns[4] = {0, 0, 0, 0};  // (records: the N bits, stored only if the record overflows)
         for (uint32_t b = 0; b < span; b += 64) {
             const uint32_t left = len > b ? len - b : 0u;
             const __mmask64 m = left >= 64 ? ~0ull : ((1ull << left) - 1ull);
@@ -376,14 +380,21 @@ __attribute__((target("avx512f,avx512bw,avx512vl"))) uint32_t pack_range_avx512(
             const __m128i c = _mm512_cvtepi32_epi8(t);
             if (span - b >= 64) {
                 _mm_storeu_si128((__m128i*)(cw + b / 4), c);
-                std::memcpy(nw + b / 8, &isn, 8);
+                if (!rec) std::memcpy(nw + b / 8, &isn, 8);
             } else {  // the last 32 bases of the span: half the words (the next window's follow)
                 _mm_storel_epi64((__m128i*)(cw + b / 4), c);
                 const uint32_t lo = (uint32_t)isn;
-                std::memcpy(nw + b / 8, &lo, 4);
+                if (!rec) std::memcpy(nw + b / 8, &lo, 4);
             }
+            if (rec && b < 256) isns[b / 64] = isn;
         }
-        flags |= nr.finish(codes + pos / 16);
+        const uint32_t f = nr.finish(codes + pos / 16);
+        if (f & PACK_OVERFLOW)  // (a record window spans <= 256 bases: 4 steps)
+            for (uint32_t b = 0; b < span; b += 32) {
+                const uint32_t word = (uint32_t)(isns[b / 64] >> (b % 64));
+                std::memcpy(nw + b / 8, &word, 4);
+            }
+        flags |= f;
         pos += span;
     }
     return flags;
@@ -392,17 +403,21 @@ __attribute__((target("avx512f,avx512bw,avx512vl"))) uint32_t pack_range_avx512(
 template <bool AVX2>
 uint32_t pack_range_impl(const uint8_t* bases, const uint64_t* offset, const uint32_t* length, uint32_t w0,
                          uint32_t w1, uint64_t first, uint32_t* codes, uint32_t* nmask, uint64_t* start_out,
-                         uint32_t* len_out, bool rec) {
+                         uint32_t* len_out, bool records) {
     uint32_t flags = 0;
     uint64_t pos = first;
     alignas(32) uint8_t tail[32];
+    uint32_t scratch[8];  // (records: the window's N-mask words, stored only if the record overflows)
     for (uint32_t w = w0; w < w1; ++w) {
         const uint8_t* src = bases + offset[w];
         const uint32_t len = length[w];
-        start_out[w - w0] = pos;
-        len_out[w - w0] = len;
+        const bool rec = records && nrec_bits(len) != 0u;  // (no room: a plain window)
+        if (!rec) {
+            start_out[w - w0] = pos;
+            len_out[w - w0] = len;
+        }
         uint32_t* cw = codes + pos / 16;
-        uint32_t* nw = nmask + pos / 32;
+        uint32_t* nw = rec ? scratch : nmask + pos / 32;
         const uint32_t full = len / 32;
         for (uint32_t b = 0; b < full; ++b) {
             if (AVX2) pack32_avx2(src + 32 * b, cw + 2 * b, nw + b);
@@ -417,20 +432,31 @@ uint32_t pack_range_impl(const uint8_t* bases, const uint64_t* offset, const uin
         NRecord nr(rec ? len : 0u);
         for (uint32_t b = 0; b < (len + 31u) / 32u; ++b)
             if (nw[b]) nr.add(nw[b], 32u * b);
-        flags |= nr.finish(cw);
+        const uint32_t f = nr.finish(cw);
+        if (f & PACK_OVERFLOW) std::memcpy(nmask + pos / 32, scratch, sizeof(uint32_t) * ((len + 31u) / 32u));
+        flags |= f;
         pos += image_span(len);
     }
     return flags;
 }
 
+// (AC_PACK_ISA=1 / 0: test builds of the AVX2 / scalar packers on an AVX-512 host, tests/test_pack_records.py)
 bool have_avx2() {
+#if defined(AC_PACK_ISA) && AC_PACK_ISA < 1
+    return false;
+#else
     static const bool v = __builtin_cpu_supports("avx2");
     return v;
+#endif
 }
 
 bool have_avx512() {
+#if defined(AC_PACK_ISA) && AC_PACK_ISA < 2
+    return false;
+#else
     static const bool v = __builtin_cpu_supports("avx512bw") && __builtin_cpu_supports("avx512vl");
     return v;
+#endif
 }
 
 __attribute__((target("avx512f"))) uint64_t span_scan_avx512(const uint32_t* len, uint32_t n, uint32_t f,

@@ -127,7 +127,9 @@ uint64_t span_scan(const uint32_t* len, uint32_t n, uint32_t* first, uint32_t* d
 // len_out[w - w0].  `codes` / `nmask` are the image's word arrays (indexed by
 // absolute image base).  Dna5 ordinals: 0..3 = A C G T, anything else = N.
 // `records`: the windows are equal (one length) and each gets its inline N
-// record (nrec.h; windows whose length leaves no room get none).  Returns the
+// record (nrec.h; the caller has checked that their length leaves room); their
+// start / length are not written, and their N-bitmap words only for a window
+// whose record overflowed (the kernel reads no others).  Returns the
 // PACK_* bits of the range: PACK_HAS_N = some window holds an N, PACK_OVERFLOW =
 // some window's N bases did not fit its record (its N-bitmap words are needed).
 constexpr uint32_t PACK_HAS_N = 1u, PACK_OVERFLOW = 2u;

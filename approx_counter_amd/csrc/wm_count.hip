@@ -58,7 +58,9 @@ constexpr int WAVES_PER_BLOCK = AC_WAVES_PER_BLOCK;
 // computed from them.
 }  // namespace
 __device__ uint64_t g_stamps[1 << 21];
-__device__ uint64_t g_stage_stamps[64];  // per segment: [s*4] final header seen by the poller, [s*4+1] its first progress record, [s*4+2] last chunk in
+__device__ uint64_t g_stage_stamps[64];  // per segment s, at [s*8 + i]: 0 final header seen by the poller, 1 its first
+                                         // progress record, 2 last chunk in, 3 first record past the k-mers, 4 first
+                                         // codes chunk flagged
 namespace {
 __device__ __forceinline__ void stamp(uint64_t wave, int i) {
     if ((threadIdx.x & 63u) == 0 && wave < (1u << 18)) {
@@ -76,7 +78,7 @@ __device__ __forceinline__ void stamp_val(uint64_t wave, int i, uint64_t v) {
     if ((threadIdx.x & 63u) == 0 && wave < (1u << 18)) g_stamps[wave * 8 + i] = v;
 }
 __device__ __forceinline__ void stage_stamp(uint32_t si, int i) {
-    if ((threadIdx.x & 63u) == 0) g_stage_stamps[si * 4 + i] = __builtin_amdgcn_s_memrealtime();
+    if ((threadIdx.x & 63u) == 0) g_stage_stamps[si * 8 + i] = __builtin_amdgcn_s_memrealtime();
 }
 #else
 __device__ __forceinline__ void stamp(uint64_t, int) {}
@@ -247,6 +249,9 @@ struct BlockLds {
     uint32_t stage_r;
 };
 
+#ifndef AC_COPY_AHEAD
+#define AC_COPY_AHEAD 32  // chunks a copier may run ahead of its segment's copied count (0: no limit; 8 / 16 / 32 measured, profiles/r03_m10/ab.log)
+#endif
 #ifndef AC_STAGE_LOAD_AUX
 #define AC_STAGE_LOAD_AUX 2  // cache policy of the staging copy's loads: nt (A/B builds: 17 = sc0 sc1)
 #endif
@@ -345,6 +350,7 @@ __device__ __attribute__((noinline)) bool stage_copy(const uint8_t* src, uint8_t
                 }
                 if (verdict != ~0u && ready > published && ready <= chunks * AC_STAGE_CHUNK) {
                     if (published == 0) stage_stamp(si, 1);
+                    if (published <= pre_chunks * AC_STAGE_CHUNK && ready > pre_chunks * AC_STAGE_CHUNK) stage_stamp(si, 3);
                     if (lane < AC_STAGE_REPL)  // every replica in one wave instruction
                         __hip_atomic_store(sw.avail + lane * AC_QUEUE_LINE, ready, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
@@ -382,6 +388,19 @@ __device__ __attribute__((noinline)) bool stage_copy(const uint8_t* src, uint8_t
             if (stage_late(t0)) return false;
             __builtin_amdgcn_s_sleep(8);
         }
+#if AC_COPY_AHEAD
+        // In chunk order: at most AC_COPY_AHEAD chunks of the segment in flight ahead of the copied
+        // count, so the first windows' chunks are not held up behind the whole region's PCIe reads
+        // (a segment packed before the poller's first look released all its copiers at once and the
+        // first codes chunk landed anywhere in the next 5-18 us: profiles/r03_m9/stamps.log).
+        if (x >= AC_COPY_AHEAD) {
+            uint32_t* my_done = sw.done + (x % AC_STAGE_REPL) * AC_QUEUE_LINE;
+            while (wave_load(my_done) < x - AC_COPY_AHEAD) {
+                if (stage_late(t0)) return false;
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+#endif
         if (limit > lo) {
             // range-checked descriptors: bytes past the valid prefix read as 0 and are not stored
             const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)src, 0, (int)limit, 0x00020000);
@@ -403,6 +422,7 @@ __device__ __attribute__((noinline)) bool stage_copy(const uint8_t* src, uint8_t
         if (lane < AC_STAGE_REPL)
             prev = __hip_atomic_fetch_add(sw.done + lane * AC_QUEUE_LINE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (__builtin_amdgcn_readfirstlane(prev) + 1u == chunks) stage_stamp(si, 2);  // (diagnostic builds) last chunk in
+        if (x == pre_chunks) stage_stamp(si, 4);  // (diagnostic builds) first codes chunk in
     }
 }
 
@@ -604,7 +624,10 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
     const uint32_t* codes_p = sg.codes;
     const uint32_t* nmask_p = sg.nmask;
     // (an N-free image: a zero-sized N-bitmap descriptor, whose loads all return 0 without a memory access)
-    uint32_t code_bytes = (uint32_t)(sg.n_bases >> 2), nmask_bytes = has_n ? (uint32_t)(sg.n_bases >> 3) : 0u;
+    // (a segment with inline N records never fetches bitmap words with its windows: only a window
+    // whose record overflowed reads its own, through a descriptor made for it)
+    uint32_t code_bytes = (uint32_t)(sg.n_bases >> 2),
+             nmask_bytes = (has_n && !sg.nrec) ? (uint32_t)(sg.n_bases >> 3) : 0u;
     asm volatile("" : "+s"(codes_p), "+s"(nmask_p), "+s"(code_bytes), "+s"(nmask_bytes));
     Image im;
     im.codes = __builtin_amdgcn_make_buffer_rsrc((void*)codes_p, 0, (int)code_bytes, 0x00020000);
@@ -760,7 +783,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
         partial = false;
         if (r == ~0u) return false;
         has_n = r;
-        nmask_bytes = has_n ? (uint32_t)(g_nbases >> 3) : 0u;
+        nmask_bytes = (has_n && rec_lane == ~0u) ? (uint32_t)(g_nbases >> 3) : 0u;
         im.nmask = __builtin_amdgcn_make_buffer_rsrc((void*)nmask_p, 0, (int)nmask_bytes, 0x00020000);
         return true;
     };
@@ -799,13 +822,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
     uint32_t nlen = 0;
     Fetch nf = {0u, 0u};
     const uint32_t lane_off = (lane < 16u ? lane : (lane - 16u) & 7u) << 2;  // this lane's word of a segment, in bytes
-    // (staged: did the next window's fetch read the N bitmap -- the descriptor changes when the
-    // segment completes; a window whose record overflowed needs its bitmap words)
-    bool nf_full = false;
-    auto fetch_next = [&](uint64_t b) __attribute__((always_inline)) {
-        tid_fetch(nf, im, b, lane, lane_off);
-        if constexpr (STAGED) nf_full = nmask_bytes != 0u;
-    };
+    auto fetch_next = [&](uint64_t b) __attribute__((always_inline)) { tid_fetch(nf, im, b, lane, lane_off); };
     if (item < n_items) {
         desc(w, nbase, nlen);
         // (staged: after the table barrier -- a wave waiting for its first window must not hold
@@ -860,7 +877,6 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
         // issued: inside the chunk loop hipcc would otherwise wait for both.
         uint32_t f0 = tid_word(nf, lane);
         asm volatile("" : "+v"(f0));
-        const bool f0_full = STAGED ? nf_full : has_n != 0u;
         const uint32_t wn = w + 1;
         const bool last = wn >= item_end;  // the item's last window: claim the next item
         uint32_t nitem = n_items;
@@ -877,17 +893,20 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
             const uint32_t rw = __builtin_amdgcn_readlane(f0, rec_lane);
             const uint32_t c = rw >> 29;
             if (c == NREC_OVERFLOW) {
-                bool have = f0_full;
+                bool have = false;
                 if constexpr (STAGED) {
-                    if (!have && partial) {  // wait for the whole segment (its N bitmap)
+                    if (partial) {  // wait for the whole segment (its N bitmap)
                         const uint64_t g = stage_gate(st_words, sg.stage_gen, sg.stage_chunks, blockIdx.x % AC_STAGE_REPL,
                                                       a.gen, 0u, ~0u, a.err);
                         if (!completed(__builtin_amdgcn_readfirstlane((uint32_t)g))) stage_ok = false;
                     }
                 }
-                if (!have && has_n && stage_ok) {
+                if (has_n && stage_ok) {  // this window's N-mask words from the bitmap
+                    Image full = im;
+                    full.nmask = __builtin_amdgcn_make_buffer_rsrc((void*)nmask_p, 0, (int)(uint32_t)(g_nbases >> 3),
+                                                                   0x00020000);
                     Fetch ff = {0u, 0u};
-                    tid_fetch(ff, im, base, lane, lane_off);
+                    tid_fetch(ff, full, base, lane, lane_off);
                     uint32_t v = tid_word(ff, lane);
                     asm volatile("" : "+v"(v));
                     if (lane >= 16u) f0 = v;

@@ -54,8 +54,9 @@ def main():
         print("                          p0      p10     p50     p90    p100  (us)")
         for s in np.unique(seg):
             m = seg == s
-            print(f" seg {s}: first progress seen {(stage[4 * s + 1] - t0) / 100:7.1f}, final header seen "
-                  f"{(stage[4 * s] - t0) / 100:7.1f}, last chunk in {(stage[4 * s + 2] - t0) / 100:7.1f}")
+            us_of = lambda i: (stage[8 * s + i] - t0) / 100  # noqa: E731
+            print(f" seg {s}: first progress seen {us_of(1):7.1f}, first codes progress {us_of(3):7.1f}, first codes "
+                  f"chunk in {us_of(4):7.1f}, final header seen {us_of(0):7.1f}, last chunk in {us_of(2):7.1f}")
             print("   entry           ", pct(us[m, 0]))
             wait_end = (raw[:, 7] - t0) / 100.0
             w0 = m & (np.arange(n) % 4 == 0)
