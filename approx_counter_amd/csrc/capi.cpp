@@ -52,6 +52,13 @@ struct ac_ctx {
     // working set (table keys, table counts, small scalars + histogram, forbidden, gather out)
     void* s_buf[4] = {nullptr, nullptr, nullptr, nullptr};
     size_t s_cap[4] = {0, 0, 0, 0};
+    // what the upload found about each slot's image: equal windows back to back (their length,
+    // else AC_NO_ULEN) and no N anywhere, so the count launch can take the EQ kernel and skip the
+    // N bitmap; keyed by the device image it describes
+    const uint32_t* s_codes[4] = {nullptr, nullptr, nullptr, nullptr};
+    uint32_t s_ulen[4] = {AC_NO_ULEN, AC_NO_ULEN, AC_NO_ULEN, AC_NO_ULEN};
+    bool s_no_n[4] = {false, false, false, false};
+    uint64_t s_windows[4] = {0, 0, 0, 0}, s_bases[4] = {0, 0, 0, 0};
     // (+ the partitioned path's keys, parts, tmp, h1/h2/stot, bstart, phist: e_buf[6..11])
     void* e_buf[12] = {};
     size_t e_cap[12] = {};
@@ -909,6 +916,19 @@ ac_status ac_sample_upload_slot(ac_ctx* ctx, int slot, const ac_windows* host, a
     dev->length = (const uint32_t*)at[3];
     dev->n_windows = host->n_windows;
     dev->n_bases = host->n_bases;
+    // equal windows back to back at ceil32(length) strides (the CLI's samples: every start window
+    // sl bases, every end window sl + 1), and an N-free image
+    uint32_t ulen = host->n_windows ? host->length[0] : AC_NO_ULEN;
+    const uint64_t stride = ((uint64_t)ulen + 31u) & ~31ull;
+    for (uint32_t i = 0; i < host->n_windows && ulen != AC_NO_ULEN; ++i)
+        if (host->length[i] != ulen || host->start[i] != (uint64_t)i * stride) ulen = AC_NO_ULEN;
+    uint32_t any_n = 0;
+    for (uint64_t i = 0; i < host->n_bases / 32; ++i) any_n |= host->nmask[i];
+    ctx->s_codes[slot] = dev->codes;
+    ctx->s_ulen[slot] = ulen;
+    ctx->s_no_n[slot] = any_n == 0u;
+    ctx->s_windows[slot] = host->n_windows;
+    ctx->s_bases[slot] = host->n_bases;
     return AC_OK;
 }
 
@@ -1173,7 +1193,28 @@ ac_status ac_error_count_samples(ac_ctx* ctx, uint32_t k, const ac_sample_job* j
         seg[j].counts = (uint32_t*)ctx->d_buf[5] + base;
         base += jobs[j].n_kmers;
     }
-    if (ac_status rc = launch(ctx, k, seg, n_jobs, st, true)) return rc;
+    // images this context uploaded: their equal-window / N-free findings (others: the general form)
+    uint32_t ulen[AC_MAX_JOBS];
+    bool no_n[AC_MAX_JOBS];
+    for (uint32_t j = 0; j < n_jobs; ++j) {
+        ulen[j] = AC_NO_ULEN;
+        no_n[j] = false;
+        for (int sl = 0; sl < AC_MAX_JOBS; ++sl)
+            if (ctx->s_codes[sl] && ctx->s_codes[sl] == jobs[j].sample.codes &&
+                jobs[j].sample.nmask == (const uint32_t*)((const char*)ctx->s_codes[sl] +
+                                                          (sizeof(uint32_t) * (ctx->s_bases[sl] / 16) + 255) / 256 * 256) &&
+                jobs[j].sample.n_windows == ctx->s_windows[sl] && jobs[j].sample.n_bases == ctx->s_bases[sl] &&
+                (const char*)jobs[j].sample.length >= (const char*)ctx->s_buf[sl] &&
+                (const char*)jobs[j].sample.length < (const char*)ctx->s_buf[sl] + ctx->s_cap[sl]) {
+                ulen[j] = ctx->s_ulen[sl];
+                no_n[j] = ctx->s_no_n[sl];
+            }
+        // (the launch's own check: equal windows must fit the image)
+        if (ulen[j] != AC_NO_ULEN &&
+            (uint64_t)jobs[j].sample.n_windows * (((uint64_t)ulen[j] + 31u) & ~31ull) > jobs[j].sample.n_bases)
+            ulen[j] = AC_NO_ULEN;
+    }
+    if (ac_status rc = launch(ctx, k, seg, n_jobs, st, true, nullptr, 0, 0, no_n, ulen)) return rc;
     ctx->h_counts.resize(total);
     AC_HIP(ctx, hipMemcpyAsync(ctx->h_counts.data(), ctx->d_buf[5], sizeof(uint32_t) * total, hipMemcpyDeviceToHost, st));
     if (ac_status rc = ac_check(ctx, st)) return rc;  // synchronises the stream
@@ -1383,7 +1424,8 @@ struct JobPlan {
 // cfg4 (2M windows) step p50 10.26-10.31 ms in four parts, 10.42-10.49 in three,
 // 11.27 in two (13.3 in one, r02_stage_parts_ab.log); cfg3 (200k windows)
 // 3.27-3.29 ms in two vs 3.24-3.40 one-part with round 2's (since removed) zero-copy / DMA chooser
-// and 3.42 one-part DMA.
+// and 3.42 one-part DMA.  Eight parts from 2^20 windows: cfg4 9.77-9.86 vs 9.79-9.96 ms in four
+// (profiles/r03_m14/parts_ab.log, round 3), not kept.
 constexpr uint64_t STAGE_PARTS2_MIN_WINDOWS = 1ull << 17, STAGE_PARTS4_MIN_WINDOWS = 1ull << 19;
 int stage_parts(uint64_t total_w) {
     return total_w >= STAGE_PARTS4_MIN_WINDOWS ? 4 : total_w >= STAGE_PARTS2_MIN_WINDOWS ? 2 : 1;
