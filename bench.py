@@ -441,13 +441,16 @@ def main():
                        "candidates": n_c, "kmer_bp_per_step": units_job, "kmer_bp_per_rank_step": units_rank,
                        "stage": ("Dna5 host buffers -> "
                                  + ("1 fused count launch issued first, then per read end: pack (host pool, "
-                                    "pinned) + flag; the kernel copies each flagged end into HBM itself and counts it "
-                                    "while the next end is packed" if stage_path == "early-launch"
-                                    else ("per read end: pack (host pool, pinned), copy into HBM while the next end "
-                                          "is packed -> 1 fused launch (>= 2^17 windows: 2 parts, >= 2^19: 4)"))
+                                    "pinned; N positions inline in each window's slot) + progress records; the kernel "
+                                    "copies each 4 KB chunk into HBM itself as it is packed and counts a window as "
+                                    "soon as its chunk is in" if stage_path == "early-launch"
+                                    else ("per part (>= 2^17 windows: 2 parts, >= 2^19: 4): pack (host pool, pinned), "
+                                          "copy-engine DMA into HBM while the previous part counts"))
                                  + " (both ends)"
                                  + (" -> RCCL all-reduce -> counts D2H" if world > 1 else
-                                    " -> counts stored to pinned host memory by the kernel, completion polled")),
+                                    (" -> counts tagged with the call's generation stored to pinned host memory by "
+                                     "each candidate group, polled" if stage_path == "early-launch"
+                                     else " -> counts stored to pinned host memory by the kernel"))),
                        "stage_path": stage_path,
                        "parallelism": (f"{args.scaling} window shards x{world}, "
                                        f"{'RCCL' if backend == 'nccl' else backend} all-reduce of counts")
