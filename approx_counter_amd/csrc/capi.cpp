@@ -1805,7 +1805,10 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
                 pool.finish();
                 return st;
             }
-        constexpr uint64_t PUBLISH_STEP = 16384;  // bytes of new prefix worth a header store
+#ifndef AC_PUBLISH_STEP
+#define AC_PUBLISH_STEP 16384
+#endif
+        constexpr uint64_t PUBLISH_STEP = AC_PUBLISH_STEP;  // bytes of new prefix worth a header store
         // per job: its tasks in claim order
         std::vector<uint32_t> jt[AC_MAX_JOBS];
         for (uint32_t t = 0; t < (uint32_t)tasks.size(); ++t) jt[tasks[t].job].push_back(t);

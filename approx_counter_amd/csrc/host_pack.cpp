@@ -53,7 +53,7 @@ WorkPool::~WorkPool() {
 
 void WorkPool::drain(uint32_t gen, uint32_t upto, uint32_t max_tasks) {
     const Job& job = jobs_[gen & 1u];
-    for (uint32_t ran = 0; ran < max_tasks; ++ran) {
+    for (uint32_t ran = 0; ran < max_tasks;) {
         uint64_t s = state_.load(std::memory_order_acquire);
         if ((uint32_t)(s >> 32) != gen) return;  // the job is over (a later one is published)
         const uint32_t i = (uint32_t)s;
@@ -63,6 +63,7 @@ void WorkPool::drain(uint32_t gen, uint32_t upto, uint32_t max_tasks) {
         if (!state_.compare_exchange_weak(s, s + 1, std::memory_order_acq_rel, std::memory_order_relaxed)) continue;
         (*fn)(i);
         jobs_[gen & 1u].done.fetch_add(1, std::memory_order_release);
+        ++ran;
     }
 }
 
