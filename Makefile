@@ -16,7 +16,7 @@ LIB := $(LIBDIR)/libapprox_counter_amd.so
 OBJDIR := build/obj
 
 DEV_SRC := $(CSRC)/wm_count.hip $(CSRC)/exact_count.hip $(CSRC)/capi.cpp $(CSRC)/host_pack.cpp
-HDRS := include/approx_counter_amd.h $(CSRC)/wm_count.h $(CSRC)/exact_count.h $(CSRC)/host_pack.h
+HDRS := include/approx_counter_amd.h include/approx_counter_amd_testing.h $(CSRC)/wm_count.h $(CSRC)/exact_count.h $(CSRC)/host_pack.h
 
 CXX ?= g++
 HOST_CXXFLAGS ?= -O3 -std=c++17 -fPIC -Wall -Wextra

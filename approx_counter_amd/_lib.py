@@ -15,6 +15,8 @@ LIB_PATH = os.path.join(_HERE, "lib", "libapprox_counter_amd.so")
 # Kernel-tuning experiments (tools/variants.sh) point this at another build of the same sources.
 LIB_PATH = os.environ.get("APPROX_COUNTER_AMD_LIB", LIB_PATH)
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "approx_counter_amd.h")
+# test-only entry points of the same library (never used by the product path)
+TESTING_HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "approx_counter_amd_testing.h")
 
 AC_OK, AC_ERR_INVALID, AC_ERR_DEVICE, AC_ERR_NOMEM, AC_ERR_INTERNAL = 0, 1, 2, 3, 4
 AC_MAX_SEGS = 4
@@ -130,6 +132,8 @@ def load():
     L.ac_check.restype = ctypes.c_int
     L.ac_stage_mode.argtypes = [vp]
     L.ac_stage_mode.restype = ctypes.c_int
+    L.ac_testing_stage_hooks.argtypes = [ctypes.c_uint32]
+    L.ac_testing_stage_hooks.restype = ctypes.c_uint32
     L.ac_exact_path.argtypes = [vp]
     L.ac_exact_path.restype = ctypes.c_int
     pint = ctypes.POINTER(ctypes.c_int)
@@ -145,8 +149,9 @@ def load():
 
 
 def header_functions():
-    """Names of the functions declared in include/approx_counter_amd.h."""
-    text = open(HEADER_PATH).read()
+    """Names of the functions declared in include/approx_counter_amd.h and the
+    test-only include/approx_counter_amd_testing.h."""
+    text = open(HEADER_PATH).read() + open(TESTING_HEADER_PATH).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     return sorted(set(re.findall(r"\b(ac_[a-z_]+)\s*\(", text)))
 

@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "approx_counter_amd.h"
+#include "approx_counter_amd_testing.h"
 #include "exact_count.h"
 #include "host_pack.h"
 #include "wm_count.h"
@@ -56,6 +57,7 @@ struct ac_ctx {
     // else AC_NO_ULEN) and no N anywhere, so the count launch can take the EQ kernel and skip the
     // N bitmap; keyed by the device image it describes
     const uint32_t* s_codes[4] = {nullptr, nullptr, nullptr, nullptr};
+    const uint64_t* s_start[4] = {nullptr, nullptr, nullptr, nullptr};
     uint32_t s_ulen[4] = {AC_NO_ULEN, AC_NO_ULEN, AC_NO_ULEN, AC_NO_ULEN};
     bool s_no_n[4] = {false, false, false, false};
     uint64_t s_windows[4] = {0, 0, 0, 0}, s_bases[4] = {0, 0, 0, 0};
@@ -263,6 +265,17 @@ ac_status check_layout(ac_ctx* ctx, const ac_windows& s) {
 // Staged launch (the early-launch stage): the kernel copies each
 // segment's region from src (the pinned block) to dst once the host flags it in
 // host_hdr, and reports its completion there.
+// Copier workgroups of a large staged launch (AC_COPIER_WGS overrides, for A/B runs): 16 = 2 per XCD,
+// 4 CUs' worth of resident slots, 64 waves, enough to keep the AC_COPY_AHEAD window of chunk reads in
+// flight over PCIe.
+uint32_t stage_copier_wgs() {
+    static const uint32_t v = [] {
+        const char* e = std::getenv("AC_COPIER_WGS");
+        return e ? (uint32_t)std::max(1, std::atoi(e)) : 16u;
+    }();
+    return v;
+}
+
 struct StageLaunch {
     uint32_t gen = 0;
     uint32_t* host_hdr = nullptr;
@@ -455,6 +468,14 @@ ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hi
         a.err_out = stage->err_out;
         a.tag = stage->tag;
         a.grp_err = stage->grp_err;
+        // Who stages (wm_count.h LaunchArgs::copier_wgs): while a call's tickets (its chunks and one
+        // host poller per segment) stay below half the workgroups, every workgroup's wave 0 claims
+        // them -- those chunks are packed within microseconds of the launch (cfg2: 164 tickets,
+        // 1,024 workgroups).  Above that, chunks keep arriving over the whole packing time and a
+        // workgroup holding one would hold its waves with it, so a few copier workgroups stage
+        // everything and the others count as the chunks land.
+        const uint64_t blocks = (wave + AC_WAVES_PER_BLOCK - 1) / AC_WAVES_PER_BLOCK;
+        if (2ull * (total_chunks + n) > blocks) a.copier_wgs = (uint32_t)std::min<uint64_t>(blocks, stage_copier_wgs());
     }
     // the equal-window instantiation when every live segment has equal windows (their fit in the
     // image checked above)
@@ -896,6 +917,12 @@ ac_status ac_sample_upload_slot(ac_ctx* ctx, int slot, const ac_windows* host, a
     if (ac_status st = check_sample(ctx, host)) return st;
     if (ac_status st = check_layout(ctx, *host)) return st;  // on the host copy
     AC_HIP(ctx, hipSetDevice(ctx->device));
+    // the slot's notes describe its image only once the upload below has completed (a
+    // failure part way must not leave notes that a later count matches to a freed or partial buffer)
+    ctx->s_codes[slot] = nullptr;
+    ctx->s_start[slot] = nullptr;
+    ctx->s_ulen[slot] = AC_NO_ULEN;
+    ctx->s_no_n[slot] = false;
     const size_t sz[4] = {sizeof(uint32_t) * (host->n_bases / 16), sizeof(uint32_t) * (host->n_bases / 32),
                           sizeof(uint64_t) * host->n_windows, sizeof(uint32_t) * host->n_windows};
     const void* src[4] = {host->codes, host->nmask, host->start, host->length};
@@ -925,6 +952,7 @@ ac_status ac_sample_upload_slot(ac_ctx* ctx, int slot, const ac_windows* host, a
     uint32_t any_n = 0;
     for (uint64_t i = 0; i < host->n_bases / 32; ++i) any_n |= host->nmask[i];
     ctx->s_codes[slot] = dev->codes;
+    ctx->s_start[slot] = dev->start;
     ctx->s_ulen[slot] = ulen;
     ctx->s_no_n[slot] = any_n == 0u;
     ctx->s_windows[slot] = host->n_windows;
@@ -1204,6 +1232,7 @@ ac_status ac_error_count_samples(ac_ctx* ctx, uint32_t k, const ac_sample_job* j
                 jobs[j].sample.nmask == (const uint32_t*)((const char*)ctx->s_codes[sl] +
                                                           (sizeof(uint32_t) * (ctx->s_bases[sl] / 16) + 255) / 256 * 256) &&
                 jobs[j].sample.n_windows == ctx->s_windows[sl] && jobs[j].sample.n_bases == ctx->s_bases[sl] &&
+                jobs[j].sample.start == ctx->s_start[sl] &&
                 (const char*)jobs[j].sample.length >= (const char*)ctx->s_buf[sl] &&
                 (const char*)jobs[j].sample.length < (const char*)ctx->s_buf[sl] + ctx->s_cap[sl]) {
                 ulen[j] = ctx->s_ulen[sl];
@@ -1470,18 +1499,23 @@ hipError_t stage_blit_launch(const void* src_dev, void* dst, size_t bytes, hipSt
     return hipGetLastError();
 }
 
-// The early-launch stage for calls counted in one part on one device, synchronous calls and
-// submits alike (default: AC_STAGE_EARLY=1).  0 = the pack -> copy kernel -> launch order of
-// round 2; 2 = the first job sent ahead of the launch by the copy kernel, the others staged by
-// the count kernel; 3 (diagnostic) = every job sent ahead.  Same box, interleaved (profiles/r03_m2/summary.log): cfg2 step 0.141-0.143
-// vs 0.148-0.149 ms.
+// The early-launch stage for calls on one device, synchronous calls and submits alike (default:
+// AC_STAGE_EARLY=1).  0 = the pack -> copy kernel / copy engine -> launch order of round 2; 2 = the
+// first job sent ahead of the launch by the copy kernel, the others staged by the count kernel.
+// Same box, interleaved (profiles/r03_m2/summary.log): cfg2 step 0.141-0.143 vs 0.148-0.149 ms.
 int stage_early() {
     static const int v = [] {
         const char* e = std::getenv("AC_STAGE_EARLY");
-        return e ? std::max(0, std::min(3, std::atoi(e))) : 1;
+        return e ? std::max(0, std::min(2, std::atoi(e))) : 1;
     }();
     return v;
 }
+
+// Test-only hooks (ac_testing_stage_hooks, include/approx_counter_amd_testing.h; never set by the
+// product): AC_TESTING_UNFLAG_LAST leaves a call's last job unflagged, so the kernel's bounded wait
+// runs out (the synchronous call then retries through the DMA path); AC_TESTING_ALL_AHEAD sends every
+// job ahead of the staged launch (the staged kernel on resident input, a diagnostic of its own cost).
+std::atomic<uint32_t> g_test_hooks{0};
 
 // Some job has candidates and windows (a launch with work, so tagged counts to wait for).
 bool live_work(const ac_job* jobs, uint32_t n_jobs) {
@@ -1562,8 +1596,12 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
     for (uint32_t j = 0; j < p.n; ++j)
         if (jobs[j].n_kmers) total_w += p.hi[j] - p.lo[j];
     // (tasks of 128 windows, or the first tasks of every job packed first, were slower: the claims
-    // contend on the pool's one state line, profiles/r03_m8/ab.log)
-    const uint64_t per = std::max<uint64_t>(256, std::min<uint64_t>(65536, total_w / (4ull * pool.size()) + 1));
+    // contend on the pool's one state line, profiles/r03_m8/ab.log).  The early launch publishes
+    // progress a finished task at a time, so its tasks stay at most 2,048 windows (~20 us of one
+    // thread's packing): a large call's first windows then reach the GPU within tens of microseconds
+    // rather than after a 1/(4 x participants) share of the whole call.
+    const uint64_t per = std::max<uint64_t>(
+        256, std::min<uint64_t>(p.early ? 2048 : 65536, total_w / (4ull * pool.size()) + 1));
     std::vector<Task> tasks;
     for (uint32_t j = 0; j < p.n; ++j) {
         if (!jobs[j].n_kmers) continue;  // nothing to count: its windows are not needed
@@ -1738,7 +1776,8 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
         // sent before the launch by the copy kernel instead, stream-ordered ahead of it.
         // (AC_STAGE_EARLY=3, diagnostic: every job sent ahead, so the staged kernel runs on resident
         // input -- its own cost against the plain kernel's)
-        const uint32_t pre = stage_early() == 3 ? p.n : (stage_early() == 2 && p.n > 1) ? 1u : 0u;
+        const uint32_t hooks = g_test_hooks.load(std::memory_order_relaxed);
+        const uint32_t pre = (hooks & AC_TESTING_ALL_AHEAD) ? p.n : (stage_early() == 2 && p.n > 1) ? 1u : 0u;
         // (Packing the jobs' tasks interleaved, so both ends arrive together, was slower:
         // 0.144 vs 0.134 ms per cfg2 step -- each end's last chunk waits for its final header,
         // which then came ~27 us into the kernel for both; profiles/r03_stage/r03_early12_step3.log.)
@@ -1789,8 +1828,14 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
         };
         std::unique_ptr<Done[]> t_done(new Done[tasks.size() + 1]);
         for (size_t t = 0; t < tasks.size(); ++t) t_done[t].v.store(0, std::memory_order_relaxed);
+        const bool slow_host = (hooks & AC_TESTING_SLOW_HOST) != 0u;  // (test-only hook)
+        uint32_t slow_left = slow_host ? 12u : 0u;
         auto publish = [&](uint32_t j, uint64_t ready) {
             __atomic_store_n((uint64_t*)(hdr + j * AC_QUEUE_LINE + AC_HDR_PGEN), (ready << 32) | p.gen, __ATOMIC_RELEASE);
+            if (launched && slow_left) {
+                --slow_left;
+                std::this_thread::sleep_for(std::chrono::milliseconds(60));
+            }
         };
         const std::function<void(uint32_t)> pack_counted = [&](uint32_t t) {
             pack(t);
@@ -1838,10 +1883,8 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
             // bytes sent); with N the published prefix stays where the first N stopped it
             if (nn) publish(j, bytes);
             line[AC_HDR_INFO] = (uint32_t)bytes | (nn ? 0u : AC_HDR_INFO_HAS_N);
-            // (test hook: AC_STAGE_TEST_UNFLAGGED=1 leaves the last job unflagged, so the kernel's bounded
-            // wait runs out and the call must fail cleanly: tests/test_gpu_jobs.py)
-            static const bool unflag = std::getenv("AC_STAGE_TEST_UNFLAGGED") != nullptr;
-            if (!(unflag && j + 1 == p.n))
+            // (test-only hook: the last job left unflagged, tests/test_gpu_jobs.py)
+            if (!((hooks & AC_TESTING_UNFLAG_LAST) && j + 1 == p.n))
                 __atomic_store_n(&line[AC_HDR_FLAG], p.gen, __ATOMIC_RELEASE);  // the kernel's waves may go
             if (first_flag) mark(3);  // (AC_STAGE_TRACE: launch -> first job flagged, in "h2d_enq")
             first_flag = false;
@@ -1851,6 +1894,10 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
         // 312-window tasks) held every progress record back until it was done.  It still packs when
         // no worker has finished a task for 20 us (workers asleep or descheduled).
         const bool serial = pool.serial();
+        // ... except when packing, not publishing, is the bottleneck: a pool of <= 4 participants (a
+        // rank's share of the host) or a large call (the kernel counts faster than a few threads
+        // pack), where a task of its own delays the records by one task but adds a packer.
+        const bool caller_packs = !serial && (pool.size() <= 4 || total_w >= (1u << 16));
         uint32_t seen_done = 0, idle_polls = 0;
         auto last_seen = std::chrono::steady_clock::now();
         while (left_jobs) {
@@ -1868,7 +1915,7 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
                 }
             }
             if (serial && helped < (uint32_t)tasks.size()) pool.help(++helped);  // packs task helped - 1
-            else if (help_now) pool.help_one();
+            else if (help_now || caller_packs) pool.help_one();
             for (uint32_t j = 0; j < p.n; ++j) {
                 if (flagged[j] || (j > 0 && j <= pre && !flagged[j - 1])) continue;  // (pre: in job order)
                 const uint64_t base_off = p.off_codes[j] - p.off_kmers[j];
@@ -1882,10 +1929,12 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
                     ++nt[j];
                 }
                 if (ready[j] >= published[j] + PUBLISH_STEP || (nt[j] == nj && ready[j] > published[j])) {
-                    publish(j, ready[j]);
-                    published[j] = ready[j];
+                    // (test-only slow host: one step per record while its sleeps last)
+                    const uint64_t r = slow_left ? std::min(ready[j], published[j] + PUBLISH_STEP) : ready[j];
+                    publish(j, r);
+                    published[j] = r;
                 }
-                if (nt[j] == nj) {
+                if (nt[j] == nj && published[j] == ready[j]) {
                     if (ac_status st = finalize(j)) {
                         pool.finish();
                         (void)record_slot();
@@ -2017,13 +2066,13 @@ std::vector<std::vector<uint32_t>> part_cuts(const ac_job* jobs, uint32_t n_jobs
 
 }  // namespace
 
-extern "C" {
+namespace {
 
-ac_status ac_error_count_jobs(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint32_t n_jobs) {
-    if (ac_status st = check_jobs(ctx, k, jobs, n_jobs)) return st;
-    for (uint32_t j = 0; j < n_jobs; ++j)
-        if (jobs[j].n_kmers && !jobs[j].counts) return fail(ctx, AC_ERR_INVALID, "job counts is NULL");
-    if (n_jobs == 0) return AC_OK;
+// The synchronous jobs stage (ac_error_count_jobs).  allow_early = false: the DMA path whatever
+// AC_STAGE_EARLY says.  *stage_timeout: the early launch gave up waiting for the host's inputs.
+ac_status count_jobs_sync(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint32_t n_jobs, bool allow_early,
+                          bool* stage_timeout) {
+    *stage_timeout = false;
     // Units of work: on an ac_create_multi context one per device (shard g of
     // every job's windows on context g); on one device up to AC_STAGE_MAX_PARTS
     // parts on their own streams, the first launched with half the resident
@@ -2055,7 +2104,11 @@ ac_status ac_error_count_jobs(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint3
             units.push_back(u);
         }
     } else {
-        const int parts = total_w >= 2048 ? stage_parts(total_w) : 1;  // small calls: one launch
+        // The early launch takes every size in one part (large ones through copier workgroups); the
+        // copy-engine parts remain for AC_STAGE_EARLY=0.  (A region of 2^31 bytes or more falls back
+        // to one DMA part inside stage_and_launch.)
+        const bool early = allow_early && stage_early() && live_work(jobs, n_jobs);
+        const int parts = (!early && total_w >= 2048) ? stage_parts(total_w) : 1;
         const std::vector<std::vector<uint32_t>> cuts = part_cuts(jobs, n_jobs, parts);
         for (int q = 0; q < parts; ++q) {
             if (q > 0 && !ctx->part_stream[q])
@@ -2064,7 +2117,7 @@ ac_status ac_error_count_jobs(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint3
             u.plan.n = n_jobs;
             u.plan.slot = q;
             u.plan.scratch = q;
-            if (parts == 1 && stage_early() && live_work(jobs, n_jobs)) {
+            if (early) {
                 // one part: the early-launch stage (alternating slots 0 / 1, so a call never waits for
                 // the previous call's launch to retire before it packs)
                 u.plan.early = true;
@@ -2114,6 +2167,7 @@ ac_status ac_error_count_jobs(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint3
             g_trace.cur[6] += t - t_sync;
             t_sync = t;
         }
+        if (u.plan.early && (err_word & AC_DEVERR_STAGE)) *stage_timeout = true;
         if (ac_status st = device_error(u.c, err_word)) {
             if (first_err == AC_OK)
                 first_err = u.c != ctx ? fail(ctx, st, "shard " + std::to_string(g) + ": " + u.c->err) : st;
@@ -2141,6 +2195,29 @@ ac_status ac_error_count_jobs(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint3
     return first_err;
 }
 
+}  // namespace
+
+extern "C" {
+
+ac_status ac_error_count_jobs(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint32_t n_jobs) {
+    if (ac_status st = check_jobs(ctx, k, jobs, n_jobs)) return st;
+    for (uint32_t j = 0; j < n_jobs; ++j)
+        if (jobs[j].n_kmers && !jobs[j].counts) return fail(ctx, AC_ERR_INVALID, "job counts is NULL");
+    if (n_jobs == 0) return AC_OK;
+    bool stage_timeout = false;
+    const ac_status st = count_jobs_sync(ctx, k, jobs, n_jobs, true, &stage_timeout);
+    // An early launch whose host inputs stopped arriving for 0.5 s (a stalled host: the kernel's waits
+    // restart their clock on every bit of progress) skipped its work and said so: the call is run
+    // again through the DMA path, which has no such wait, instead of failing.
+    if (st != AC_OK && stage_timeout) {
+        std::fprintf(stderr, "[approx_counter_amd] early launch timed out waiting for the host; retrying via DMA\n");
+        return count_jobs_sync(ctx, k, jobs, n_jobs, false, &stage_timeout);
+    }
+    return st;
+}
+
+uint32_t ac_testing_stage_hooks(uint32_t flags) { return g_test_hooks.exchange(flags); }
+
 ac_status ac_error_count_jobs_submit(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint32_t n_jobs,
                                      uint32_t* d_counts, void* hip_stream) {
     if (ac_status st = check_jobs(ctx, k, jobs, n_jobs)) return st;
@@ -2161,7 +2238,8 @@ ac_status ac_error_count_jobs_submit(ac_ctx* ctx, uint32_t k, const ac_job* jobs
     // submit streams, ordered after the zeroing and joined back into the caller's stream.
     // Submits alternate between two sets of staging slots, so a submit packs while the
     // previous one's launch may still read its inputs.
-    const int parts = total_w >= 2048 ? stage_parts(total_w) : 1;
+    const bool early = stage_early() && live_work(jobs, n_jobs);  // every size in one part (as above)
+    const int parts = (!early && total_w >= 2048) ? stage_parts(total_w) : 1;
     const int set = (int)ctx->next_slot;
     ctx->next_slot ^= 1u;
     const std::vector<std::vector<uint32_t>> cuts = part_cuts(jobs, n_jobs, parts);
@@ -2187,11 +2265,12 @@ ac_status ac_error_count_jobs_submit(ac_ctx* ctx, uint32_t k, const ac_job* jobs
         p.slot = AC_STAGE_MAX_PARTS * (1 + set) + q;
         p.scratch = AC_STAGE_MAX_PARTS + q;
         // one part: the early launch, counts and errors into device memory (ac_check reads them)
-        p.early = parts == 1 && stage_early() && live_work(jobs, n_jobs);
+        p.early = early;
         if (ac_status rc = stage_and_launch(ctx, k, jobs, p, st, d_counts, q, (parts > 1 && q == 0) ? 2u : 0u,
                                             parts == 1))
             return rc;
         if (q > 0) AC_HIP(ctx, hipEventRecord(ctx->sub_ev[q], st));
+        if (q == 0) ctx->last_mode = p.early ? 2 : 0;
     }
     for (int q = 1; q < parts; ++q) AC_HIP(ctx, hipStreamWaitEvent(caller, ctx->sub_ev[q], 0));
     if (g_trace.on) {

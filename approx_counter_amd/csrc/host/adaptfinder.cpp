@@ -461,6 +461,9 @@ int main(int argc, char const** argv) {
                                                   &n_found, &had_n);
                 } catch (const std::exception& e) {
                     std::cerr << error_pref << "exact count failed: " << e.what() << std::endl;
+                    // the reference exported the earlier end's approximate count before reaching this end
+                    // (ADVICE r3): its own upload slot is intact, so count and write it first
+                    flush();
                     return 1;
                 }
             }

@@ -62,7 +62,9 @@ constexpr int waves_per_simd(int W) { return W == 2 ? 4 : 8; }
 #define AC_STAGE_SEG_LINES (4 + 2 * AC_STAGE_REPL)
 #define AC_STAGE_L_SEG(s) (1 + (s) * AC_STAGE_SEG_LINES)
 #define AC_STAGE_LINES (1 + AC_MAX_SEGS * AC_STAGE_SEG_LINES)
-#define AC_STAGE_TIMEOUT_TICKS 50000000ull  // 0.5 s of s_memrealtime (100 MHz): every wait is bounded
+// 0.5 s of s_memrealtime (100 MHz) WITHOUT PROGRESS: every wait is bounded, and its clock restarts
+// whenever the words it waits on advance (a large call may take far longer than this to pack)
+#define AC_STAGE_TIMEOUT_TICKS 50000000ull
 
 namespace acamd {
 
@@ -132,6 +134,12 @@ struct LaunchArgs {
     // and each candidate group stores its error snapshot (generation << 32 | bits) at grp_err[ticket index]
     uint32_t tag;
     uint64_t* grp_err;
+    // staged: 0 = wave 0 of every workgroup claims staging tickets of its own segment before it
+    // counts (small calls: the tickets run out after a few hundred workgroups); n > 0 = only
+    // workgroups 0 .. n-1 stage, every wave of them, every segment in order, then they count like
+    // the rest (large calls: thousands of chunks arrive over the whole packing time, and a
+    // workgroup holding a ticket would hold its waves until its chunk is packed)
+    uint32_t copier_wgs;
     uint32_t n_segs;
     uint32_t eq;  // every live segment has equal windows (ulen), checked on the host to fit its image
     uint32_t m;  // k-mer length

@@ -23,20 +23,26 @@
 //    patterns are INTERLEAVED in one 32-bit register: character i of pattern p
 //    sits at bit 31 - (i*P + p), so one logical right shift by P advances every
 //    pattern at once and the zero fill reaches every pattern's first character.
-//  * ~Eq is a table lookup, as in the textbook algorithm: each wave keeps a
-//    5 x 64-word LDS table (lane's ~Eq for A, C, G, T, and all ones for N) and
-//    reads one word per lane per text base with ds_read_addtid_b32, the
-//    address coming from M0 = 256 * character, two SALU ops from the
-//    wave-uniform 2-bit text held in an SGPR.  No VALU op per base for ~Eq.
+//  * W lane words per wave (words_for(P): 2 for P = 2, i.e. k = 11-16, else 1):
+//    each lane carries W x P candidates, and the W NFAs share every base's
+//    SALU work and text.
+//  * ~Eq is a table lookup, as in the textbook algorithm: each WORKGROUP (4
+//    waves, all on one candidate group) keeps one W x 5 x 64-word LDS table
+//    (per lane word: the lane's ~Eq for A, C, G, T, and all ones for N), built
+//    by its wave 0; every wave reads one word per lane, lane word and text base
+//    with ds_read_addtid_b32, the address coming from M0 = 256 * character,
+//    two SALU ops from the wave-uniform 2-bit text held in an SGPR.  No VALU op
+//    per base for ~Eq.
 //  * The NFA runs in generated inline-asm blocks (wm_tid_blocks.inc,
 //    tools/gen_tid_blocks.py): 8 full-rate VALU ops per base (v_or, v_lshrrev,
 //    v_bitop3 -- the forms that issue in 2 cycles per wave64 on gfx950,
 //    profiles/r01_ubench_valu.txt) + 1.5 of hit accumulation (AND3 over two
-//    bases) = 9.5 VALU ops per base for P candidates, scheduled skewed (row 0
-//    of base s, row 1 of base s-1, row 2 of base s-2 per step) so a wave has
-//    three independent dependency chains, with the LDS reads three bases ahead.
-//  * One wave per workgroup, so the table sits at LDS address 0 and M0 needs no
-//    per-wave add: per base 2 SALU + 1 LDS + 9.5 VALU.  The SALU is the
+//    bases) = 9.5 VALU ops per base and lane word (P candidates), scheduled
+//    skewed (row 0 of base s, row 1 of base s-1, row 2 of base s-2 per step) so
+//    a lane word has three independent dependency chains, with the LDS reads
+//    three bases ahead.
+//  * The table is the workgroup's first LDS object, at address 0, so M0 needs
+//    no per-wave add: per base 2 SALU + W LDS + 9.5 W VALU.  The SALU is the
 //    CU-shared resource the first table-driven version ran out of (5 SALU per
 //    base: no faster than computing ~Eq with 2 VALU ops; profiles/r01_kernel_log.md).
 //  * Integer-only VALU work: no MFMA.  Counts are uint32 atomics
@@ -167,8 +173,9 @@ __device__ __forceinline__ void load_desc_vec(const uint64_t* start, const uint3
     len = __builtin_amdgcn_readfirstlane(l);
 }
 
-// Per-wave ~Eq table: word c*64 + lane = the lane's ~Eq mask for character c
-// (A C G T, then N = all ones), read per base with ds_read_addtid_b32.
+// The workgroup's ~Eq table (shared by its waves): for lane word w, word w*320 + c*64 + lane =
+// the lane's ~Eq mask for character c (A C G T, then N = all ones), read per base with
+// ds_read_addtid_b32.
 template <int W>
 struct TidTable {
     uint32_t e[W * 5 * 64];  // lane word w's table at e[w * 320]
@@ -320,12 +327,13 @@ __device__ __attribute__((noinline)) bool stage_copy(const uint8_t* src, uint8_t
                                                      uint32_t* chunk_gen, uint32_t gen, uint32_t si) {
     const uint32_t lane = threadIdx.x & 63u;
     const StageWords sw = stage_words(words);
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     for (;;) {
         uint32_t c = 0;
         if (lane == 0) c = __hip_atomic_fetch_add(sw.claim, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         c = __builtin_amdgcn_readfirstlane(c);
         if (c > chunks) return true;
+        t0 = __builtin_amdgcn_s_memrealtime();  // (each ticket's wait is bounded on its own)
         if (c == 0) {  // the segment's host poller
             // The header's four words in ONE 16-byte system-scope load (one PCIe read): the host
             // stores the progress record as one 8-byte store and the flag after INFO, so a read
@@ -355,6 +363,7 @@ __device__ __attribute__((noinline)) bool stage_copy(const uint8_t* src, uint8_t
                         __hip_atomic_store(sw.avail + lane * AC_QUEUE_LINE, ready, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
                     published = ready;
+                    t0 = __builtin_amdgcn_s_memrealtime();  // the host is making progress
                 }
                 if (fin) {
                     stage_stamp(si, 0);
@@ -373,11 +382,13 @@ __device__ __attribute__((noinline)) bool stage_copy(const uint8_t* src, uint8_t
         const uint32_t x = c - 1u, lo = x * AC_STAGE_CHUNK, hi = lo + AC_STAGE_CHUNK;
         uint32_t* my_avail = sw.avail + (x % AC_STAGE_REPL) * AC_QUEUE_LINE;
         uint32_t limit = x < pre_chunks ? hi : 0u;  // bytes of the region known to be valid
+        uint32_t seen = 0;  // N-free bytes seen published (the wait's clock restarts when they grow)
         while (limit == 0u) {
             // both words in one wave instruction (lane 0: N-free bytes, lane 1: final seen)
             uint32_t v = 0;
             if (lane < 2u) v = __hip_atomic_load(lane ? sw.fin : my_avail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (__builtin_amdgcn_readlane(v, 0) >= hi) {
+            const uint32_t av = __builtin_amdgcn_readlane(v, 0);
+            if (av >= hi) {
                 limit = hi;
                 break;
             }
@@ -385,7 +396,12 @@ __device__ __attribute__((noinline)) bool stage_copy(const uint8_t* src, uint8_t
                 limit = wave_load(sw.verdict) == ~0u ? 0u : wave_load(sw.bytes);
                 break;
             }
-            if (stage_late(t0)) return false;
+            if (av > seen) {
+                seen = av;
+                t0 = __builtin_amdgcn_s_memrealtime();
+            } else if (stage_late(t0)) {
+                return false;
+            }
             __builtin_amdgcn_s_sleep(8);
         }
 #if AC_COPY_AHEAD
@@ -395,8 +411,15 @@ __device__ __attribute__((noinline)) bool stage_copy(const uint8_t* src, uint8_t
         // first codes chunk landed anywhere in the next 5-18 us: profiles/r03_m9/stamps.log).
         if (x >= AC_COPY_AHEAD) {
             uint32_t* my_done = sw.done + (x % AC_STAGE_REPL) * AC_QUEUE_LINE;
-            while (wave_load(my_done) < x - AC_COPY_AHEAD) {
-                if (stage_late(t0)) return false;
+            uint32_t dn = 0, dseen = 0;
+            t0 = __builtin_amdgcn_s_memrealtime();
+            while ((dn = wave_load(my_done)) < x - AC_COPY_AHEAD) {
+                if (dn > dseen) {  // (the copies ahead of it are moving)
+                    dseen = dn;
+                    t0 = __builtin_amdgcn_s_memrealtime();
+                } else if (stage_late(t0)) {
+                    return false;
+                }
                 __builtin_amdgcn_s_sleep(2);
             }
         }
@@ -430,9 +453,13 @@ __device__ __attribute__((noinline)) bool stage_copy(const uint8_t* src, uint8_t
 __device__ __attribute__((noinline)) uint32_t stage_wait_all(uint32_t* words, uint32_t chunks, uint32_t replica,
                                                              uint32_t* err) {
     const StageWords sw = stage_words(words);
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (wave_load(sw.done + replica * AC_QUEUE_LINE) < chunks) {
-        if (stage_late(t0)) {
+    uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t dn = 0, seen = 0;
+    while ((dn = wave_load(sw.done + replica * AC_QUEUE_LINE)) < chunks) {
+        if (dn > seen) {  // copies are landing: the wait's clock restarts
+            seen = dn;
+            t0 = __builtin_amdgcn_s_memrealtime();
+        } else if (stage_late(t0)) {
             if ((threadIdx.x & 63u) == 0) atomicOr(err, AC_DEVERR_STAGE);
             return ~0u;
         }
@@ -462,11 +489,12 @@ __device__ __forceinline__ uint64_t stage_gate(uint32_t* words, const uint32_t* 
                                                          uint32_t* err, uint32_t pre = 0u) {
     const uint32_t lane = threadIdx.x & 63u;
     const StageWords sw = stage_words(words);
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     const uint32_t x0 = r0 / AC_STAGE_CHUNK, x1 = (r1 - 1u) / AC_STAGE_CHUNK;
     // (more chunks than lanes, or past the launch's chunks: wait for the whole segment)
     const uint32_t nx = (x1 < chunks && x1 - x0 < 62u) ? x1 - x0 + 1u : 0u;
     bool in_prefix = nx && r1 <= pre;  // the N-free prefix covers [r0, r1) (it only grows; `pre`: at launch)
+    uint32_t seen = 0;  // done + N-free bytes last seen (the wait's clock restarts when they move)
     for (;;) {
         // one wave instruction: lane 0 the done count, lane 1 the N-free bytes (this workgroup's
         // replicas), lanes 2.. the chunks' flags once the prefix covers them
@@ -475,11 +503,15 @@ __device__ __forceinline__ uint64_t stage_gate(uint32_t* words, const uint32_t* 
                                        : (in_prefix && lane - 2u < nx ? chunk_flag(chunk_gen, x0 + (lane - 2u)) : nullptr);
         uint32_t v = 0;
         if (p) v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (__builtin_amdgcn_readlane(v, 0) >= chunks) return wave_load(sw.verdict);
+        const uint32_t dn = __builtin_amdgcn_readlane(v, 0), av = __builtin_amdgcn_readlane(v, 1);
+        if (dn >= chunks) return wave_load(sw.verdict);
         const uint64_t miss = __ballot(lane >= 2u && lane - 2u < nx && v != gen);
         if (in_prefix && miss == 0) return ((uint64_t)(x1 + 1u) << 32) | 2u;
-        in_prefix = nx && (r1 <= pre || __builtin_amdgcn_readlane(v, 1) >= r1);
-        if (stage_late(t0)) {
+        in_prefix = nx && (r1 <= pre || av >= r1);
+        if (dn + av != seen) {
+            seen = dn + av;
+            t0 = __builtin_amdgcn_s_memrealtime();
+        } else if (stage_late(t0)) {
             if (lane == 0) atomicOr(err, AC_DEVERR_STAGE);
             return ~0u;
         }
@@ -594,13 +626,27 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
         st_words = a.stage + AC_STAGE_L_SEG(si) * AC_QUEUE_LINE;
         // the k-mer section fills whole chunks and is in the pinned block before the launch
         const uint32_t pre_chunks = sg.stage_codes_off / AC_STAGE_CHUNK;
+        if (a.copier_wgs && blockIdx.x < a.copier_wgs) {
+            // Copier workgroup of a large call: every wave serves every segment's tickets, segments
+            // in the order the host packs them, before the workgroup counts like the others.
+            for (uint32_t s2 = 0; s2 < a.n_segs; ++s2) {
+                const SegDev& c2 = a.seg[s2];
+                if (!c2.stage_chunks) continue;
+                if (!__builtin_amdgcn_readfirstlane((uint32_t)stage_copy(
+                        c2.stage_src, c2.stage_dst, c2.stage_chunks, c2.stage_codes_off / AC_STAGE_CHUNK,
+                        a.host_hdr + s2 * AC_QUEUE_LINE, a.stage + AC_STAGE_L_SEG(s2) * AC_QUEUE_LINE, c2.stage_gen,
+                        a.gen, s2)))
+                    if (lane == 0) atomicOr(a.err, AC_DEVERR_STAGE);
+            }
+        }
         if (wib == 0) {
             uint32_t r = ~0u;
             const bool equal = sg.ulen != AC_NO_ULEN && sg.n_kmers;
             // (serving a chunk that has to wait for the host after the table barrier instead, so the
             // workgroup's other waves start counting, measured slower: its copy starts later,
             // profiles/r03_stage2/defer_ab.log)
-            if (!__builtin_amdgcn_readfirstlane(
+            if (!a.copier_wgs &&
+                !__builtin_amdgcn_readfirstlane(
                     (uint32_t)stage_copy(sg.stage_src, sg.stage_dst, sg.stage_chunks, pre_chunks,
                                          a.host_hdr + (uint32_t)si * AC_QUEUE_LINE, st_words, sg.stage_gen, a.gen,
                                          (uint32_t)si))) {

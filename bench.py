@@ -89,6 +89,9 @@ def parse():
                     help="skip the device-resident kernel timing (and with it the roofline)")
     ap.add_argument("--no-pipelined", action="store_true", help="skip the informational pipelined leg")
     ap.add_argument("--verify", action="store_true", help="check the stage's counts against the oracle (slow)")
+    ap.add_argument("--shard", metavar="R/N",
+                    help="rehearsal on one GPU: time rank R's shard of an N-rank strong-scaling run alone "
+                         "(the projection basis for N GPUs; never the default line)")
     ap.add_argument("--kernel-launches", type=int, default=100,
                     help="launches of the kernel-only leg (at least --steps); it runs before the stage, so the "
                          "device is at its sustained clock when the stage's warmup starts (DESIGN.md 4c)")
@@ -261,7 +264,13 @@ def main():
 
     import approx_counter_amd as ac
 
-    wl, units_job = build_workload(args, rank, world)
+    if args.shard:  # one rank's shard of an N-rank strong run, timed alone (a projection, not a scaling run)
+        r_s, n_s = (int(x) for x in args.shard.split("/"))
+        args.scaling = "strong"
+        wl, _ = build_workload(args, r_s, n_s)
+        units_job = sum(wl[e]["kmers"].size * sum(int(w.size) for w in wl[e]["windows"]) for e in ("start", "end"))
+    else:
+        wl, units_job = build_workload(args, rank, world)
     from approx_counter_amd.counter import host_pool_cpus
     ends = ("start", "end")
     n_c = [int(wl[e]["kmers"].size) for e in ends]
@@ -421,7 +430,8 @@ def main():
     if rank == 0:
         P = min(32 // args.k, 4)
         reads_note = (f"{args.sn} reads sharded over {world} ranks" if world > 1 and args.scaling == "strong"
-                      else f"{args.sn} reads/rank")
+                      else f"shard {args.shard} of {args.sn} reads (rehearsal: one rank's share, timed alone)"
+                      if args.shard else f"{args.sn} reads/rank")
         workload_name = (f"{args.config}: k={args.k} sn={args.sn} sl={args.sl} lim={args.lim}, "
                          f"start+end ends fused, {reads_note}")
         out = {

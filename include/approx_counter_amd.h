@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define AC_ABI_VERSION 3
+#define AC_ABI_VERSION 4
 
 typedef int32_t ac_status;
 #define AC_OK 0
@@ -280,9 +280,11 @@ typedef struct ac_job {
  * windows are packed to 2-bit codes + N bitmap by the host worker pool
  * straight into a pinned staging block, moved into device memory job by job
  * (ac_stage_mode: by the count kernel itself -- launched first -- or by a copy
- * ahead of it), counted by ONE fused kernel launch over all jobs (calls of >=
- * 2^17 windows: 2-4 parts, each launched once it is sent), and the kernel writes
- * the counts into the pinned block.  On an
+ * ahead of it), counted by ONE fused kernel launch over all jobs (every size
+ * since ABI 4; with AC_STAGE_EARLY=0, calls of >= 2^17 windows are cut into 2-4
+ * parts, each launched once it is sent), and the kernel writes the counts into
+ * the pinned block.  An early launch that times out waiting for the host (0.5 s
+ * without progress) is run again through the DMA path.  On an
  * ac_create_multi context every job's windows are split into contiguous shards
  * balanced by bases, one per device, and the shard counts are summed.
  * Replaces the index build (537-541), the OpenMP search loop (547-599) and
@@ -362,21 +364,27 @@ int ac_plan_host_cpus(const char* const* rank_cpulists, int n_ranks, int rank, c
                       const int* core_of, int n_core_of, int* out, int cap);
 
 /*
- * How the last ac_error_count_jobs call on ctx moved its packed inputs (no
- * reference counterpart): 2 = the early launch, for calls counted in one part
- * on one device (default; AC_STAGE_EARLY=0 turns it off): the count kernel is
+ * How the last ac_error_count_jobs / _submit call on ctx moved its packed
+ * inputs (no reference counterpart).  ABI note: the values changed in ABI 3 --
+ * 1 (zero-copy, round 2) is no longer returned -- and in ABI 4 large calls moved
+ * from 0 to 2; callers should compare against 2 / 0 only.
+ * 2 = the early launch, for every single-device call
+ * (default; AC_STAGE_EARLY=0 turns it off): the count kernel is
  * launched before the host packs, the host flags each job in a pinned header as
  * soon as it is packed, the kernel copies the flagged job into device memory
  * itself and counts it while later jobs are still being packed, and each
  * candidate group's last workgroup stores its counts and error bits, tagged with
- * the call's generation, into pinned memory, which the host polls.  0 = the DMA
- * path (calls of >= 2^17 windows, cut into 2-4 parts, each packed and copied by
- * the copy engine while the previous part counts; or AC_STAGE_EARLY=0).  Either
+ * the call's generation, into pinned memory, which the host polls.  Large calls
+ * (more staging chunks than half the workgroups) are staged by a few copier
+ * workgroups while the others count.  0 = the DMA path (AC_STAGE_EARLY=0: calls
+ * of >= 2^17 windows cut into 2-4 parts, each packed and copied by the copy
+ * engine while the previous part counts; a multi-device context; a staging
+ * region of 2^31 bytes or more; the retry of a timed-out early launch).  Either
  * way a job is sent without its N bitmap when no window needs it (no N, or, for
  * equal windows, every N inside the window's inline record) and without window
  * descriptors when its windows have one length.  -1 = no
- * call yet.  ac_error_count_jobs_submit takes the early launch for one-part calls
- * too (its counts and errors go to device memory; ac_check reports the errors).
+ * call yet.  ac_error_count_jobs_submit takes the early launch too (its counts
+ * and errors go to device memory; ac_check reports the errors).
  */
 int ac_stage_mode(const ac_ctx* ctx);
 

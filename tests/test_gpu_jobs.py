@@ -345,26 +345,61 @@ def test_early_launch_rotating_inputs_bit_exact(mode):
     assert r.returncode == 0 and "OK" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])
 
 
-def test_early_launch_unflagged_job_fails_cleanly():
-    """The early-launch kernel's waits are bounded: a job the host never flags (test hook)
-    makes its waves give up after 0.5 s, report it, and the launch still completes -- the
-    call fails with AC_ERR_INTERNAL instead of hanging, in a child process (the hook is read
-    once per process)."""
-    code = (
-        "import numpy as np, approx_counter_amd as ac\n"
-        "from tests import cases\n"
-        "a = cases.planted_case(41, 16, 100, 200, win_len=(100, 101))\n"
-        "b = cases.planted_case(42, 16, 100, 200, win_len=(100, 101))\n"
-        "c = ac.ApproxCounter(0)\n"
-        "try:\n"
-        "    c.count_jobs(16, [(a[0], ac.Dna5Sample.from_windows(a[1])), (b[0], ac.Dna5Sample.from_windows(b[1]))])\n"
-        "    print('NO ERROR')\n"
-        "except ac.ApproxCounterError as e:\n"
-        "    print('STATUS', e.status, e)\n"
-    )
-    env = dict(os.environ, AC_STAGE_TEST_UNFLAGGED="1", AC_STAGE_EARLY="1", PYTHONPATH=ROOT)
-    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=100, cwd=ROOT)
-    assert "STATUS 4" in r.stdout and "timed out" in r.stdout, (r.stdout, r.stderr[-2000:])
+def test_early_launch_unflagged_job_recovers():
+    """The early-launch kernel's waits are bounded: a job the host never flags (test-only
+    hook, include/approx_counter_amd_testing.h) makes its waves give up after 0.5 s without
+    progress and report it; the launch still completes, and the synchronous call runs again
+    through the DMA path instead of failing or hanging -- exact counts, ac_stage_mode() 0."""
+    from approx_counter_amd import _lib
+
+    a = cases.planted_case(41, 16, 100, 200, win_len=(100, 101))
+    b = cases.planted_case(42, 16, 100, 200, win_len=(100, 101))
+    jobs = [(a[0], ac.Dna5Sample.from_windows(a[1])), (b[0], ac.Dna5Sample.from_windows(b[1]))]
+    L = _lib.load()
+    with ac.ApproxCounter(0) as c:
+        prev = L.ac_testing_stage_hooks(1)  # AC_TESTING_UNFLAG_LAST
+        try:
+            got = c.count_jobs(16, jobs)
+            assert c.stage_mode() == 0  # the retry's path
+        finally:
+            L.ac_testing_stage_hooks(prev)
+        assert np.array_equal(got[0], oracle.count_myers(16, *a))
+        assert np.array_equal(got[1], oracle.count_myers(16, *b))
+        got = c.count_jobs(16, jobs)  # hooks off: the early launch again, same context
+        assert c.stage_mode() == 2
+        assert np.array_equal(got[1], oracle.count_myers(16, *b))
+
+
+def test_early_launch_slow_host_is_not_a_timeout():
+    """a staged launch's waits restart their clock whenever the host makes
+    progress, so a call whose packing takes longer than the 0.5 s timeout in total -- a
+    large call on one or two CPUs -- is counted, not failed.  The test-only hook
+    AC_TESTING_SLOW_HOST makes the publishing thread sleep 60 ms after each of the call's
+    first 12 progress records (> 0.7 s in all, every gap far below 0.5 s): the early
+    launch must complete by itself (ac_stage_mode 2, no retry), bit-exact."""
+    import time
+
+    from approx_counter_amd import _lib
+
+    a = cases.planted_case(51, 16, 300, 6000, win_len=(100, 100), p_n=0.0)
+    b = cases.planted_case(52, 16, 200, 6000, win_len=(101, 101), p_n=0.002)
+    wa = [(w + "A" * 100)[:100] for w in a[1]]
+    wb = [(w + "A" * 101)[:101] for w in b[1]]
+    jobs = [(a[0], ac.Dna5Sample.from_windows(wa)), (b[0], ac.Dna5Sample.from_windows(wb))]
+    L = _lib.load()
+    with ac.ApproxCounter(0) as c:
+        c.count_jobs(16, jobs)  # (allocations out of the timed call)
+        prev = L.ac_testing_stage_hooks(4)  # AC_TESTING_SLOW_HOST
+        try:
+            t = time.perf_counter()
+            got = c.count_jobs(16, jobs)
+            dt = time.perf_counter() - t
+            assert c.stage_mode() == 2, "the early launch timed out and was retried"
+        finally:
+            L.ac_testing_stage_hooks(prev)
+    assert dt > 0.6, dt
+    assert np.array_equal(got[0], oracle.count_myers(16, a[0], wa))
+    assert np.array_equal(got[1], oracle.count_myers(16, b[0], wb))
 
 
 def test_image_size_limit_rejected(counter):
@@ -383,13 +418,14 @@ def test_image_size_limit_rejected(counter):
     assert np.array_equal(seg.counts_numpy(), oracle.count_myers(16, kmers, wins, 16))
 
 
-def test_large_image_takes_dma_path():
-    """A call whose zero-copy would move more than 256 MB over PCIe (image x candidate
-    groups; zero-copy may read the image once per group) is staged by DMA: a fresh
-    context reports DMA at once (ac_stage_mode 0), and the kernel writes the counts into
-    the pinned block, bit-exact (checked on a prefix of the candidates)."""
+def test_large_call_early_launch_copier_workgroups():
+    """A large call (700k windows: 22 MB of staging region, ~5,500 chunks, far more than
+    half the workgroups) takes the early launch in one part since round 4: a few copier
+    workgroups stage every chunk while the others count windows as their chunks land
+    (wm_count.h LaunchArgs::copier_wgs).  Tasks of <= 2,048 windows, progress published
+    as they finish; bit-exact on every candidate group's first and last lanes."""
     rng = np.random.default_rng(7)
-    n, L = 700_000, 100  # 700k x 128 bases x 3/8 B x 8 groups = 269 MB
+    n, L = 700_000, 100
     win = rng.integers(0, 4, size=(n, L), dtype=np.uint8)
     win[rng.integers(0, n, size=2000), rng.integers(0, L, size=2000)] = 4  # a few N
     picks = rng.integers(0, n, size=1000)
@@ -401,11 +437,42 @@ def test_large_image_takes_dma_path():
     try:
         assert c.stage_mode() == -1
         got = c.count_jobs(16, [(kmers, sample)])[0]
-        assert c.stage_mode() == 0
+        assert c.stage_mode() == 2
+        again = c.count_jobs(16, [(kmers, sample)])[0]  # the other staging slot
+        assert np.array_equal(got, again)
     finally:
         c.close()
     sub = np.r_[0:16, 500:508, 992:1000]  # every candidate group's first and last lanes, and more
     assert np.array_equal(got[sub], oracle.count_myers(16, kmers[sub], win, 16))
+
+
+def test_dma_parts_path_without_early_launch():
+    """AC_STAGE_EARLY=0 keeps round 2's copy-engine path: a call of >= 2^17 windows cut
+    into parts, each packed and sent while the previous part counts (ac_stage_mode 0), for
+    the synchronous call and a submit; ragged windows with N.  In a child process
+    (AC_STAGE_EARLY is read once per process)."""
+    code = (
+        "import numpy as np, torch, approx_counter_amd as ac, oracle\n"
+        "from tests import cases\n"
+        "km, wins = cases.planted_case(61, 16, 300, 140_000, win_len=(90, 110), p_n=0.002)\n"
+        "km2, wins2 = cases.planted_case(62, 16, 200, 10_000, win_len=(101, 101), p_n=0.002)\n"
+        "jobs = ac.Jobs([(km, ac.Dna5Sample.from_windows(wins)), (km2, ac.Dna5Sample.from_windows(wins2))])\n"
+        "exp = [oracle.count_myers(16, km, wins, 16), oracle.count_myers(16, km2, wins2, 16)]\n"
+        "with ac.ApproxCounter(0) as c:\n"
+        "    got = c.count_jobs(16, jobs)\n"
+        "    assert c.stage_mode() == 0, c.stage_mode()\n"
+        "    assert all(np.array_equal(g, e) for g, e in zip(got, exp))\n"
+        "    d = torch.full((jobs.n_counts,), -1, dtype=torch.int32, device='cuda')\n"
+        "    st = torch.cuda.current_stream()\n"
+        "    c.submit_jobs(16, jobs, d, stream=st.cuda_stream)\n"
+        "    c.check(stream=st.cuda_stream)\n"
+        "    assert c.stage_mode() == 0\n"
+        "    assert np.array_equal(d.cpu().numpy().view(np.uint32).astype(np.uint64), np.concatenate(exp))\n"
+        "print('OK')\n"
+    )
+    env = dict(os.environ, AC_STAGE_EARLY="0", PYTHONPATH=ROOT)
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=250, cwd=ROOT)
+    assert r.returncode == 0 and "OK" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])
 
 
 def test_rccl_allreduce_single_rank(counter):

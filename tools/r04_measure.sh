@@ -1,0 +1,58 @@
+#!/bin/bash
+# Round-4 measurement batch on the GPU box (one box acquisition per call).  Every step has its
+# own time limit; a test failure (rc 1) lets the next step run, anything else stops the batch.
+# usage: tools/r04_measure.sh OUTDIR part...
+#   tests     the GPU test files touched this round (early launch, bench path, scale)
+#   suite     the whole -m gpu suite
+#   configs   bench lines at cfg2-cfg5 (stage traces on)
+#   shard     one rank's 1/8 cfg4 shard alone, pool capped at 2 and at 16 participants
+#   copiers   copier-workgroup count A/B at cfg4 and on the shard
+#   cfg2      cfg2 bench x3 (400 steps) with stage trace
+#   stamps    per-wave timelines (resident cfg2 launch, staged calls)
+set -u
+OUT=$1; shift
+case $OUT in /*) ;; *) OUT=${GRAFT_REPO_ROOT:-$(pwd)}/$OUT ;; esac
+mkdir -p "$OUT"
+run() {  # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  echo "== $name" | tee -a "$OUT/summary.log"
+  timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "   rc=$rc" | tee -a "$OUT/summary.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after rc=$rc"; tail -20 "$OUT/$name.log"; exit $rc; fi
+  grep -h 'passed\|failed\|stage trace\|"ms_per_step"' "$OUT/$name.log" \
+    | sed -e 's/.*"value": \([0-9.e+]*\).*"ms_per_step": \([0-9.]*\).*"step_ms": \({[^}]*}\).*"kernel_ms": \([0-9.]*\).*/value \1 ms_per_step \2 \3 kernel_ms \4/' \
+    | cut -c1-400 | tee -a "$OUT/summary.log"
+}
+PYT="python3 -u -m pytest -x -v --timeout 300 --timeout-method thread -p no:cacheprovider"
+BQ="--no-cpu-baseline --no-pipelined"
+for part in "$@"; do
+case $part in
+tests)
+  run tests_bench_path 400 $PYT -m gpu tests/test_gpu_bench_path.py
+  run tests_jobs 400 $PYT -m gpu tests/test_gpu_jobs.py
+  run tests_scale 600 $PYT -m gpu tests/test_gpu_scale.py ;;
+suite)
+  run suite 1100 $PYT -m gpu tests ;;
+configs)
+  for c in cfg2 cfg3 cfg5 cfg4; do
+    run bench_$c 300 env AC_STAGE_TRACE=1 python3 bench.py --config $c --steps 20 --warmup 5 $BQ
+  done ;;
+shard)
+  for t in 2 16 2; do
+    run shard_t$t 300 env AC_HOST_THREADS=$t AC_STAGE_TRACE=1 python3 bench.py --config cfg4 --shard 0/8 --steps 30 --warmup 5 $BQ
+  done ;;
+copiers)
+  for w in 8 16 32 64; do
+    run shard_t2_cw$w 300 env AC_COPIER_WGS=$w AC_HOST_THREADS=2 python3 bench.py --config cfg4 --shard 0/8 --steps 30 --warmup 5 $BQ --no-kernel-leg
+    run cfg4_cw$w 300 env AC_COPIER_WGS=$w python3 bench.py --config cfg4 --steps 10 --warmup 3 $BQ --no-kernel-leg
+  done ;;
+stamps)  # per-wave timelines of a -DAC_STAMPS build (tools/variants.sh stamps "-DAC_STAMPS")
+  run stamps_resident 120 env APPROX_COUNTER_AMD_LIB=build/var/stamps/libapprox_counter_amd.so python3 tools/stamps.py
+  run stamps_staged 120 env APPROX_COUNTER_AMD_LIB=build/var/stamps/libapprox_counter_amd.so python3 tools/stage_stamps.py --calls 40 ;;
+cfg2)
+  for i in 1 2 3; do
+    run cfg2_$i 200 env AC_STAGE_TRACE=1 python3 bench.py --steps 400 --warmup 10 $BQ
+  done ;;
+esac
+done
