@@ -401,6 +401,87 @@ __attribute__((target("avx512f,avx512bw,avx512vl"))) uint32_t pack_range_avx512(
     return flags;
 }
 
+// The stage's common case on AVX-512: equal windows of L bases (a read end: every start window sl
+// bases, every end window sl + 1) with inline N records, L <= 256.  One window per iteration with
+// every step's masks, shifts and the record's place hoisted out of the loop (they depend on L only),
+// the slot's codes kept in registers until the record is in, then stored whole -- with streaming
+// stores when the slot is 32-byte aligned (a read end's slots are: the image starts 256-B aligned and
+// S = 128 / 256), so the pinned block's lines are not read for ownership first.  NS = 64-base steps
+// per slot (S = 32 NS2 bases: NS = ceil(NS2 / 2)).
+// (A window of another length -- the caller broke its promise -- goes through the general packer.)
+template <int NS>
+__attribute__((target("avx512f,avx512bw,avx512vl"))) uint32_t pack_equal_records_avx512(
+    const uint8_t* bases, const uint64_t* offset, const uint32_t* length, uint32_t L, uint32_t w0, uint32_t w1,
+    uint64_t first, uint32_t* codes, uint32_t* nmask, uint64_t* start_out, uint32_t* len_out) {
+    const uint32_t S = (L + 31u) & ~31u;
+    const bool half = (S % 64u) != 0u;  // the last step covers 32 bases of the slot
+    const __m512i three = _mm512_set1_epi8(3);
+    const __m512i pair = _mm512_set1_epi16(0x0401);
+    const __m512i quad = _mm512_set1_epi32(0x00100001);
+    __mmask64 m[NS];
+    for (int b = 0; b < NS; ++b) {
+        const uint32_t left = L > 64u * b ? L - 64u * b : 0u;
+        m[b] = left >= 64u ? ~0ull : ((1ull << left) - 1ull);
+    }
+    uint32_t flags = 0;
+    uint64_t pos = first;
+    bool stream = ((uintptr_t)(codes + pos / 16) % 32u) == 0u && (S % 128u) == 0u;
+    const bool streamed = stream;
+    for (uint32_t w = w0; w < w1; ++w, pos += S) {
+        if (__builtin_expect(length[w] != L, 0)) {
+            flags |= pack_range_avx512(bases, offset, length, w, w + 1, pos, codes, nmask, start_out + (w - w0),
+                                       len_out + (w - w0), true);
+            pos += image_span(length[w]) - S;
+            stream = false;  // (the next slots may not be 32-byte aligned any more)
+            continue;
+        }
+        const uint8_t* src = bases + offset[w];
+        __m128i c[NS];
+        uint64_t isn[NS];
+        uint64_t any = 0;
+#pragma GCC unroll 4
+        for (int b = 0; b < NS; ++b) {
+            const __m512i v = _mm512_maskz_loadu_epi8(m[b], src + 64 * b);
+            isn[b] = _mm512_mask_cmpgt_epu8_mask(m[b], v, three);
+            any |= isn[b];
+            __m512i t = _mm512_maddubs_epi16(_mm512_and_si512(v, three), pair);
+            t = _mm512_madd_epi16(t, quad);
+            c[b] = _mm512_cvtepi32_epi8(t);
+        }
+        uint32_t* slot = codes + pos / 16;
+        if (__builtin_expect(any != 0, 0)) {  // the record (rare: 0.1 % N per base is ~10 % of windows)
+            NRecord nr(L);
+            for (int b = 0; b < NS; ++b)
+                if (isn[b]) nr.add(isn[b], 64u * b);
+            alignas(16) uint32_t words[4 * NS];
+            for (int b = 0; b < NS; ++b) _mm_store_si128((__m128i*)(words + 4 * b), c[b]);
+            const uint32_t f = nr.finish(words);  // ORs the record into words[rw]
+            for (int b = 0; b < NS; ++b) c[b] = _mm_load_si128((const __m128i*)(words + 4 * b));
+            if (f & PACK_OVERFLOW) {
+                uint8_t* nw = (uint8_t*)(nmask + pos / 32);
+                for (uint32_t b = 0; b < S; b += 32) {
+                    const uint32_t word = (uint32_t)(isn[b / 64] >> (b % 64));
+                    std::memcpy(nw + b / 8, &word, 4);
+                }
+            }
+            flags |= f;
+        }
+        if (stream) {
+#pragma GCC unroll 4
+            for (int b = 0; b + 1 < NS; b += 2)
+                _mm256_stream_si256((__m256i*)(slot + 4 * b), _mm256_inserti128_si256(_mm256_castsi128_si256(c[b]), c[b + 1], 1));
+            if (NS % 2) _mm_stream_si128((__m128i*)(slot + 4 * (NS - 1)), c[NS - 1]);
+        } else {
+#pragma GCC unroll 4
+            for (int b = 0; b + 1 < NS; ++b) _mm_storeu_si128((__m128i*)(slot + 4 * b), c[b]);
+            if (half) _mm_storel_epi64((__m128i*)(slot + 4 * (NS - 1)), c[NS - 1]);
+            else _mm_storeu_si128((__m128i*)(slot + 4 * (NS - 1)), c[NS - 1]);
+        }
+    }
+    if (streamed) _mm_sfence();  // streamed slots are in memory before the caller publishes them
+    return flags;
+}
+
 template <bool AVX2>
 uint32_t pack_range_impl(const uint8_t* bases, const uint64_t* offset, const uint32_t* length, uint32_t w0,
                          uint32_t w1, uint64_t first, uint32_t* codes, uint32_t* nmask, uint64_t* start_out,
@@ -506,8 +587,20 @@ uint64_t span_scan(const uint32_t* len, uint32_t n, uint32_t* first, uint32_t* d
 uint32_t pack_dna5_range(const uint8_t* bases, const uint64_t* offset, const uint32_t* length, uint32_t w0,
                          uint32_t w1, uint64_t first, uint32_t* codes, uint32_t* nmask, uint64_t* start_out,
                          uint32_t* len_out, bool records) {
-    if (have_avx512())
+    if (have_avx512()) {
+        // equal windows with records (the caller's promise: every window of the job has one length)
+        const uint32_t L = w1 > w0 ? length[w0] : 0u;
+        if (records && nrec_bits(L) != 0u) {
+            switch ((((L + 31u) & ~31u) + 63u) / 64u) {
+                case 1: return pack_equal_records_avx512<1>(bases, offset, length, L, w0, w1, first, codes, nmask, start_out, len_out);
+                case 2: return pack_equal_records_avx512<2>(bases, offset, length, L, w0, w1, first, codes, nmask, start_out, len_out);
+                case 3: return pack_equal_records_avx512<3>(bases, offset, length, L, w0, w1, first, codes, nmask, start_out, len_out);
+                case 4: return pack_equal_records_avx512<4>(bases, offset, length, L, w0, w1, first, codes, nmask, start_out, len_out);
+                default: break;
+            }
+        }
         return pack_range_avx512(bases, offset, length, w0, w1, first, codes, nmask, start_out, len_out, records);
+    }
     if (have_avx2())
         return pack_range_impl<true>(bases, offset, length, w0, w1, first, codes, nmask, start_out, len_out, records);
     return pack_range_impl<false>(bases, offset, length, w0, w1, first, codes, nmask, start_out, len_out, records);

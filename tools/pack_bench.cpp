@@ -2,7 +2,7 @@
 // of n Dna5 windows (100 / 101 bases) packed by the pool the way ac_error_count_jobs does
 // (tasks in job order, the caller helping), timing when job 0 and job 1 are complete.
 //   g++ -O3 -std=c++17 -pthread -Iapprox_counter_amd/csrc tools/pack_bench.cpp \
-//       approx_counter_amd/csrc/host_pack.cpp -o /tmp/pack_bench && /tmp/pack_bench [n] [iters] [per]
+//       approx_counter_amd/csrc/host_pack.cpp -o /tmp/pack_bench && /tmp/pack_bench [n] [iters] [per] [records]
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -21,6 +21,8 @@ int main(int argc, char** argv) {
     const uint32_t n = argc > 1 ? (uint32_t)std::atoi(argv[1]) : 10000;
     const int iters = argc > 2 ? std::atoi(argv[2]) : 2000;
     const uint32_t per_arg = argc > 3 ? (uint32_t)std::atoi(argv[3]) : 0;
+    // records = 1: the stage's equal-window form (inline N records, no descriptors), 0.1 % N bases
+    const bool records = argc > 4 ? std::atoi(argv[4]) != 0 : true;
     acamd::WorkPool& pool = acamd::host_pool();
     std::mt19937 rng(1);
     struct Job {
@@ -34,7 +36,7 @@ int main(int argc, char** argv) {
     for (int j = 0; j < 2; ++j) {
         const uint32_t L = 100 + j;
         job[j].bases.resize((size_t)n * L);
-        for (auto& b : job[j].bases) b = (uint8_t)(rng() & 3u);
+        for (auto& b : job[j].bases) b = (rng() % 1000u == 0u) ? 4u : (uint8_t)(rng() & 3u);
         for (uint32_t i = 0; i < n; ++i) {
             job[j].off.push_back((uint64_t)i * L);
             job[j].len.push_back(L);
@@ -61,7 +63,7 @@ int main(int argc, char** argv) {
             const Task& x = tasks[t];
             Job& b = job[x.j];
             acamd::pack_dna5_range(b.bases.data(), b.off.data(), b.len.data(), x.w0, x.w1, (uint64_t)x.w0 * 128,
-                                   b.codes.data(), b.nmask.data(), b.st.data() + x.w0, b.ln.data() + x.w0);
+                                   b.codes.data(), b.nmask.data(), b.st.data() + x.w0, b.ln.data() + x.w0, records);
             left[x.j].fetch_sub(1, std::memory_order_release);
         };
         const double t0 = now_us();
@@ -84,7 +86,8 @@ int main(int argc, char** argv) {
     std::sort(d0.begin(), d0.end());
     std::sort(d1.begin(), d1.end());
     auto q = [](const std::vector<double>& v, double f) { return v[(size_t)(f * (v.size() - 1))]; };
-    std::printf("participants %u, %zu tasks of %u windows, n=%u per job\n", pool.size(), tasks.size(), per, n);
+    std::printf("participants %u, %zu tasks of %u windows, n=%u per job, records %d\n", pool.size(), tasks.size(), per, n,
+                (int)records);
     std::printf("job 0 packed: p10 %.1f p50 %.1f p90 %.1f max %.1f us\n", q(d0, .1), q(d0, .5), q(d0, .9), d0.back());
     std::printf("both packed:  p10 %.1f p50 %.1f p90 %.1f max %.1f us\n", q(d1, .1), q(d1, .5), q(d1, .9), d1.back());
     return 0;
