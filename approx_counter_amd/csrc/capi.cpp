@@ -122,6 +122,12 @@ struct ac_ctx {
     uint32_t early_flip = 0;         // early-launch calls alternate between staging slots 0 and 1
     int exact_path = -1;             // the last exact count's path: 1 partitioned, 0 hash table
     int last_mode = -1;  // ac_stage_mode: 2 the last jobs call was an early launch, 0 the DMA path
+    // Warm-up started by ac_create on a thread of its own (ensure_warm joins it before the first count
+    // launch): the count kernels' code object is loaded by the occupancy queries, so the first launch
+    // -- the CLI's one approximate count per run -- does not pay for it; it overlaps the caller's FASTA
+    // parsing and exact count instead.
+    std::thread warm;
+    uint32_t warm_resident[AC_MAX_PACK + 1] = {0, 0, 0, 0, 0};
 };
 
 namespace {
@@ -288,10 +294,19 @@ struct StageLaunch {
     uint64_t* grp_err = nullptr;   // its per-group error words (device-visible pinned address)
 };
 
+// Joins ac_create's warm-up thread (once) and takes the resident-wave counts it queried.
+void ensure_warm(ac_ctx* ctx) {
+    if (!ctx->warm.joinable()) return;
+    ctx->warm.join();
+    for (uint32_t P = 1; P <= AC_MAX_PACK; ++P)
+        if (!ctx->resident[P]) ctx->resident[P] = ctx->warm_resident[P];
+}
+
 ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hipStream_t stream,
                  bool zero, uint32_t* err = nullptr, int scratch = 0, uint64_t wave_cap = 0,
                  const bool* no_n = nullptr, const uint32_t* ulen = nullptr, const StageLaunch* stage = nullptr,
                  const bool* nrec = nullptr) {
+    ensure_warm(ctx);
     ac_ctx::Scratch& sc = ctx->sc[scratch];
     if (ac_status st = check_k(ctx, k)) return st;
     if (n > AC_MAX_SEGS) return fail(ctx, AC_ERR_INVALID, "too many segments in one launch (max 4)");
@@ -631,12 +646,34 @@ ac_status ac_create(ac_ctx** out, int device) {
         ac_destroy(ctx);
         return st;
     }
+    // (a query that fails leaves its count 0: launch() queries again and reports the error there)
+    // The warm-up also allocates the first scratch set at the sizes a few-candidate-group launch needs
+    // (it grows on demand later), so that launch does not wait for allocations either.
+    ctx->warm = std::thread([ctx] {
+        if (hipSetDevice(ctx->device) != hipSuccess) return;
+        for (uint32_t P = 1; P <= AC_MAX_PACK; ++P)
+            (void)acamd::resident_waves(P, ctx->cu_count, &ctx->warm_resident[P]);
+        ac_ctx::Scratch& sc = ctx->sc[0];
+        auto zeroed = [](void** p, size_t bytes) {
+            if (hipMalloc(p, bytes) != hipSuccess) return false;
+            if (hipMemset(*p, 0, bytes) == hipSuccess) return true;
+            (void)hipFree(*p);
+            *p = nullptr;
+            return false;
+        };
+        constexpr uint32_t QCAP = 2048, ACC = 64 * 256, TICKETS = 64, CHUNKS = 1024;
+        if (zeroed((void**)&sc.queue, sizeof(uint32_t) * AC_QUEUE_LINE * 2 * QCAP)) sc.qcap = QCAP;
+        if (zeroed((void**)&sc.acc, sizeof(uint32_t) * ACC)) sc.acc_cap = ACC;
+        if (zeroed((void**)&sc.tickets, sizeof(uint32_t) * AC_QUEUE_LINE * TICKETS)) sc.ticket_cap = TICKETS;
+        if (zeroed((void**)&sc.stage_gen, sizeof(uint32_t) * AC_QUEUE_LINE * CHUNKS)) sc.stage_gen_cap = CHUNKS;
+    });
     *out = ctx;
     return AC_OK;
 }
 
 void ac_destroy(ac_ctx* ctx) {
     if (!ctx) return;
+    if (ctx->warm.joinable()) ctx->warm.join();
     for (ac_ctx* p : ctx->peers) ac_destroy(p);
     (void)hipSetDevice(ctx->device);
     if (ctx->comm) (void)rccl().comm_destroy(ctx->comm);

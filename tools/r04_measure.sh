@@ -9,6 +9,7 @@
 #   copiers   copier-workgroup count A/B at cfg4 and on the shard
 #   cfg2      cfg2 bench x3 (400 steps) with stage trace
 #   stamps    per-wave timelines (resident cfg2 launch, staged calls)
+#   pmc       SQ issue/wait counters, WRITE/FETCH_SIZE and a kernel trace of the resident cfg2 kernel
 set -u
 OUT=$1; shift
 case $OUT in /*) ;; *) OUT=${GRAFT_REPO_ROOT:-$(pwd)}/$OUT ;; esac
@@ -50,6 +51,18 @@ copiers)
 stamps)  # per-wave timelines of a -DAC_STAMPS build (tools/variants.sh stamps "-DAC_STAMPS")
   run stamps_resident 120 env APPROX_COUNTER_AMD_LIB=build/var/stamps/libapprox_counter_amd.so python3 tools/stamps.py
   run stamps_staged 120 env APPROX_COUNTER_AMD_LIB=build/var/stamps/libapprox_counter_amd.so python3 tools/stage_stamps.py --calls 40 ;;
+pmc)  # issue-time attribution of the resident cfg2 count kernel (20 launches of tools/kernel_run.py per pass)
+  for c in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_SALU SQ_ACTIVE_INST_LDS" \
+           "SQ_WAIT_INST_LDS SQ_ACTIVE_INST_SCA SQ_INSTS_VALU SQ_WAVES SQ_INSTS_SALU SQ_INSTS_LDS SQ_LEVEL_WAVES SQ_BUSY_CU_CYCLES" \
+           "WRITE_SIZE" "FETCH_SIZE"; do
+    n=$(echo $c | cut -d' ' -f1)
+    ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 60 rocprofv3 --pmc $c -d "$OUT/pmc_$n" -o run -- \
+      python3 "$GRAFT_REPO_ROOT/tools/kernel_run.py" --config cfg2 --launches 20 ) > "$OUT/pmc_$n.log" 2>&1 || { echo "pmc $n failed"; exit 3; }
+    echo "== pmc $n ok" | tee -a "$OUT/summary.log"
+  done
+  ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 90 rocprofv3 --kernel-trace --stats -d "$OUT/trace_cfg2" -o run -- \
+    python3 "$GRAFT_REPO_ROOT/tools/kernel_run.py" --config cfg2 --launches 50 --warmup 150 ) > "$OUT/trace_cfg2.log" 2>&1 || exit 4
+  echo "== trace ok" | tee -a "$OUT/summary.log" ;;
 cfg2)
   for i in 1 2 3; do
     run cfg2_$i 200 env AC_STAGE_TRACE=1 python3 bench.py --steps 400 --warmup 10 $BQ
