@@ -292,7 +292,17 @@ struct StageLaunch {
     uint32_t* err_out = nullptr;  // device word the launch's error bits are also or-ed into (submits: ac_check)
     uint32_t tag = 0;              // tagged completion (wm_count.h LaunchArgs::tag)
     uint64_t* grp_err = nullptr;   // its per-group error words (device-visible pinned address)
+    uint32_t copiers = 0;          // copier workgroups (wm_count.h LaunchArgs::copier_wgs; 0: every workgroup)
 };
+
+// Who stages a staged launch (wm_count.h LaunchArgs::copier_wgs): while its tickets (chunks plus one
+// host poller per segment) stay below half the workgroups, every workgroup's wave 0 claims them --
+// those chunks are packed within microseconds of the launch (cfg2: 164 tickets, 1,024 workgroups).
+// Above that, chunks keep arriving over the whole packing time and a workgroup holding one would hold
+// its waves with it, so a few copier workgroups stage everything and the others count as chunks land.
+uint32_t stage_copiers(uint64_t tickets, uint64_t resident_waves) {
+    return 2ull * tickets > resident_waves / AC_WAVES_PER_BLOCK ? stage_copier_wgs() : 0u;
+}
 
 // Joins ac_create's warm-up thread (once) and takes the resident-wave counts it queried.
 void ensure_warm(ac_ctx* ctx) {
@@ -483,14 +493,8 @@ ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hi
         a.err_out = stage->err_out;
         a.tag = stage->tag;
         a.grp_err = stage->grp_err;
-        // Who stages (wm_count.h LaunchArgs::copier_wgs): while a call's tickets (its chunks and one
-        // host poller per segment) stay below half the workgroups, every workgroup's wave 0 claims
-        // them -- those chunks are packed within microseconds of the launch (cfg2: 164 tickets,
-        // 1,024 workgroups).  Above that, chunks keep arriving over the whole packing time and a
-        // workgroup holding one would hold its waves with it, so a few copier workgroups stage
-        // everything and the others count as the chunks land.
         const uint64_t blocks = (wave + AC_WAVES_PER_BLOCK - 1) / AC_WAVES_PER_BLOCK;
-        if (2ull * (total_chunks + n) > blocks) a.copier_wgs = (uint32_t)std::min<uint64_t>(blocks, stage_copier_wgs());
+        a.copier_wgs = (uint32_t)std::min<uint64_t>(blocks, stage->copiers);
     }
     // the equal-window instantiation when every live segment has equal windows (their fit in the
     // image checked above)
@@ -1833,6 +1837,26 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
             stg.dst[j] = (uint8_t*)(d + p.off_kmers[j]);
             stg.chunks[j] = j < pre ? 0u : (uint32_t)((region[j] + AC_STAGE_CHUNK - 1) / AC_STAGE_CHUNK);
             stg.codes_off[j] = (uint32_t)(p.off_codes[j] - p.off_kmers[j]);
+        }
+        {
+            ensure_warm(ctx);
+            const uint32_t P = acamd::pack_factor(k);
+            if (!ctx->resident[P]) AC_HIP(ctx, acamd::resident_waves(P, ctx->cu_count, &ctx->resident[P]));
+            uint64_t tickets = 0;
+            for (uint32_t j = 0; j < p.n; ++j) tickets += stg.chunks[j] ? stg.chunks[j] + 1u : 0u;
+            stg.copiers = stage_copiers(tickets, ctx->resident[P]);
+        }
+        // A large call (copier workgroups) packs its jobs' tasks interleaved, so every segment's
+        // windows arrive from the start and no segment's waves sit idle while the jobs before it are
+        // packed (each copier workgroup starts on its own segment, wm_count.hip).  Small calls keep
+        // job order (see above).
+        if (stg.copiers && p.n > 1 && pre == 0) {
+            std::vector<Task> by_job[AC_MAX_JOBS];
+            for (const Task& x : tasks) by_job[x.job].push_back(x);
+            tasks.clear();
+            for (size_t i = 0; tasks.size() < task_n.size(); ++i)
+                for (uint32_t j = 0; j < p.n; ++j)
+                    if (i < by_job[j].size()) tasks.push_back(by_job[j][i]);
         }
         // (the slot's event is recorded after the publishing loop, not right after the launch: the
         // caller's first progress records went out 1.2 us later with it there)

@@ -627,9 +627,11 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
         // the k-mer section fills whole chunks and is in the pinned block before the launch
         const uint32_t pre_chunks = sg.stage_codes_off / AC_STAGE_CHUNK;
         if (a.copier_wgs && blockIdx.x < a.copier_wgs) {
-            // Copier workgroup of a large call: every wave serves every segment's tickets, segments
-            // in the order the host packs them, before the workgroup counts like the others.
-            for (uint32_t s2 = 0; s2 < a.n_segs; ++s2) {
+            // Copier workgroup of a large call: every wave serves every segment's tickets, starting
+            // with segment (workgroup mod segments) -- the host packs a large call's jobs interleaved,
+            // so all segments arrive together -- before the workgroup counts like the others.
+            for (uint32_t i2 = 0; i2 < a.n_segs; ++i2) {
+                const uint32_t s2 = (blockIdx.x + i2) % a.n_segs;
                 const SegDev& c2 = a.seg[s2];
                 if (!c2.stage_chunks) continue;
                 if (!__builtin_amdgcn_readfirstlane((uint32_t)stage_copy(
