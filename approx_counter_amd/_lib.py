@@ -132,8 +132,9 @@ def load():
     L.ac_check.restype = ctypes.c_int
     L.ac_stage_mode.argtypes = [vp]
     L.ac_stage_mode.restype = ctypes.c_int
-    L.ac_testing_stage_hooks.argtypes = [ctypes.c_uint32]
-    L.ac_testing_stage_hooks.restype = ctypes.c_uint32
+    if hasattr(L, "ac_testing_stage_hooks"):  # (an A/B build of an older ABI may lack it)
+        L.ac_testing_stage_hooks.argtypes = [ctypes.c_uint32]
+        L.ac_testing_stage_hooks.restype = ctypes.c_uint32
     L.ac_exact_path.argtypes = [vp]
     L.ac_exact_path.restype = ctypes.c_int
     pint = ctypes.POINTER(ctypes.c_int)

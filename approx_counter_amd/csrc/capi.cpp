@@ -301,7 +301,13 @@ struct StageLaunch {
 // Above that, chunks keep arriving over the whole packing time and a workgroup holding one would hold
 // its waves with it, so a few copier workgroups stage everything and the others count as chunks land.
 uint32_t stage_copiers(uint64_t tickets, uint64_t resident_waves) {
-    return 2ull * tickets > resident_waves / AC_WAVES_PER_BLOCK ? stage_copier_wgs() : 0u;
+    // (AC_COPIER_MIN_TICKETS: the threshold instead of half the workgroups, for A/B runs)
+    static const int64_t min_tickets = [] {
+        const char* e = std::getenv("AC_COPIER_MIN_TICKETS");
+        return e ? (int64_t)std::atoll(e) : (int64_t)-1;
+    }();
+    const uint64_t th = min_tickets >= 0 ? (uint64_t)min_tickets : resident_waves / AC_WAVES_PER_BLOCK / 2;
+    return tickets > th ? stage_copier_wgs() : 0u;
 }
 
 // Joins ac_create's warm-up thread (once) and takes the resident-wave counts it queried.

@@ -425,7 +425,10 @@ __attribute__((target("avx512f,avx512bw,avx512vl"))) uint32_t pack_equal_records
     }
     uint32_t flags = 0;
     uint64_t pos = first;
-    bool stream = ((uintptr_t)(codes + pos / 16) % 32u) == 0u && (S % 128u) == 0u;
+#ifndef AC_PACK_STREAM
+#define AC_PACK_STREAM 1  // (A/B builds: 0 = plain stores)
+#endif
+    bool stream = AC_PACK_STREAM && ((uintptr_t)(codes + pos / 16) % 32u) == 0u && (S % 128u) == 0u;
     const bool streamed = stream;
     for (uint32_t w = w0; w < w1; ++w, pos += S) {
         if (__builtin_expect(length[w] != L, 0)) {

@@ -316,9 +316,21 @@ __device__ __forceinline__ uint32_t wave_load(const uint32_t* p) {  // lane 0's 
 __device__ __forceinline__ void wave_store(uint32_t* p, uint32_t v) {
     if ((threadIdx.x & 63u) == 0) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ bool stage_late(uint64_t t0) {
-    return __builtin_amdgcn_s_memrealtime() - t0 > AC_STAGE_TIMEOUT_TICKS;
-}
+// A staged wait's bound: AC_STAGE_TIMEOUT_TICKS without progress.  The clock is read lazily -- only on
+// a poll that saw no progress (the first such poll starts it), and progress() stops it -- so a wait
+// that never stalls, e.g. a chunk copy whose chunk is already packed, reads no clock at all.
+struct StageClock {
+    uint64_t t0 = 0;
+    __device__ __forceinline__ void progress() { t0 = 0; }
+    __device__ __forceinline__ bool late() {
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        if (t0 == 0) {
+            t0 = now;
+            return false;
+        }
+        return now - t0 > AC_STAGE_TIMEOUT_TICKS;
+    }
+};
 
 // Claims and serves tickets until none is left; false on timeout.  Chunks below `pre_chunks` (the
 // k-mer section, in place in the pinned block before the launch) are copied without waiting.
@@ -327,13 +339,13 @@ __device__ __attribute__((noinline)) bool stage_copy(const uint8_t* src, uint8_t
                                                      uint32_t* chunk_gen, uint32_t gen, uint32_t si) {
     const uint32_t lane = threadIdx.x & 63u;
     const StageWords sw = stage_words(words);
-    uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    StageClock clk;
     for (;;) {
         uint32_t c = 0;
         if (lane == 0) c = __hip_atomic_fetch_add(sw.claim, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         c = __builtin_amdgcn_readfirstlane(c);
         if (c > chunks) return true;
-        t0 = __builtin_amdgcn_s_memrealtime();  // (each ticket's wait is bounded on its own)
+        clk.progress();  // (each ticket's wait is bounded on its own)
         if (c == 0) {  // the segment's host poller
             // The header's four words in ONE 16-byte system-scope load (one PCIe read): the host
             // stores the progress record as one 8-byte store and the flag after INFO, so a read
@@ -363,7 +375,7 @@ __device__ __attribute__((noinline)) bool stage_copy(const uint8_t* src, uint8_t
                         __hip_atomic_store(sw.avail + lane * AC_QUEUE_LINE, ready, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
                     published = ready;
-                    t0 = __builtin_amdgcn_s_memrealtime();  // the host is making progress
+                    clk.progress();  // the host is making progress
                 }
                 if (fin) {
                     stage_stamp(si, 0);
@@ -373,7 +385,7 @@ __device__ __attribute__((noinline)) bool stage_copy(const uint8_t* src, uint8_t
                     wave_store(sw.fin, 1u);
                     break;
                 }
-                if (stage_late(t0)) return false;
+                if (clk.late()) return false;
                 __builtin_amdgcn_s_sleep(8);
             }
             continue;
@@ -398,8 +410,8 @@ __device__ __attribute__((noinline)) bool stage_copy(const uint8_t* src, uint8_t
             }
             if (av > seen) {
                 seen = av;
-                t0 = __builtin_amdgcn_s_memrealtime();
-            } else if (stage_late(t0)) {
+                clk.progress();
+            } else if (clk.late()) {
                 return false;
             }
             __builtin_amdgcn_s_sleep(8);
@@ -412,12 +424,12 @@ __device__ __attribute__((noinline)) bool stage_copy(const uint8_t* src, uint8_t
         if (x >= AC_COPY_AHEAD) {
             uint32_t* my_done = sw.done + (x % AC_STAGE_REPL) * AC_QUEUE_LINE;
             uint32_t dn = 0, dseen = 0;
-            t0 = __builtin_amdgcn_s_memrealtime();
+            clk.progress();
             while ((dn = wave_load(my_done)) < x - AC_COPY_AHEAD) {
                 if (dn > dseen) {  // (the copies ahead of it are moving)
                     dseen = dn;
-                    t0 = __builtin_amdgcn_s_memrealtime();
-                } else if (stage_late(t0)) {
+                    clk.progress();
+                } else if (clk.late()) {
                     return false;
                 }
                 __builtin_amdgcn_s_sleep(2);
@@ -453,13 +465,13 @@ __device__ __attribute__((noinline)) bool stage_copy(const uint8_t* src, uint8_t
 __device__ __attribute__((noinline)) uint32_t stage_wait_all(uint32_t* words, uint32_t chunks, uint32_t replica,
                                                              uint32_t* err) {
     const StageWords sw = stage_words(words);
-    uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    StageClock clk;
     uint32_t dn = 0, seen = 0;
     while ((dn = wave_load(sw.done + replica * AC_QUEUE_LINE)) < chunks) {
         if (dn > seen) {  // copies are landing: the wait's clock restarts
             seen = dn;
-            t0 = __builtin_amdgcn_s_memrealtime();
-        } else if (stage_late(t0)) {
+            clk.progress();
+        } else if (clk.late()) {
             if ((threadIdx.x & 63u) == 0) atomicOr(err, AC_DEVERR_STAGE);
             return ~0u;
         }
@@ -489,7 +501,7 @@ __device__ __forceinline__ uint64_t stage_gate(uint32_t* words, const uint32_t* 
                                                          uint32_t* err, uint32_t pre = 0u) {
     const uint32_t lane = threadIdx.x & 63u;
     const StageWords sw = stage_words(words);
-    uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    StageClock clk;
     const uint32_t x0 = r0 / AC_STAGE_CHUNK, x1 = (r1 - 1u) / AC_STAGE_CHUNK;
     // (more chunks than lanes, or past the launch's chunks: wait for the whole segment)
     const uint32_t nx = (x1 < chunks && x1 - x0 < 62u) ? x1 - x0 + 1u : 0u;
@@ -510,8 +522,8 @@ __device__ __forceinline__ uint64_t stage_gate(uint32_t* words, const uint32_t* 
         in_prefix = nx && (r1 <= pre || av >= r1);
         if (dn + av != seen) {
             seen = dn + av;
-            t0 = __builtin_amdgcn_s_memrealtime();
-        } else if (stage_late(t0)) {
+            clk.progress();
+        } else if (clk.late()) {
             if (lane == 0) atomicOr(err, AC_DEVERR_STAGE);
             return ~0u;
         }

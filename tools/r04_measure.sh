@@ -9,6 +9,7 @@
 #   copiers   copier-workgroup count A/B at cfg4 and on the shard
 #   cfg2      cfg2 bench x3 (400 steps) with stage trace
 #   stamps    per-wave timelines (resident cfg2 launch, staged calls)
+#   ab        same-box A/B of the cfg2 stage (round-3 library, copier modes, packer stores, copy-ahead)
 #   pmc       SQ issue/wait counters, WRITE/FETCH_SIZE and a kernel trace of the resident cfg2 kernel
 set -u
 OUT=$1; shift
@@ -63,6 +64,29 @@ pmc)  # issue-time attribution of the resident cfg2 count kernel (20 launches of
   ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 90 rocprofv3 --kernel-trace --stats -d "$OUT/trace_cfg2" -o run -- \
     python3 "$GRAFT_REPO_ROOT/tools/kernel_run.py" --config cfg2 --launches 50 --warmup 150 ) > "$OUT/trace_cfg2.log" 2>&1 || exit 4
   echo "== trace ok" | tee -a "$OUT/summary.log" ;;
+ab)  # same-box A/B of the cfg2 stage (400 steps each, interleaved twice): round-3 library, this tree,
+    # copier workgroups for small calls too, plain stores in the packer, 64 chunks of copy-ahead
+  B="python3 bench.py --steps 400 --warmup 20 --no-cpu-baseline --no-pipelined --no-kernel-leg"
+  for rep in 1 2; do
+    run ab_r03_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/r03/libapprox_counter_amd.so $B
+    run ab_main_$rep 120 $B
+    for w in 16 32 64; do run ab_cw${w}_$rep 120 env AC_COPIER_MIN_TICKETS=0 AC_COPIER_WGS=$w $B; done
+    run ab_nostream_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/nostream/libapprox_counter_amd.so $B
+    run ab_ahead64_cw32_$rep 120 env AC_COPIER_MIN_TICKETS=0 AC_COPIER_WGS=32 APPROX_COUNTER_AMD_LIB=build/var/ahead64/libapprox_counter_amd.so $B
+  done ;;
+ab2)  # same-box A/B: round-3 library vs this tree (small calls all-workgroup or copier staging), cfg2; cfg3 / cfg5
+  B="python3 bench.py --steps 400 --warmup 20 --no-cpu-baseline --no-pipelined --no-kernel-leg"
+  for rep in 1 2; do
+    run ab_r03_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/r03/libapprox_counter_amd.so $B
+    run ab_main_$rep 120 $B
+    for w in 8 16 32; do run ab_cw${w}_$rep 120 env AC_COPIER_MIN_TICKETS=0 AC_COPIER_WGS=$w $B; done
+  done
+  for c in cfg3 cfg5; do
+    for rep in 1 2; do
+      run ab_${c}_r03_$rep 200 env APPROX_COUNTER_AMD_LIB=build/var/r03/libapprox_counter_amd.so python3 bench.py --config $c --steps 30 --warmup 5 --no-cpu-baseline --no-pipelined --no-kernel-leg
+      for w in 16 32; do run ab_${c}_cw${w}_$rep 200 env AC_COPIER_WGS=$w python3 bench.py --config $c --steps 30 --warmup 5 --no-cpu-baseline --no-pipelined --no-kernel-leg; done
+    done
+  done ;;
 cfg2)
   for i in 1 2 3; do
     run cfg2_$i 200 env AC_STAGE_TRACE=1 python3 bench.py --steps 400 --warmup 10 $BQ

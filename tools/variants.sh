@@ -14,7 +14,7 @@ while [ $# -gt 1 ]; do
     -c approx_counter_amd/csrc/exact_count.hip -o $out/exact_count.o
   /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Iinclude -Iapprox_counter_amd/csrc $flags \
     -x hip -c approx_counter_amd/csrc/capi.cpp -o $out/capi.o
-  g++ -O3 -std=c++17 -fPIC -Wall -c approx_counter_amd/csrc/host_pack.cpp -o $out/host_pack.o
+  g++ -O3 -std=c++17 -fPIC -Wall $flags -c approx_counter_amd/csrc/host_pack.cpp -o $out/host_pack.o
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $out/libapprox_counter_amd.so $out/wm_count.o $out/exact_count.o $out/capi.o $out/host_pack.o -pthread
   echo "built $out"
 done
