@@ -25,7 +25,10 @@ constexpr int words_for(int P) {
 #endif
 }
 // resident count-kernel waves per SIMD, set by the LDS allocation (<= 64 VGPRs with one word)
-constexpr int waves_per_simd(int W) { return W == 2 ? 4 : 8; }
+#ifndef AC_W2_WAVES
+#define AC_W2_WAVES 4  // (A/B builds: resident waves per SIMD with two lane words)
+#endif
+constexpr int waves_per_simd(int W) { return W == 2 ? AC_W2_WAVES : 8; }
 
 // Device error word bits (ac_check, include/approx_counter_amd.h): a window
 // that is misaligned or reaches past the image was skipped; the kernel found

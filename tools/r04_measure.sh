@@ -10,6 +10,9 @@
 #   cfg2      cfg2 bench x3 (400 steps) with stage trace
 #   stamps    per-wave timelines (resident cfg2 launch, staged calls)
 #   ab        same-box A/B of the cfg2 stage (round-3 library, copier modes, packer stores, copy-ahead)
+#   cli       CLI end to end at 10^4 / 10^5 reads
+#   rehearse  1/2/4-rank cfg4 rehearsal on one GPU (gloo)
+#   prof      kernel trace of bench.py at cfg2
 #   pmc       SQ issue/wait counters, WRITE/FETCH_SIZE and a kernel trace of the resident cfg2 kernel
 set -u
 OUT=$1; shift
@@ -87,6 +90,19 @@ ab2)  # same-box A/B: round-3 library vs this tree (small calls all-workgroup or
       for w in 16 32; do run ab_${c}_cw${w}_$rep 200 env AC_COPIER_WGS=$w python3 bench.py --config $c --steps 30 --warmup 5 --no-cpu-baseline --no-pipelined --no-kernel-leg; done
     done
   done ;;
+cli)  # the drop-in CLI end to end (approximate-count interval from its own log), 10^4 and 10^5 reads, twice
+  for rep in 1 2; do
+    run cli_10000_$rep 300 python3 tools/cli_e2e.py --reads 10000 --lim 500
+    run cli_100000_$rep 400 python3 tools/cli_e2e.py --reads 100000 --lim 2000
+  done ;;
+rehearse)  # the N > 1 bench path with 1 / 2 / 4 ranks sharing this GPU (gloo all-reduce), cfg4 strong
+  ( bash tools/rehearse_ranks.sh "$OUT/rehearsal" cfg4 ) > "$OUT/rehearsal.log" 2>&1 || { echo "rehearsal failed"; tail -20 "$OUT/rehearsal.log"; exit 5; }
+  tail -12 "$OUT/rehearsal.log" | cut -c1-300 ;;
+prof)  # kernel trace of the bench's own run (stage + kernel leg) at cfg2
+  ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_bench" -o run -- \
+    python3 "$GRAFT_REPO_ROOT/bench.py" --steps 100 --warmup 10 --no-cpu-baseline --no-pipelined --kernel-launches 100 ) \
+    > "$OUT/prof_bench.log" 2>&1 || { echo "prof failed"; exit 6; }
+  tail -2 "$OUT/prof_bench.log" | cut -c1-300 ;;
 cfg2)
   for i in 1 2 3; do
     run cfg2_$i 200 env AC_STAGE_TRACE=1 python3 bench.py --steps 400 --warmup 10 $BQ
