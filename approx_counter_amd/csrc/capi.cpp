@@ -1647,6 +1647,9 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
     // progress a finished task at a time, so its tasks stay at most 2,048 windows (~20 us of one
     // thread's packing): a large call's first windows then reach the GPU within tens of microseconds
     // rather than after a 1/(4 x participants) share of the whole call.
+    // (Packing a small call with part of the pool -- the others sleeping through it -- was slower:
+    // cfg2 stage p50 0.129-0.138 vs 0.120-0.122 ms, with multi-ms stalls from waking the sleepers at
+    // every call; profiles/r04_m6/ab_table.txt.)
     const uint64_t per = std::max<uint64_t>(
         256, std::min<uint64_t>(p.early ? 2048 : 65536, total_w / (4ull * pool.size()) + 1));
     std::vector<Task> tasks;

@@ -103,6 +103,18 @@ prof)  # kernel trace of the bench's own run (stage + kernel leg) at cfg2
     python3 "$GRAFT_REPO_ROOT/bench.py" --steps 100 --warmup 10 --no-cpu-baseline --no-pipelined --kernel-launches 100 ) \
     > "$OUT/prof_bench.log" 2>&1 || { echo "prof failed"; exit 6; }
   tail -2 "$OUT/prof_bench.log" | cut -c1-300 ;;
+ab3)  # packing teams: same-box cfg2 stage A/B vs the round-3 library (400 steps), then 2,000-step runs for the
+     # step-time tail, and the host packer alone with teams of 2 / 4 / 8 / 16 of the 16-thread pool
+  B="python3 bench.py --steps 400 --warmup 20 --no-cpu-baseline --no-pipelined --no-kernel-leg"
+  for rep in 1 2 3; do
+    run ab_r03_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/r03/libapprox_counter_amd.so $B
+    run ab_main_$rep 120 $B
+    run ab_cw16_$rep 120 env AC_COPIER_MIN_TICKETS=0 AC_COPIER_WGS=16 $B
+  done
+  run long_r03 200 env APPROX_COUNTER_AMD_LIB=build/var/r03/libapprox_counter_amd.so python3 bench.py --steps 2000 --warmup 20 --no-cpu-baseline --no-pipelined --no-kernel-leg
+  run long_main 200 python3 bench.py --steps 2000 --warmup 20 --no-cpu-baseline --no-pipelined --no-kernel-leg
+  g++ -O3 -std=c++17 -pthread -Iapprox_counter_amd/csrc tools/pack_bench.cpp approx_counter_amd/csrc/host_pack.cpp -o "$OUT/pack_bench" || exit 2
+  for t in 2 4 8 16; do run pack_team$t 60 "$OUT/pack_bench" 10000 2000 0 1 $t; done ;;
 cfg2)
   for i in 1 2 3; do
     run cfg2_$i 200 env AC_STAGE_TRACE=1 python3 bench.py --steps 400 --warmup 10 $BQ
