@@ -2,7 +2,7 @@
 // of n Dna5 windows (100 / 101 bases) packed by the pool the way ac_error_count_jobs does
 // (tasks in job order, the caller helping), timing when job 0 and job 1 are complete.
 //   g++ -O3 -std=c++17 -pthread -Iapprox_counter_amd/csrc tools/pack_bench.cpp \
-//       approx_counter_amd/csrc/host_pack.cpp -o /tmp/pack_bench && /tmp/pack_bench [n] [iters] [per] [records] [team]
+//       approx_counter_amd/csrc/host_pack.cpp -o /tmp/pack_bench && /tmp/pack_bench [n] [iters] [per] [records]
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -23,7 +23,6 @@ int main(int argc, char** argv) {
     const uint32_t per_arg = argc > 3 ? (uint32_t)std::atoi(argv[3]) : 0;
     // records = 1: the stage's equal-window form (inline N records, no descriptors), 0.1 % N bases
     const bool records = argc > 4 ? std::atoi(argv[4]) != 0 : true;
-    const uint32_t team = argc > 5 ? (uint32_t)std::atoi(argv[5]) : 0u;  // participants per call (0: the pool)
     acamd::WorkPool& pool = acamd::host_pool();
     std::mt19937 rng(1);
     struct Job {
@@ -68,7 +67,7 @@ int main(int argc, char** argv) {
             left[x.j].fetch_sub(1, std::memory_order_release);
         };
         const double t0 = now_us();
-        pool.begin((uint32_t)tasks.size(), fn, team);
+        pool.begin((uint32_t)tasks.size(), fn);
         pool.help(t_split);
         while (left[0].load(std::memory_order_acquire)) __builtin_ia32_pause();
         const double t1 = now_us();
@@ -87,8 +86,8 @@ int main(int argc, char** argv) {
     std::sort(d0.begin(), d0.end());
     std::sort(d1.begin(), d1.end());
     auto q = [](const std::vector<double>& v, double f) { return v[(size_t)(f * (v.size() - 1))]; };
-    std::printf("participants %u (team %u), %zu tasks of %u windows, n=%u per job, records %d\n", pool.size(), team,
-                tasks.size(), per, n, (int)records);
+    std::printf("participants %u, %zu tasks of %u windows, n=%u per job, records %d\n", pool.size(), tasks.size(), per,
+                n, (int)records);
     std::printf("job 0 packed: p10 %.1f p50 %.1f p90 %.1f max %.1f us\n", q(d0, .1), q(d0, .5), q(d0, .9), d0.back());
     std::printf("both packed:  p10 %.1f p50 %.1f p90 %.1f max %.1f us\n", q(d1, .1), q(d1, .5), q(d1, .9), d1.back());
     return 0;

@@ -114,7 +114,7 @@ ab3)  # packing teams: same-box cfg2 stage A/B vs the round-3 library (400 steps
   run long_r03 200 env APPROX_COUNTER_AMD_LIB=build/var/r03/libapprox_counter_amd.so python3 bench.py --steps 2000 --warmup 20 --no-cpu-baseline --no-pipelined --no-kernel-leg
   run long_main 200 python3 bench.py --steps 2000 --warmup 20 --no-cpu-baseline --no-pipelined --no-kernel-leg
   g++ -O3 -std=c++17 -pthread -Iapprox_counter_amd/csrc tools/pack_bench.cpp approx_counter_amd/csrc/host_pack.cpp -o "$OUT/pack_bench" || exit 2
-  for t in 2 4 8 16; do run pack_team$t 60 "$OUT/pack_bench" 10000 2000 0 1 $t; done ;;
+  for t in 2 4 8 16; do run pack_threads$t 60 env AC_HOST_THREADS=$t "$OUT/pack_bench" 10000 2000 0 1; done ;;
 cfg2)
   for i in 1 2 3; do
     run cfg2_$i 200 env AC_STAGE_TRACE=1 python3 bench.py --steps 400 --warmup 10 $BQ
