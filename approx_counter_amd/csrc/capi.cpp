@@ -295,19 +295,20 @@ struct StageLaunch {
     uint32_t copiers = 0;          // copier workgroups (wm_count.h LaunchArgs::copier_wgs; 0: every workgroup)
 };
 
-// Who stages a staged launch (wm_count.h LaunchArgs::copier_wgs): while its tickets (chunks plus one
-// host poller per segment) stay below half the workgroups, every workgroup's wave 0 claims them --
-// those chunks are packed within microseconds of the launch (cfg2: 164 tickets, 1,024 workgroups).
-// Above that, chunks keep arriving over the whole packing time and a workgroup holding one would hold
-// its waves with it, so a few copier workgroups stage everything and the others count as chunks land.
-uint32_t stage_copiers(uint64_t tickets, uint64_t resident_waves) {
-    // (AC_COPIER_MIN_TICKETS: the threshold instead of half the workgroups, for A/B runs)
+// Who stages a staged launch (wm_count.h LaunchArgs::copier_wgs): a few copier workgroups stage
+// every chunk while the others count as chunks land.  Round 3 let every workgroup's wave 0 claim
+// tickets instead: fine while a call's chunks are packed within microseconds of the launch, but each
+// such wave held its workgroup's other three waves at the table barrier until its chunk was in (the
+// p90 workgroup started counting ~30 us into a cfg2 launch, profiles/r04_m1/stamps_staged.log), and a
+// large call's chunks arrive over the whole packing time.  Copier workgroups at cfg2: stage p50
+// 0.1143-0.1146 vs 0.1189-0.1193 ms (same box, profiles/r04_m7/ab_table.txt).  AC_COPIER_MIN_TICKETS
+// keeps the round-3 scheme up to that many tickets (A/B runs).
+uint32_t stage_copiers(uint64_t tickets, uint64_t /*resident_waves*/) {
     static const int64_t min_tickets = [] {
         const char* e = std::getenv("AC_COPIER_MIN_TICKETS");
-        return e ? (int64_t)std::atoll(e) : (int64_t)-1;
+        return e ? (int64_t)std::atoll(e) : (int64_t)0;
     }();
-    const uint64_t th = min_tickets >= 0 ? (uint64_t)min_tickets : resident_waves / AC_WAVES_PER_BLOCK / 2;
-    return tickets > th ? stage_copier_wgs() : 0u;
+    return tickets > (uint64_t)min_tickets ? stage_copier_wgs() : 0u;
 }
 
 // Joins ac_create's warm-up thread (once) and takes the resident-wave counts it queried.
@@ -1650,8 +1651,13 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
     // (Packing a small call with part of the pool -- the others sleeping through it -- was slower:
     // cfg2 stage p50 0.129-0.138 vs 0.120-0.122 ms, with multi-ms stalls from waking the sleepers at
     // every call; profiles/r04_m6/ab_table.txt.)
+    // Tasks of at least 1,280 windows: with the round-4 packer (~2.3 ns per 100-base window) a
+    // 313-window task is shorter than the pool's contended claim, so a cfg2 end took ~15 us to pack
+    // on 16 threads; 1,280 gave cfg2 stage p50 0.1189-0.1193 vs 0.1223-0.1243 ms at 256, 640 and 2,560
+    // in between (same box, profiles/r04_m7/ab_table.txt).  AC_TASK_WINDOWS overrides (A/B runs).
+    static const uint64_t min_task = (uint64_t)std::max(1, env_int("AC_TASK_WINDOWS", 1280));
     const uint64_t per = std::max<uint64_t>(
-        256, std::min<uint64_t>(p.early ? 2048 : 65536, total_w / (4ull * pool.size()) + 1));
+        min_task, std::min<uint64_t>(p.early ? std::max<uint64_t>(2048, min_task) : 65536, total_w / (4ull * pool.size()) + 1));
     std::vector<Task> tasks;
     for (uint32_t j = 0; j < p.n; ++j) {
         if (!jobs[j].n_kmers) continue;  // nothing to count: its windows are not needed

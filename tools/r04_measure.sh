@@ -115,6 +115,23 @@ ab3)  # packing teams: same-box cfg2 stage A/B vs the round-3 library (400 steps
   run long_main 200 python3 bench.py --steps 2000 --warmup 20 --no-cpu-baseline --no-pipelined --no-kernel-leg
   g++ -O3 -std=c++17 -pthread -Iapprox_counter_amd/csrc tools/pack_bench.cpp approx_counter_amd/csrc/host_pack.cpp -o "$OUT/pack_bench" || exit 2
   for t in 2 4 8 16; do run pack_threads$t 60 env AC_HOST_THREADS=$t "$OUT/pack_bench" 10000 2000 0 1; done ;;
+ab4)  # packing-task size (windows per task; the 16-participant pool's claims contend on one line) vs round 3
+  B="python3 bench.py --steps 400 --warmup 20 --no-cpu-baseline --no-pipelined --no-kernel-leg"
+  for rep in 1 2; do
+    run ab_r03_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/r03/libapprox_counter_amd.so $B
+    for tw in 256 640 1280 2560; do run ab_task${tw}_$rep 120 env AC_TASK_WINDOWS=$tw $B; done
+    run ab_task1280_cw16_$rep 120 env AC_TASK_WINDOWS=1280 AC_COPIER_MIN_TICKETS=0 AC_COPIER_WGS=16 $B
+  done
+  run long_main 200 python3 bench.py --steps 2000 --warmup 20 --no-cpu-baseline --no-pipelined --no-kernel-leg ;;
+ab5)  # around the new defaults (copier workgroups always, 1,280-window tasks): copier count, task size
+  B="python3 bench.py --steps 400 --warmup 20 --no-cpu-baseline --no-pipelined --no-kernel-leg"
+  for rep in 1 2; do
+    run ab_r03_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/r03/libapprox_counter_amd.so $B
+    run ab_main_$rep 120 $B
+    for w in 8 32; do run ab_cw${w}_$rep 120 env AC_COPIER_WGS=$w $B; done
+    for tw in 960 1664; do run ab_task${tw}_$rep 120 env AC_TASK_WINDOWS=$tw $B; done
+    run ab_ahead64_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/ahead64/libapprox_counter_amd.so $B
+  done ;;
 cfg2)
   for i in 1 2 3; do
     run cfg2_$i 200 env AC_STAGE_TRACE=1 python3 bench.py --steps 400 --warmup 10 $BQ
