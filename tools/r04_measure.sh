@@ -35,6 +35,7 @@ for part in "$@"; do
 case $part in
 tests)
   run tests_bench_path 400 $PYT -m gpu tests/test_gpu_bench_path.py
+  run tests_parity 400 $PYT -m gpu tests/test_gpu_parity.py
   run tests_jobs 400 $PYT -m gpu tests/test_gpu_jobs.py
   run tests_scale 600 $PYT -m gpu tests/test_gpu_scale.py ;;
 suite)
@@ -131,6 +132,14 @@ ab5)  # around the new defaults (copier workgroups always, 1,280-window tasks): 
     for w in 8 32; do run ab_cw${w}_$rep 120 env AC_COPIER_WGS=$w $B; done
     for tw in 960 1664; do run ab_task${tw}_$rep 120 env AC_TASK_WINDOWS=$tw $B; done
     run ab_ahead64_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/ahead64/libapprox_counter_amd.so $B
+  done ;;
+ab6)  # copier tickets of 1 / 4 (default) / 8 chunks vs round 3
+  B="python3 bench.py --steps 400 --warmup 20 --no-cpu-baseline --no-pipelined --no-kernel-leg"
+  for rep in 1 2; do
+    run ab_r03_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/r03/libapprox_counter_amd.so $B
+    run ab_main_$rep 120 $B
+    run ab_group1_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/group1/libapprox_counter_amd.so $B
+    run ab_group8_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/group8/libapprox_counter_amd.so $B
   done ;;
 cfg2)
   for i in 1 2 3; do
