@@ -6,7 +6,7 @@
 // into it, 1 and 8 threads; (2) whether a kernel that already read the region (lines in its
 // L2) sees the host's new data after a host flag, with plain loads, after an acquire fence at
 // system scope, and with nontemporal loads; (3) the kernel's read time of that memory against
-// ordinary device memory.  Build: hipcc -O2 --offload-arch=gfx950 tools/bar_probe.hip -o bar_probe
+// ordinary device memory.  Build: hipcc -O2 --offload-arch=gfx950 -Xarch_host -mavx512f tools/bar_probe.hip -o bar_probe
 #include <hip/hip_runtime.h>
 #include <immintrin.h>
 #include <signal.h>
@@ -102,12 +102,22 @@ int main() {
     CK(hipHostGetDevicePointer((void**)&flag_d, flag, 0));
     CK(hipHostGetDevicePointer((void**)&bad_d, bad, 0));
     hipPointerAttribute_t at;
-    if (hipPointerGetAttributes(&at, fg) == hipSuccess)
-        std::printf("fine-grained allocation: type %d device %d host pointer %p device pointer %p\n", (int)at.type,
-                    at.device, at.hostPointer, at.devicePointer);
+    if (hipPointerGetAttributes(&at, fg) != hipSuccess) {
+        std::printf("fine-grained allocation: no pointer attributes; not probing host stores\n");
+        return 0;
+    }
+    std::printf("fine-grained allocation: type %d device %d host pointer %p device pointer %p\n", (int)at.type,
+                at.device, at.hostPointer, at.devicePointer);
+    // Refuse rather than fault: without a host mapping of the allocation (hostPointer NULL,
+    // as on some boxes of this pool, profiles/r03_bar_probe.log) a host store to it is not a BAR write.
+    if (!at.hostPointer) {
+        std::printf("no host mapping of the device allocation on this box: host writes into device memory "
+                    "are not available here; nothing probed\n");
+        return 0;
+    }
 
     // (1) host write bandwidth
-    fg[0] = 7;  // SIGSEGV here = no host mapping
+    fg[0] = 7;
     std::printf("host store + load back: %u\n", fg[0]);
     for (int threads : {1, 4, 8}) {
         std::vector<double> t;
