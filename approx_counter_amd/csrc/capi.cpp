@@ -1679,7 +1679,12 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
     if (total_w <= (1u << 18)) {  // a serial pass is cheaper than a pool round trip up to ~256k windows
         for (uint32_t t = 0; t < (uint32_t)tasks.size(); ++t) span_of(t);
     } else {
-        pool.run((uint32_t)tasks.size(), span_of);
+        // in blocks of consecutive tasks, ~2 per participant: one pool task per packing task (~1,000 at
+        // cfg4) spent ~220 us in contended claims for a ~30 us scan (profiles/r04_m1/bench_cfg4.log)
+        const uint32_t nt = (uint32_t)tasks.size(), nb = std::min<uint32_t>(nt, 2u * pool.size());
+        pool.run(nb, [&](uint32_t b) {
+            for (uint32_t t = (uint32_t)((uint64_t)nt * b / nb); t < (uint32_t)((uint64_t)nt * (b + 1) / nb); ++t) span_of(t);
+        });
     }
     mark(0);
     // Image of each job: its tasks' ranges back to back; at least one 32-base block.
