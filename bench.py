@@ -8,9 +8,10 @@ A step is one pass of the stage BASELINE.md defines over one batch: both read
 ends of one run (start + end windows, approx_counter.cpp:858), each against its
 own top-`lim` candidates, from HOST buffers to HOST counts -- the sample as a
 StringSet<Dna5String> (one byte per base, what errorCount receives), packed to
-2-bit codes + N bitmap by the library's host worker pool into pinned memory, one
-DMA, ONE fused kernel launch over both ends, (N > 1: one RCCL all-reduce of the
-count vector), counts back.  That is `value`.  Default workload = BASELINE.json
+2-bit codes (N positions inline) by the library's host worker pool into pinned
+memory, pulled into HBM by the count kernel's own copier workgroups while it
+counts -- ONE fused kernel launch over both ends, issued before the packing --
+(N > 1: one RCCL all-reduce of the count vector), counts back.  That is `value`.  Default workload = BASELINE.json
 configs[1] (k=16, sn=10,000, sl=100, lim=500), on seeded synthetic reads
 (SURVEY.md §8(d)).
 
@@ -327,9 +328,9 @@ def main():
         geo = kc.last_launch()
         kc.close()
 
-    # ---- the stage's path (ac_stage_mode, after the cold call above): the early launch for calls
-    # counted in one part (the count kernel launched first, staging each read end itself as soon
-    # as the host has packed it), the DMA path (copy engine, 2-4 parts) for >= 2^17 windows.
+    # ---- the stage's path (ac_stage_mode, after the cold call above): the early launch at every
+    # size (the count kernel launched first, its copier workgroups staging each read end as the host
+    # packs it); the DMA path (copy engine, 2-4 parts) only with AC_STAGE_EARLY=0.
     tune_calls = 0
     while counter.stage_mode() < 0 and tune_calls < 4:
         counter.count_jobs(args.k, jobs)
@@ -450,10 +451,10 @@ def main():
             "config": {"workload": workload_name, "k": args.k, "sn": args.sn, "sl": args.sl, "lim": args.lim,
                        "candidates": n_c, "kmer_bp_per_step": units_job, "kmer_bp_per_rank_step": units_rank,
                        "stage": ("Dna5 host buffers -> "
-                                 + ("1 fused count launch issued first, then per read end: pack (host pool, "
-                                    "pinned; N positions inline in each window's slot) + progress records; the kernel "
-                                    "copies each 4 KB chunk into HBM itself as it is packed and counts a window as "
-                                    "soon as its chunk is in" if stage_path == "early-launch"
+                                 + ("1 fused count launch issued first, then both read ends packed (host pool, "
+                                    "pinned; N positions inline in each window's slot) with progress records; 16 "
+                                    "copier workgroups of the kernel pull each 4 KB chunk into HBM as it is packed "
+                                    "while the others count a window as soon as its chunk is in" if stage_path == "early-launch"
                                     else ("per part (>= 2^17 windows: 2 parts, >= 2^19: 4): pack (host pool, pinned), "
                                           "copy-engine DMA into HBM while the previous part counts"))
                                  + " (both ends)"
@@ -475,8 +476,8 @@ def main():
                             "note": "rank 0's pack pool: GPU-local CPUs split among the local ranks, at most its "
                                     "share of the cgroup CPU quota (ac_host_pool_cpus)"}
         out["stage_path_choice"] = {"path": stage_path, "untimed_calls": tune_calls,
-                                    "note": "ac_stage_mode: early launch for calls counted in one part, DMA parts "
-                                            "for >= 2^17 windows (no timing-based choice since round 3)"}
+                                    "note": "ac_stage_mode: the early launch at every size since round 4 (DMA parts "
+                                            "only with AC_STAGE_EARLY=0)"}
         if kern_ms is not None:
             ops = OPS_PER_BASE_WORD / P * units_rank  # algorithmic lane-ops per launch (this rank)
             achieved = ops / (kern_ms * 1e-3)
