@@ -141,6 +141,21 @@ ab6)  # copier tickets of 1 / 4 (default) / 8 chunks vs round 3
     run ab_group1_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/group1/libapprox_counter_amd.so $B
     run ab_group8_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/group8/libapprox_counter_amd.so $B
   done ;;
+ab7)  # two lane words at 5 resident waves per SIMD (w5 build) vs 4: kernel leg and stage at cfg2, kernel at cfg3
+  for rep in 1 2; do
+    run ab_k4_$rep 120 python3 bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-pipelined --kernel-launches 300
+    run ab_k5_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/w5/libapprox_counter_amd.so python3 bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-pipelined --kernel-launches 300
+    run ab_k4_cfg3_$rep 200 python3 bench.py --config cfg3 --steps 20 --warmup 5 --no-cpu-baseline --no-pipelined
+    run ab_k5_cfg3_$rep 200 env APPROX_COUNTER_AMD_LIB=build/var/w5/libapprox_counter_amd.so python3 bench.py --config cfg3 --steps 20 --warmup 5 --no-cpu-baseline --no-pipelined
+  done ;;
+ab8)  # half items (the queue's last round split by lane word): AC_SPLIT_ROUNDS 0 / 1 / 2, kernel leg + stage
+  for rep in 1 2; do
+    for r in 0 1 2; do
+      run ab_split${r}_$rep 120 env AC_SPLIT_ROUNDS=$r python3 bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-pipelined --kernel-launches 300
+    done
+  done
+  run ab_split1_cfg3 200 env AC_SPLIT_ROUNDS=1 python3 bench.py --config cfg3 --steps 20 --warmup 5 --no-cpu-baseline --no-pipelined
+  run ab_split0_cfg3 200 env AC_SPLIT_ROUNDS=0 python3 bench.py --config cfg3 --steps 20 --warmup 5 --no-cpu-baseline --no-pipelined ;;
 cfg2)
   for i in 1 2 3; do
     run cfg2_$i 200 env AC_STAGE_TRACE=1 python3 bench.py --steps 400 --warmup 10 $BQ
