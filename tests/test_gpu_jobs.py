@@ -446,6 +446,44 @@ def test_large_call_early_launch_copier_workgroups():
     assert np.array_equal(got[sub], oracle.count_myers(16, kmers[sub], win, 16))
 
 
+def test_large_call_four_jobs_mixed():
+    """A large early launch with four jobs (segments): the host packs their tasks interleaved
+    and each copier workgroup starts on its own segment (blockIdx mod segments).  Equal
+    windows with N (inline records), ragged windows (descriptors sent: the segment waits for
+    its whole region), a small job and a job without windows, all in one call -- bit-exact
+    on every candidate of the small jobs and on a candidate subset of the large ones."""
+    rng = np.random.default_rng(17)
+    jobs, exp_fn = [], []
+    # 1: 70k equal windows of 100 bases, 0.2 % N
+    n1 = 70_000
+    w1 = rng.integers(0, 4, size=(n1, 100), dtype=np.uint8)
+    w1[rng.random((n1, 100)) < 0.002] = 4
+    km1 = np.array([int(sum(int(b) << (2 * (15 - i)) for i, b in enumerate(w1[p, 30:46])))
+                    for p in rng.integers(0, n1, size=300)], dtype=np.uint64)
+    jobs.append((km1, ac.Dna5Sample(w1.reshape(-1), np.arange(n1, dtype=np.uint64) * np.uint64(100),
+                                   np.full(n1, 100, np.uint32))))
+    exp_fn.append(lambda sub: oracle.count_myers(16, km1[sub], w1, 16))
+    # 2: 50k ragged windows (60-140 bases)
+    km2, wins2 = cases.planted_case(71, 16, 200, 50_000, win_len=(60, 140), p_n=0.01)
+    jobs.append((km2, ac.Dna5Sample.from_windows(wins2)))
+    exp_fn.append(lambda sub: oracle.count_myers(16, km2[sub], wins2, 16))
+    # 3: a small job; 4: candidates without windows
+    km3, wins3 = cases.planted_case(72, 16, 90, 700, win_len=(101, 101), p_n=0.01)
+    wins3 = [(w + "A" * 101)[:101] for w in wins3]
+    jobs.append((km3, ac.Dna5Sample.from_windows(wins3)))
+    exp_fn.append(lambda sub: oracle.count_myers(16, km3[sub], wins3, 16))
+    km4 = km3[:40].copy()
+    jobs.append((km4, ac.Dna5Sample.from_windows([])))
+    exp_fn.append(lambda sub: np.zeros(len(km4[sub]), np.uint64))
+    with ac.ApproxCounter(0) as c:
+        for _ in range(2):  # both staging slots
+            got = c.count_jobs(16, ac.Jobs(jobs))
+            assert c.stage_mode() == 2
+            for j, (g, f) in enumerate(zip(got, exp_fn)):
+                sub = np.arange(len(g)) if len(g) <= 200 else np.r_[0:12, len(g) - 12:len(g)]
+                assert np.array_equal(g[sub], f(sub)), j
+
+
 def test_dma_parts_path_without_early_launch():
     """AC_STAGE_EARLY=0 keeps round 2's copy-engine path: a call of >= 2^17 windows cut
     into parts, each packed and sent while the previous part counts (ac_stage_mode 0), for

@@ -156,6 +156,15 @@ ab8)  # half items (the queue's last round split by lane word): AC_SPLIT_ROUNDS 
   done
   run ab_split1_cfg3 200 env AC_SPLIT_ROUNDS=1 python3 bench.py --config cfg3 --steps 20 --warmup 5 --no-cpu-baseline --no-pipelined
   run ab_split0_cfg3 200 env AC_SPLIT_ROUNDS=0 python3 bench.py --config cfg3 --steps 20 --warmup 5 --no-cpu-baseline --no-pipelined ;;
+ab9)  # the kernel launched by a pool worker (task 0) while the caller publishes, vs the caller launching
+  B="python3 bench.py --steps 400 --warmup 20 --no-cpu-baseline --no-pipelined --no-kernel-leg"
+  for rep in 1 2 3; do
+    run ab_r03_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/r03/libapprox_counter_amd.so $B
+    run ab_task1_$rep 120 env AC_LAUNCH_TASK=1 $B
+    run ab_task0_$rep 120 env AC_LAUNCH_TASK=0 $B
+  done
+  run ab_task1_shard_t2 200 env AC_HOST_THREADS=2 python3 bench.py --config cfg4 --shard 0/8 --steps 30 --warmup 5 --no-cpu-baseline --no-pipelined --no-kernel-leg
+  run ab_task0_shard_t2 200 env AC_LAUNCH_TASK=0 AC_HOST_THREADS=2 python3 bench.py --config cfg4 --shard 0/8 --steps 30 --warmup 5 --no-cpu-baseline --no-pipelined --no-kernel-leg ;;
 cfg2)
   for i in 1 2 3; do
     run cfg2_$i 200 env AC_STAGE_TRACE=1 python3 bench.py --steps 400 --warmup 10 $BQ
