@@ -152,8 +152,9 @@ def test_inline_n_records(counter, L):
 
 
 def test_inline_n_records_large_call(counter):
-    """The multi-part DMA path (>= 2^17 windows) with inline N records: N-bitmap sent only
-    for the part whose records overflowed."""
+    """A large call (150k windows: the early launch with copier workgroups, both jobs packed
+    interleaved) with inline N records: the N bitmap is sent only for the job whose records
+    overflowed, and its windows with overflowed records wait for it."""
     L = 101
     a = _n_record_windows(7, 90_000, L, [0] * 20 + [1, 2, 3, 4])
     b = _n_record_windows(8, 60_000, L, [0] * 50 + [1, 5])
@@ -465,10 +466,12 @@ def test_large_call_four_jobs_mixed():
     exp_fn.append(lambda sub: oracle.count_myers(16, km1[sub], w1, 16))
     # 2: 50k ragged windows (60-140 bases)
     km2, wins2 = cases.planted_case(71, 16, 200, 50_000, win_len=(60, 140), p_n=0.01)
+    km2 = np.asarray(km2, dtype=np.uint64)
     jobs.append((km2, ac.Dna5Sample.from_windows(wins2)))
     exp_fn.append(lambda sub: oracle.count_myers(16, km2[sub], wins2, 16))
     # 3: a small job; 4: candidates without windows
     km3, wins3 = cases.planted_case(72, 16, 90, 700, win_len=(101, 101), p_n=0.01)
+    km3 = np.asarray(km3, dtype=np.uint64)
     wins3 = [(w + "A" * 101)[:101] for w in wins3]
     jobs.append((km3, ac.Dna5Sample.from_windows(wins3)))
     exp_fn.append(lambda sub: oracle.count_myers(16, km3[sub], wins3, 16))

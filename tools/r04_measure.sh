@@ -165,6 +165,22 @@ ab9)  # the kernel launched by a pool worker (task 0) while the caller publishes
   done
   run ab_task1_shard_t2 200 env AC_HOST_THREADS=2 python3 bench.py --config cfg4 --shard 0/8 --steps 30 --warmup 5 --no-cpu-baseline --no-pipelined --no-kernel-leg
   run ab_task0_shard_t2 200 env AC_LAUNCH_TASK=0 AC_HOST_THREADS=2 python3 bench.py --config cfg4 --shard 0/8 --steps 30 --warmup 5 --no-cpu-baseline --no-pipelined --no-kernel-leg ;;
+ab10)  # fewer resident waves for the cfg2 launch (AC_WAVE_CAP: 3 or 3.5 per SIMD instead of 4), kernel + stage
+  for rep in 1 2; do
+    for c in 0 3072 3584; do
+      run ab_cap${c}_$rep 120 env AC_WAVE_CAP=$c python3 bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-pipelined --kernel-launches 300
+    done
+  done ;;
+ab11)  # the first windows read from the host's pinned block before their chunk is copied, vs not
+  B="python3 bench.py --steps 400 --warmup 20 --no-cpu-baseline --no-pipelined --no-kernel-leg"
+  for rep in 1 2 3 4 5 6; do
+    run ab_host_$rep 120 $B
+    run ab_nohost_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/nohost/libapprox_counter_amd.so $B
+  done
+  for c in cfg5 cfg4; do
+    run ab_host_$c 200 python3 bench.py --config $c --steps 20 --warmup 5 --no-cpu-baseline --no-pipelined --no-kernel-leg
+    run ab_nohost_$c 200 env APPROX_COUNTER_AMD_LIB=build/var/nohost/libapprox_counter_amd.so python3 bench.py --config $c --steps 20 --warmup 5 --no-cpu-baseline --no-pipelined --no-kernel-leg
+  done ;;
 cfg2)
   for i in 1 2 3; do
     run cfg2_$i 200 env AC_STAGE_TRACE=1 python3 bench.py --steps 400 --warmup 10 $BQ
