@@ -332,11 +332,63 @@ struct StageClock {
     }
 };
 
+// Armed launch (LaunchArgs::arm_ticks): waits for the call, seen through the header line `rh` of
+// segment si.  Segment 0's poller decides once, in the launch's device word `dec`: the call came (its
+// first progress record or final header is out: 1) or, after `arm` ticks of s_memrealtime without
+// one, expired (2).  Expiring is a handshake with the host through the ARM word of segment 0's header
+// (wm_count.h): the poller stores EXPIRING, reads the header once more and stores the outcome; the
+// host publishes its first records, then reads the word -- so of a call published just then and an
+// expiry, at least one side sees the other, and the host waits for the outcome when it sees
+// EXPIRING.  The other segments' pollers follow the decision.  True: the call came.
+__device__ __forceinline__ bool stage_arm_wait(__amdgpu_buffer_rsrc_t rh, uint32_t* hdr, uint32_t* dec, uint32_t gen,
+                                               uint32_t si, uint32_t arm, StageClock& clk, bool& late) {
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    const uint32_t lane = threadIdx.x & 63u;
+    late = false;
+    if (si != 0u) {
+        for (;;) {
+            const uint32_t d = wave_load(dec);
+            if (d) return d == 1u;
+            if (clk.late()) {
+                late = true;
+                return false;
+            }
+            __builtin_amdgcn_s_sleep(8);
+        }
+    }
+    auto called = [&]() {
+        const v4u hv = __builtin_amdgcn_raw_buffer_load_b128(rh, 0, 0, 17);  // sc0 sc1: system scope
+        return __builtin_amdgcn_readfirstlane(hv.x) == gen || __builtin_amdgcn_readfirstlane(hv.z) == gen;
+    };
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    bool came = true;
+    while (!called()) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > arm) {
+            uint64_t* aw = (uint64_t*)(hdr + AC_HDR_ARM);
+            if (lane == 0)
+                __hip_atomic_store(aw, ((uint64_t)AC_ARM_EXPIRING << 32) | gen, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+            // the store is out before the header is read again (system-scope fence, vector memory only)
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            came = called();
+            if (lane == 0)
+                __hip_atomic_store(aw, ((uint64_t)(came ? AC_ARM_GO : AC_ARM_EXPIRED) << 32) | gen,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(8);
+    }
+    wave_store(dec, came ? 1u : 2u);
+    return came;
+}
+
 // Claims and serves tickets until none is left; false on timeout.  Chunks below `pre_chunks` (the
 // k-mer section, in place in the pinned block before the launch) are copied without waiting.
+// `arm`: LaunchArgs::arm_ticks (an armed launch's pollers first wait for the call, stage_arm_wait).
 __device__ __attribute__((noinline)) bool stage_copy(const uint8_t* src, uint8_t* dst, uint32_t chunks,
                                                      uint32_t pre_chunks, uint32_t* hdr, uint32_t* words,
-                                                     uint32_t* chunk_gen, uint32_t gen, uint32_t si) {
+                                                     uint32_t* chunk_gen, uint32_t gen, uint32_t si, uint32_t arm) {
     const uint32_t lane = threadIdx.x & 63u;
     const StageWords sw = stage_words(words);
     StageClock clk;
@@ -354,6 +406,20 @@ __device__ __attribute__((noinline)) bool stage_copy(const uint8_t* src, uint8_t
             static_assert(AC_HDR_PGEN == 0 && AC_HDR_READY == 1 && AC_HDR_FLAG == 2 && AC_HDR_INFO == 3,
                           "header layout");
             const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc((void*)hdr, 0, 16, 0x00020000);
+            if (arm) {
+                bool late = false;
+                if (!stage_arm_wait(rh, hdr, words + (AC_STAGE_L_ARM - AC_STAGE_L_SEG(si)) * AC_QUEUE_LINE, gen, si,
+                                    arm, clk, late)) {
+                    // expired (or, never expected, no decision): every wave skips the segment
+                    wave_store(sw.verdict, ~0u);
+                    wave_store(sw.bytes, 0u);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    wave_store(sw.fin, 1u);
+                    if (late) return false;
+                    continue;
+                }
+                clk.progress();
+            }
             uint32_t published = 0;
             for (;;) {
                 const v4u hv = __builtin_amdgcn_raw_buffer_load_b128(rh, 0, 0, 17);  // sc0 sc1: system scope
@@ -494,7 +560,8 @@ __device__ __attribute__((noinline)) uint32_t stage_wait_all(uint32_t* words, ui
 #endif
 // Early counting: waits until region bytes [r0, r1) are in device memory (their chunks flagged)
 // and inside the N-free prefix, or until the whole segment is in.  Low word: 2 for "count it
-// with an all-zero N bitmap" (high word: the end of the chunks checked, in chunks), the
+// with an all-zero N bitmap" (high word: the byte where the checked chunks' N-free part ends, at
+// least r1), the
 // segment's verdict (0 / 1) once it is complete, ~0u to skip (timeout: error bit set).
 __device__ __forceinline__ uint64_t stage_gate(uint32_t* words, const uint32_t* chunk_gen, uint32_t chunks,
                                                          uint32_t replica, uint32_t gen, uint32_t r0, uint32_t r1,
@@ -518,7 +585,12 @@ __device__ __forceinline__ uint64_t stage_gate(uint32_t* words, const uint32_t* 
         const uint32_t dn = __builtin_amdgcn_readlane(v, 0), av = __builtin_amdgcn_readlane(v, 1);
         if (dn >= chunks) return wave_load(sw.verdict);
         const uint64_t miss = __ballot(lane >= 2u && lane - 2u < nx && v != gen);
-        if (in_prefix && miss == 0) return ((uint64_t)(x1 + 1u) << 32) | 2u;
+        if (in_prefix && miss == 0) {
+            // the chunks checked, up to where the N-free prefix ends: once the final header is out a
+            // flagged chunk may reach past it, and its bytes there can hold N
+            const uint32_t lim = av > pre ? av : pre, hi = (x1 + 1u) * AC_STAGE_CHUNK;
+            return ((uint64_t)(hi < lim ? hi : lim) << 32) | 2u;
+        }
         in_prefix = nx && (r1 <= pre || av >= r1);
         if (dn + av != seen) {
             seen = dn + av;
@@ -636,8 +708,9 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
     uint32_t* st_words = nullptr;
     if (STAGED && sg.stage_chunks) {  // (a segment sent ahead of a staged launch has no chunks)
         st_words = a.stage + AC_STAGE_L_SEG(si) * AC_QUEUE_LINE;
-        // the k-mer section fills whole chunks and is in the pinned block before the launch
-        const uint32_t pre_chunks = sg.stage_codes_off / AC_STAGE_CHUNK;
+        // the k-mer section fills whole chunks and is in the pinned block before the launch (an armed
+        // launch's: not yet, its k-mers wait for the progress records like the codes)
+        const uint32_t pre_bytes = a.arm_ticks ? 0u : sg.stage_codes_off, pre_chunks = pre_bytes / AC_STAGE_CHUNK;
         if (a.copier_wgs && blockIdx.x < a.copier_wgs) {
             // Copier workgroup of a large call: every wave serves every segment's tickets, starting
             // with segment (workgroup mod segments) -- the host packs a large call's jobs interleaved,
@@ -647,9 +720,9 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
                 const SegDev& c2 = a.seg[s2];
                 if (!c2.stage_chunks) continue;
                 if (!__builtin_amdgcn_readfirstlane((uint32_t)stage_copy(
-                        c2.stage_src, c2.stage_dst, c2.stage_chunks, c2.stage_codes_off / AC_STAGE_CHUNK,
+                        c2.stage_src, c2.stage_dst, c2.stage_chunks, a.arm_ticks ? 0u : c2.stage_codes_off / AC_STAGE_CHUNK,
                         a.host_hdr + s2 * AC_QUEUE_LINE, a.stage + AC_STAGE_L_SEG(s2) * AC_QUEUE_LINE, c2.stage_gen,
-                        a.gen, s2)))
+                        a.gen, s2, a.arm_ticks)))
                     if (lane == 0) atomicOr(a.err, AC_DEVERR_STAGE);
             }
         }
@@ -663,12 +736,12 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
                 !__builtin_amdgcn_readfirstlane(
                     (uint32_t)stage_copy(sg.stage_src, sg.stage_dst, sg.stage_chunks, pre_chunks,
                                          a.host_hdr + (uint32_t)si * AC_QUEUE_LINE, st_words, sg.stage_gen, a.gen,
-                                         (uint32_t)si))) {
+                                         (uint32_t)si, a.arm_ticks))) {
                 if (lane == 0) atomicOr(a.err, AC_DEVERR_STAGE);
             } else if (equal) {
                 // only the k-mers (the ~Eq table) are needed before counting starts
                 r = (uint32_t)stage_gate(st_words, sg.stage_gen, sg.stage_chunks, blockIdx.x % AC_STAGE_REPL, a.gen, 0u,
-                                         8u * sg.n_kmers, a.err, sg.stage_codes_off);
+                                         8u * sg.n_kmers, a.err, pre_bytes);
             } else {
                 r = stage_wait_all(st_words, sg.stage_chunks, blockIdx.x % AC_STAGE_REPL, a.err);
             }
@@ -868,7 +941,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
             const uint32_t r = __builtin_amdgcn_readfirstlane((uint32_t)g);
             if (r == 2u) {
                 v_lo = (r0 / AC_STAGE_CHUNK) * AC_STAGE_CHUNK;
-                v_hi = __builtin_amdgcn_readfirstlane((uint32_t)(g >> 32)) * AC_STAGE_CHUNK;
+                v_hi = __builtin_amdgcn_readfirstlane((uint32_t)(g >> 32));
                 return true;
             }
             return completed(r);

@@ -402,15 +402,21 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    # (back-to-back calls of one shape keep the next call's kernel enqueued -- the armed launch,
+    # DESIGN.md §4c; no call follows here, so it is cancelled before the device-wide sync)
+    counter.idle()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    arm0 = counter.arm_stats()
     t0 = time.perf_counter()
     marks = []
     for _ in range(args.steps):
         step()
         marks.append(time.perf_counter())
+    counter.idle()  # (the armed launch of a step K + 1 that never comes)
+    arm1 = counter.arm_stats()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -451,7 +457,8 @@ def main():
             "config": {"workload": workload_name, "k": args.k, "sn": args.sn, "sl": args.sl, "lim": args.lim,
                        "candidates": n_c, "kmer_bp_per_step": units_job, "kmer_bp_per_rank_step": units_rank,
                        "stage": ("Dna5 host buffers -> "
-                                 + ("1 fused count launch issued first, then both read ends packed (host pool, "
+                                 + ("1 fused count launch (enqueued during the previous step when the shape repeats "
+                                    "-- the armed launch -- else issued first), then both read ends packed (host pool, "
                                     "pinned; N positions inline in each window's slot) with progress records; 16 "
                                     "copier workgroups of the kernel pull each 4 KB chunk into HBM as it is packed "
                                     "while the others count a window as soon as its chunk is in" if stage_path == "early-launch"
@@ -472,6 +479,10 @@ def main():
             d = np.diff(np.array([t0] + marks)) * 1e3
             out["step_ms"] = {"min": float(d.min()), "p50": float(np.median(d)), "max": float(d.max())}
         out["stage_cold_call_ms"] = cold_ms
+        out["armed_launch"] = {"enqueued": arm1[0] - arm0[0], "taken_over": arm1[1] - arm0[1],
+                               "expired": arm1[2] - arm0[2], "cancelled": arm1[3] - arm0[3],
+                               "note": "timed steps: each step's count kernel enqueued by the step before it "
+                                       "(DESIGN.md 4c; ac_idle cancels the one left after the last step)"}
         out["host_pool"] = {"participants": pool_participants, "cpus": _ranges(pool_cpus),
                             "note": "rank 0's pack pool: GPU-local CPUs split among the local ranks, at most its "
                                     "share of the cgroup CPU quota (ac_host_pool_cpus)"}

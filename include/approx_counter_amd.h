@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define AC_ABI_VERSION 4
+#define AC_ABI_VERSION 5
 
 typedef int32_t ac_status;
 #define AC_OK 0
@@ -292,6 +292,22 @@ typedef struct ac_job {
  */
 #define AC_MAX_JOBS 4
 ac_status ac_error_count_jobs(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint32_t n_jobs);
+
+/*
+ * Armed launches (ABI 5): once two consecutive ac_error_count_jobs calls on ctx
+ * have the same shape (k, the jobs' candidate and window counts, window
+ * lengths), each such call also enqueues the NEXT call's count kernel behind
+ * its own, on the other staging slot.  Its waves start as soon as this call's
+ * kernel ends and wait for the next call's inputs, so that call pays no launch
+ * latency; a call of another shape, or any other entry point, cancels it
+ * first, and it gives up by itself after AC_ARM_US microseconds without a call
+ * (default 100; 0 disables arming).  While it waits it holds the device's
+ * compute units, so a caller that makes no further call soon -- and is about to
+ * synchronise the device or run other GPU work -- cancels it with ac_idle.
+ * The reference makes one errorCount call per read end per run
+ * (approx_counter.cpp:922); repeated calls are a serving loop's pattern.
+ */
+ac_status ac_idle(ac_ctx* ctx);
 
 /*
  * The same stage without the way back, for callers that combine shards with

@@ -27,7 +27,7 @@ def test_library_targets_gfx950():
 
 
 def test_abi_version():
-    assert _lib.load().ac_abi_version() == 4
+    assert _lib.load().ac_abi_version() == 5
 
 
 def test_pack_layout():

@@ -181,6 +181,29 @@ ab11)  # the first windows read from the host's pinned block before their chunk 
     run ab_host_$c 200 python3 bench.py --config $c --steps 20 --warmup 5 --no-cpu-baseline --no-pipelined --no-kernel-leg
     run ab_nohost_$c 200 env APPROX_COUNTER_AMD_LIB=build/var/nohost/libapprox_counter_amd.so python3 bench.py --config $c --steps 20 --warmup 5 --no-cpu-baseline --no-pipelined --no-kernel-leg
   done ;;
+ab12)  # the early-counting gate looking 62 chunks ahead vs 16 vs only the window's own chunks (kept: r04_m17)
+  B="python3 bench.py --steps 400 --warmup 20 --no-cpu-baseline --no-pipelined --no-kernel-leg"
+  for rep in 1 2 3; do
+    run ab_ahead62_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/ahead62/libapprox_counter_amd.so $B
+    run ab_ahead16_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/ahead16/libapprox_counter_amd.so $B
+    run ab_ahead1_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/ahead1/libapprox_counter_amd.so $B
+  done
+  for c in cfg5 cfg4; do
+    run ab_ahead62_$c 200 env APPROX_COUNTER_AMD_LIB=build/var/ahead62/libapprox_counter_amd.so python3 bench.py --config $c --steps 20 --warmup 5 --no-cpu-baseline --no-pipelined --no-kernel-leg
+    run ab_ahead1_$c 200 env APPROX_COUNTER_AMD_LIB=build/var/ahead1/libapprox_counter_amd.so python3 bench.py --config $c --steps 20 --warmup 5 --no-cpu-baseline --no-pipelined --no-kernel-leg
+  done ;;
+tests_arm)  # the armed-launch tests first (a hang shows here, not in the suite)
+  run tests_armed 400 $PYT -m gpu tests/test_gpu_armed.py ;;
+arm)  # armed launches (the default) vs none (AC_ARM_US=0): cfg2 stage 400 steps x3 interleaved; cfg3/5/4
+  B="python3 bench.py --steps 400 --warmup 20 --no-cpu-baseline --no-pipelined --no-kernel-leg"
+  for rep in 1 2 3; do
+    run ab_arm_$rep 120 $B
+    run ab_noarm_$rep 120 env AC_ARM_US=0 $B
+  done
+  for c in cfg3 cfg5 cfg4; do
+    run ab_arm_$c 200 python3 bench.py --config $c --steps 20 --warmup 5 $BQ --no-kernel-leg
+    run ab_noarm_$c 200 env AC_ARM_US=0 python3 bench.py --config $c --steps 20 --warmup 5 $BQ --no-kernel-leg
+  done ;;
 cfg2)
   for i in 1 2 3; do
     run cfg2_$i 200 env AC_STAGE_TRACE=1 python3 bench.py --steps 400 --warmup 10 $BQ
