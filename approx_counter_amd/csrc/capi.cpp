@@ -1724,10 +1724,21 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
     static const uint64_t min_task = (uint64_t)std::max(1, env_int("AC_TASK_WINDOWS", 1280));
     const uint64_t per = std::max<uint64_t>(
         min_task, std::min<uint64_t>(p.early ? std::max<uint64_t>(2048, min_task) : 65536, total_w / (4ull * pool.size()) + 1));
+    // An armed launch's waves are already waiting when the call starts: each job's first windows go
+    // out as a small head task of their own (AC_HEAD_WINDOWS, default 256: ~0.6 us of packing), so
+    // the first codes are published -- and the first windows counted -- that much sooner.  (A launch
+    // made by this call arrives after the first full task is packed anyway.)
+    static const uint64_t head = (uint64_t)std::max(0, env_int("AC_HEAD_WINDOWS", 256));
+    const uint64_t head_w = (p.early && ctx->arm.live && head && head < per) ? head : 0;
     std::vector<Task> tasks;
     for (uint32_t j = 0; j < p.n; ++j) {
         if (!jobs[j].n_kmers) continue;  // nothing to count: its windows are not needed
-        for (uint64_t w = p.lo[j]; w < p.hi[j]; w += per)
+        uint64_t w = p.lo[j];
+        if (head_w && p.hi[j] - w > head_w) {
+            tasks.push_back({j, (uint32_t)w, (uint32_t)(w + head_w), 0, 0, 0u, 0u});
+            w += head_w;
+        }
+        for (; w < p.hi[j]; w += per)
             tasks.push_back({j, (uint32_t)w, (uint32_t)std::min<uint64_t>(p.hi[j], w + per), 0, 0, 0u, 0u});
     }
     const std::function<void(uint32_t)> span_of = [&](uint32_t t) {
@@ -2140,7 +2151,9 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
                     if (!n_seen[j]) ready[j] = base_off + (x.bases + x.span) / 4;
                     ++nt[j];
                 }
-                if (ready[j] >= published[j] + PUBLISH_STEP || (nt[j] == nj && ready[j] > published[j])) {
+                // (the first codes at once, however few: the kernel may be waiting for them)
+                if (ready[j] >= published[j] + PUBLISH_STEP || (nt[j] == nj && ready[j] > published[j]) ||
+                    (published[j] == base_off && ready[j] > published[j])) {
                     // (test-only slow host: one step per record while its sleeps last)
                     const uint64_t r = slow_left ? std::min(ready[j], published[j] + PUBLISH_STEP) : ready[j];
                     publish(j, r);
@@ -2233,13 +2246,13 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
 // and publishing, while its kernel runs.  When this call's signature repeats the previous call's, the
 // NEXT call's staged kernel is enqueued now, behind this one on the stream: the other early-launch
 // slot, the next generation, the same layout, and LaunchArgs::arm_ticks set -- so it waits for the
-// k-mers' progress records too, and gives up after AC_ARM_US microseconds (default 100) without a
-// call.  The next call with the same signature takes it over (stage_and_launch: no launch, its
+// k-mers' progress records too, and gives up after AC_ARM_US microseconds without a call.  Opt-in
+// (AC_ARM_US > 0, e.g. 100): at cfg2 it measured no faster than launching in the call.  The next call with the same signature takes it over (stage_and_launch: no launch, its
 // waves already resident and polling); anything else cancels it (disarm).
 ac_status maybe_arm(ac_ctx* ctx, uint32_t k, const ac_job* jobs, const JobPlan& p, hipStream_t stream) {
     // 0: never armed; at most 0.1 s (below the staged waits' 0.5 s bound, which an armed launch's
     // waves waiting for their k-mers must not reach while it waits for the call)
-    static const int arm_us = std::min(env_int("AC_ARM_US", 100), 100000);
+    static const int arm_us = std::min(env_int("AC_ARM_US", 0), 100000);
     const bool repeat = ctx->last_sig_ok && ctx->last_sig == p.sig;
     ctx->last_sig = p.sig;
     ctx->last_sig_ok = true;
@@ -2433,8 +2446,14 @@ ac_status count_jobs_sync(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint32_t 
     }
     // the next call's armed launch, enqueued behind this call's kernel while it runs (DESIGN.md §4c;
     // not this call's business if it cannot be made: the next call then launches its own)
-    if (units.size() == 1 && units[0].plan.early && units[0].c == ctx)
+    if (units.size() == 1 && units[0].plan.early && units[0].c == ctx) {
+        const double ta = g_trace.on ? now_us() : 0.0;
         if (maybe_arm(ctx, k, jobs, units[0].plan, units[0].stream) != AC_OK) ctx->err.clear();
+        if (g_trace.on) {  // (AC_STAGE_TRACE: in "d2h_enq", which an early launch does not use)
+            g_trace.sum[5] += now_us() - ta;
+            g_trace.cur[5] += now_us() - ta;
+        }
+    }
     for (uint32_t j = 0; j < n_jobs; ++j)
         for (uint32_t i = 0; i < jobs[j].n_kmers; ++i) jobs[j].counts[i] = 0;
     ac_status first_err = AC_OK;

@@ -294,14 +294,15 @@ typedef struct ac_job {
 ac_status ac_error_count_jobs(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint32_t n_jobs);
 
 /*
- * Armed launches (ABI 5): once two consecutive ac_error_count_jobs calls on ctx
+ * Armed launches (ABI 5; opt-in: the environment variable AC_ARM_US > 0, read
+ * once per process): once two consecutive ac_error_count_jobs calls on ctx
  * have the same shape (k, the jobs' candidate and window counts, window
  * lengths), each such call also enqueues the NEXT call's count kernel behind
  * its own, on the other staging slot.  Its waves start as soon as this call's
  * kernel ends and wait for the next call's inputs, so that call pays no launch
  * latency; a call of another shape, or any other entry point, cancels it
  * first, and it gives up by itself after AC_ARM_US microseconds without a call
- * (default 100; 0 disables arming).  While it waits it holds the device's
+ * (at most 100000).  While it waits it holds the device's
  * compute units, so a caller that makes no further call soon -- and is about to
  * synchronise the device or run other GPU work -- cancels it with ac_idle.
  * The reference makes one errorCount call per read end per run

@@ -1,8 +1,10 @@
-"""Armed launches (ABI 5): a synchronous ac_error_count_jobs call whose shape repeats
-the previous call's enqueues the NEXT call's staged count kernel behind its own; the next call of
-that shape takes it over, anything else cancels it, and it gives up by itself after AC_ARM_US
-microseconds without a call.  Every path -- taken over, expired, cancelled, and the race between an
-expiry and a call -- must give the oracle's counts (errorCount, approx_counter.cpp:531-601)."""
+"""Armed launches (ABI 5; opt-in: AC_ARM_US > 0): a synchronous ac_error_count_jobs
+call whose shape repeats the previous call's enqueues the NEXT call's staged count kernel behind its
+own; the next call of that shape takes it over, anything else cancels it, and it gives up by itself
+after AC_ARM_US microseconds without a call.  Every path -- taken over, expired, cancelled, and the
+race between an expiry and a call -- must give the oracle's counts (errorCount,
+approx_counter.cpp:531-601).  Each test runs in a child process with AC_ARM_US set (read once per
+process)."""
 import os
 import subprocess
 import sys
@@ -43,7 +45,7 @@ def _check(got, exp, tag):
         assert np.array_equal(g, e), tag
 
 
-def test_armed_launch_taken_over_rotating_data():
+def armed_taken_over():
     """Back-to-back calls of one shape: from the third call on each call's kernel was enqueued by
     the call before (taken over), with the data of three workloads rotating through the two
     slots -- bit-exact every time, and the early-launch mode reported."""
@@ -59,7 +61,7 @@ def test_armed_launch_taken_over_rotating_data():
         assert c.arm_stats()[3] == cancelled + 1  # the last call's armed launch, cancelled
 
 
-def test_armed_launch_expires_then_call_runs_its_own():
+def armed_expires():
     """A call that comes after the armed launch gave up (AC_ARM_US, default 100 us) launches its
     own kernel: counted the same."""
     work = same_shape_workloads(n_work=2, nw=800, n_k=200, seed=90)
@@ -73,7 +75,7 @@ def test_armed_launch_expires_then_call_runs_its_own():
         assert expired >= 5 and taken == 0, c.arm_stats()
 
 
-def test_armed_launch_cancelled_by_other_shapes_and_entry_points():
+def armed_cancelled():
     """An armed launch is cancelled by a call of another shape, by any other entry point (device
     count, exact count, submit) and by ac_idle; every result stays exact and nothing waits on the
     cancelled kernel."""
@@ -114,6 +116,26 @@ def test_armed_launch_cancelled_by_other_shapes_and_entry_points():
         _check(c.count_jobs(16, work[1][0]), work[1][1], "after idle")
 
 
+def _child(code, us="100"):
+    env = dict(os.environ, AC_ARM_US=us, PYTHONPATH=ROOT)
+    r = subprocess.run([sys.executable, "-c", code + "; print('OK')"], env=env, capture_output=True, text=True,
+                       timeout=200, cwd=ROOT)
+    assert r.returncode == 0 and "OK" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])
+    return r.stdout
+
+
+def test_armed_launch_taken_over_rotating_data():
+    _child("from tests.test_gpu_armed import armed_taken_over; armed_taken_over()")
+
+
+def test_armed_launch_expires_then_call_runs_its_own():
+    _child("from tests.test_gpu_armed import armed_expires; armed_expires()")
+
+
+def test_armed_launch_cancelled_by_other_shapes_and_entry_points():
+    _child("from tests.test_gpu_armed import armed_cancelled; armed_cancelled()")
+
+
 def armed_race(calls=300):
     """Calls of one shape with the idle limit set so short (AC_ARM_US in the environment) that the
     armed kernel gives up while the call is publishing: the handshake decides, and either way the
@@ -130,23 +152,27 @@ def armed_race(calls=300):
 
 @pytest.mark.parametrize("us", ["2", "8", "30"])
 def test_armed_launch_expiry_race_is_exact(us):
-    """In a child process (AC_ARM_US is read once per process)."""
-    env = dict(os.environ, AC_ARM_US=us, PYTHONPATH=ROOT)
-    code = "from tests.test_gpu_armed import armed_race; armed_race(); print('OK')"
-    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=200, cwd=ROOT)
-    assert r.returncode == 0 and "OK" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])
-    stats = eval(r.stdout.split("STATS", 1)[1].splitlines()[0])
+    out = _child("from tests.test_gpu_armed import armed_race; armed_race()", us)
+    stats = eval(out.split("STATS", 1)[1].splitlines()[0])
     assert stats[0] >= 250 and stats[1] + stats[2] >= 250, stats
 
 
-def test_armed_launch_disabled_by_env():
-    env = dict(os.environ, AC_ARM_US="0", PYTHONPATH=ROOT)
-    code = ("from tests.test_gpu_armed import same_shape_workloads, _check\n"
-            "import approx_counter_amd as ac\n"
-            "w = same_shape_workloads(n_work=2, nw=300, n_k=64, seed=170)\n"
-            "c = ac.ApproxCounter(0)\n"
-            "for i in range(6): _check(c.count_jobs(16, w[i % 2][0]), w[i % 2][1], i)\n"
-            "print('STATS', c.arm_stats()); c.close(); print('OK')")
-    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=200, cwd=ROOT)
+def armed_off():
+    w = same_shape_workloads(n_work=2, nw=300, n_k=64, seed=170)
+    with ac.ApproxCounter(0) as c:
+        for i in range(6):
+            _check(c.count_jobs(16, w[i % 2][0]), w[i % 2][1], i)
+        print("STATS", c.arm_stats())
+
+
+@pytest.mark.parametrize("us", ["0", None])
+def test_armed_launch_off_by_default_and_with_zero(us):
+    """The default (no AC_ARM_US) and AC_ARM_US=0 never arm."""
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    env.pop("AC_ARM_US", None)
+    if us is not None:
+        env["AC_ARM_US"] = us
+    r = subprocess.run([sys.executable, "-c", "from tests.test_gpu_armed import armed_off; armed_off(); print('OK')"],
+                       env=env, capture_output=True, text=True, timeout=200, cwd=ROOT)
     assert r.returncode == 0 and "OK" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])
     assert "STATS (0, 0, 0, 0)" in r.stdout

@@ -194,15 +194,42 @@ ab12)  # the early-counting gate looking 62 chunks ahead vs 16 vs only the windo
   done ;;
 tests_arm)  # the armed-launch tests first (a hang shows here, not in the suite)
   run tests_armed 400 $PYT -m gpu tests/test_gpu_armed.py ;;
-arm)  # armed launches (the default) vs none (AC_ARM_US=0): cfg2 stage 400 steps x3 interleaved; cfg3/5/4
+arm)  # armed launches (AC_ARM_US=100; the default until r04_m21) vs none (AC_ARM_US=0): cfg2 stage 400 steps x3 interleaved; cfg3/5/4
   B="python3 bench.py --steps 400 --warmup 20 --no-cpu-baseline --no-pipelined --no-kernel-leg"
   for rep in 1 2 3; do
-    run ab_arm_$rep 120 $B
+    run ab_arm_$rep 120 env AC_ARM_US=100 $B
     run ab_noarm_$rep 120 env AC_ARM_US=0 $B
   done
   for c in cfg3 cfg5 cfg4; do
-    run ab_arm_$c 200 python3 bench.py --config $c --steps 20 --warmup 5 $BQ --no-kernel-leg
+    run ab_arm_$c 200 env AC_ARM_US=100 python3 bench.py --config $c --steps 20 --warmup 5 $BQ --no-kernel-leg
     run ab_noarm_$c 200 env AC_ARM_US=0 python3 bench.py --config $c --steps 20 --warmup 5 $BQ --no-kernel-leg
+  done ;;
+arm2)  # armed launches with a 256-window head task (default) / no head task / no arming, cfg2, x3
+  B="python3 bench.py --steps 400 --warmup 20 --no-cpu-baseline --no-pipelined --no-kernel-leg"
+  for rep in 1 2 3; do
+    run ab_head256_$rep 120 env AC_ARM_US=100 $B
+    run ab_head128_$rep 120 env AC_ARM_US=100 AC_HEAD_WINDOWS=128 $B
+    run ab_head0_$rep 120 env AC_ARM_US=100 AC_HEAD_WINDOWS=0 $B
+    run ab_noarm_$rep 120 env AC_ARM_US=0 $B
+  done ;;
+armstamps)  # in-kernel timelines from segment 0's first sight of the call: armed (the next kernel waiting
+           # through the read-back) vs not
+  S="env APPROX_COUNTER_AMD_LIB=build/var/stamps/libapprox_counter_amd.so"
+  run stamps_armed 120 $S AC_ARM_US=100000 python3 tools/stage_stamps.py --calls 40 --t0 progress
+  run stamps_noarm 120 $S AC_ARM_US=0 python3 tools/stage_stamps.py --calls 40 --t0 progress
+  run trace_arm 120 env AC_STAGE_TRACE=1 AC_ARM_US=100000 python3 bench.py --steps 400 --warmup 20 $BQ --no-kernel-leg ;;
+armprof)  # kernel traces of the cfg2 stage, armed and not (tools/kernel_gaps.py: duration, idle gap, period)
+  for m in arm noarm; do
+    a=$([ $m = noarm ] && echo 0 || echo 100)
+    ( cd /tmp && export TMPDIR=/tmp && AC_ARM_US=$a timeout -k 10 200 rocprofv3 --kernel-trace -d "$OUT/prof_$m" -o run -- \
+      python3 "$GRAFT_REPO_ROOT/bench.py" --steps 300 --warmup 20 --no-cpu-baseline --no-pipelined --no-kernel-leg ) \
+      > "$OUT/prof_$m.log" 2>&1 || { echo "prof $m failed"; exit 6; }
+    python3 tools/kernel_gaps.py "$(find "$OUT/prof_$m" -name '*.db' | head -1)" "wm2_count_kernel<2, true" | tee -a "$OUT/summary.log"
+  done ;;
+armtrace)  # host phases (AC_STAGE_TRACE) of the cfg2 stage with and without armed launches
+  for rep in 1 2; do
+    run trace_arm_$rep 120 env AC_STAGE_TRACE=1 AC_ARM_US=100 python3 bench.py --steps 400 --warmup 20 $BQ --no-kernel-leg
+    run trace_noarm_$rep 120 env AC_STAGE_TRACE=1 AC_ARM_US=0 python3 bench.py --steps 400 --warmup 20 $BQ --no-kernel-leg
   done ;;
 cfg2)
   for i in 1 2 3; do

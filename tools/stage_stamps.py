@@ -25,6 +25,9 @@ def main():
     ap.add_argument("--k", type=int, default=16)
     ap.add_argument("--lim", type=int, default=500)
     ap.add_argument("--calls", type=int, default=60)
+    ap.add_argument("--t0", choices=("entry", "progress"), default="entry",
+                    help="progress: time from segment 0's poller first seeing the call (armed launches: the next "
+                         "call's kernel overwrites the entry stamps while it waits, so read with a long AC_ARM_US)")
     a = ap.parse_args()
     import approx_counter_amd as ac
     from approx_counter_amd import _lib
@@ -47,7 +50,7 @@ def main():
         assert L.ac_debug_stamps(buf.ctypes.data, buf.nbytes) == 0
         raw = buf[: 8 * n].reshape(n, 8).astype(np.int64)
         stage = buf[8 * (1 << 18):].astype(np.int64)
-        t0 = raw[:, 0].min()
+        t0 = raw[:, 0].min() if a.t0 == "entry" else int(stage[1])
         us = (raw[:, :4] - t0) / 100.0
         seg = raw[:, 6] >> 32
         print(f"call {call}: mode {c.stage_mode()} waves={n} kernel span {us[:, 3].max():.1f} us")
