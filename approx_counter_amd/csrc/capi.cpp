@@ -715,6 +715,7 @@ void ac_destroy(ac_ctx* ctx) {
         disarm(ctx);
         (void)hipSetDevice(ctx->device);
         (void)hipStreamSynchronize(ctx->stream);
+        if (ctx->part_stream[1]) (void)hipStreamSynchronize(ctx->part_stream[1]);  // (slot 1's, slot_stream)
     }
     if (ctx->warm.joinable()) ctx->warm.join();
     for (ac_ctx* p : ctx->peers) ac_destroy(p);
@@ -1851,8 +1852,7 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
         LaunchSig& g = p.sig;
         g = LaunchSig();
         for (uint64_t v : {(uint64_t)k, (uint64_t)p.n, (uint64_t)p.tag, (uint64_t)p.pre, (uint64_t)p.copiers,
-                           (uint64_t)p.scratch, (uint64_t)p.off_err, (uint64_t)p.off_gerr, (uint64_t)p.n_gerr,
-                           (uint64_t)p.total})
+                           (uint64_t)p.off_err, (uint64_t)p.off_gerr, (uint64_t)p.n_gerr, (uint64_t)p.total})
             g.add(v);
         for (uint32_t j = 0; j < p.n; ++j)
             for (uint64_t v : {(uint64_t)jobs[j].n_kmers, (uint64_t)p.lo[j], (uint64_t)p.hi[j], p.n_bases[j],
@@ -2242,6 +2242,24 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
     return AC_OK;
 }
 
+// Early-launch slot s runs on its own stream with its own count-kernel scratch set (slot 0: the
+// context's stream and set 0, slot 1: part stream 1 and set 1), so a call's kernel can start while
+// the previous call's kernel -- whose counts are already back -- still drains its last waves and
+// retires: consecutive calls overlap on the device by that tail instead of queueing behind it.  (The
+// DMA path's part 1 uses the same stream and set, stream-ordered behind any early call of slot 1.)
+// Opt-in, AC_SLOT_STREAMS=1: built at the end of round 4 and not yet measured on the GPU (DESIGN.md
+// §8); by default both slots run on the context's stream with scratch set 0, as measured.
+ac_status slot_stream(ac_ctx* ctx, int slot, hipStream_t* stream, int* scratch) {
+    static const bool own = env_int("AC_SLOT_STREAMS", 0) != 0;
+    *stream = ctx->stream;
+    *scratch = 0;
+    if (!own || slot == 0) return AC_OK;
+    if (!ctx->part_stream[1]) AC_HIP(ctx, hipStreamCreateWithFlags(&ctx->part_stream[1], hipStreamNonBlocking));
+    *stream = ctx->part_stream[1];
+    *scratch = 1;
+    return AC_OK;
+}
+
 // Armed launch: called by a synchronous early-launch call right after its own launch
 // and publishing, while its kernel runs.  When this call's signature repeats the previous call's, the
 // NEXT call's staged kernel is enqueued now, behind this one on the stream: the other early-launch
@@ -2249,7 +2267,7 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
 // k-mers' progress records too, and gives up after AC_ARM_US microseconds without a call.  Opt-in
 // (AC_ARM_US > 0, e.g. 100): at cfg2 it measured no faster than launching in the call.  The next call with the same signature takes it over (stage_and_launch: no launch, its
 // waves already resident and polling); anything else cancels it (disarm).
-ac_status maybe_arm(ac_ctx* ctx, uint32_t k, const ac_job* jobs, const JobPlan& p, hipStream_t stream) {
+ac_status maybe_arm(ac_ctx* ctx, uint32_t k, const ac_job* jobs, const JobPlan& p) {
     // 0: never armed; at most 0.1 s (below the staged waits' 0.5 s bound, which an armed launch's
     // waves waiting for their k-mers must not reach while it waits for the call)
     static const int arm_us = std::min(env_int("AC_ARM_US", 0), 100000);
@@ -2258,6 +2276,9 @@ ac_status maybe_arm(ac_ctx* ctx, uint32_t k, const ac_job* jobs, const JobPlan& 
     ctx->last_sig_ok = true;
     if (arm_us <= 0 || !repeat || !p.tag || p.pre != 0 || !ctx->peers.empty() || ctx->arm.live) return AC_OK;
     const int s2 = p.slot ^ 1;  // the next early-launch call's slot (ctx->early_flip)
+    hipStream_t stream = nullptr;
+    int scratch = 0;
+    if (ac_status st = slot_stream(ctx, s2, &stream, &scratch)) return st;
     ac_ctx::Slot& sl = ctx->slot[s2];
     if (sl.pending) {  // the call before this one (its kernel ran before this call's)
         AC_HIP(ctx, hipEventSynchronize(sl.ev));
@@ -2309,7 +2330,10 @@ ac_status maybe_arm(ac_ctx* ctx, uint32_t k, const ac_job* jobs, const JobPlan& 
                               p.n_bases[j]};
         g.counts = (uint32_t*)(hd + p.off_counts[j]);
     }
-    if (ac_status st = launch(ctx, k, segs, p.n, stream, true, nullptr, p.scratch, 0, no_n, p.ulen, &stg, p.nrec))
+    // behind this call's kernel, as on one stream (slot_stream: the slots' own streams), so its idle
+    // clock starts when this kernel is done
+    AC_HIP(ctx, hipStreamWaitEvent(stream, ctx->slot[p.slot].ev, 0));
+    if (ac_status st = launch(ctx, k, segs, p.n, stream, true, nullptr, scratch, 0, no_n, p.ulen, &stg, p.nrec))
         return st;
     AC_HIP(ctx, hipEventRecord(sl.ev, stream));
     sl.pending = true;
@@ -2428,6 +2452,7 @@ ac_status count_jobs_sync(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint32_t 
                 u.plan.early = true;
                 u.plan.slot = (int)ctx->early_flip;
                 ctx->early_flip ^= 1u;
+                if (ac_status st = slot_stream(ctx, u.plan.slot, &u.stream, &u.plan.scratch)) return st;
             }
             for (uint32_t j = 0; j < n_jobs; ++j) {
                 u.plan.lo[j] = cuts[j][q];
@@ -2448,7 +2473,7 @@ ac_status count_jobs_sync(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint32_t 
     // not this call's business if it cannot be made: the next call then launches its own)
     if (units.size() == 1 && units[0].plan.early && units[0].c == ctx) {
         const double ta = g_trace.on ? now_us() : 0.0;
-        if (maybe_arm(ctx, k, jobs, units[0].plan, units[0].stream) != AC_OK) ctx->err.clear();
+        if (maybe_arm(ctx, k, jobs, units[0].plan) != AC_OK) ctx->err.clear();
         if (g_trace.on) {  // (AC_STAGE_TRACE: in "d2h_enq", which an early launch does not use)
             g_trace.sum[5] += now_us() - ta;
             g_trace.cur[5] += now_us() - ta;
