@@ -69,6 +69,17 @@ def test_comm_entry_points_without_a_context():
     assert L.ac_allreduce_counts(None, None, 0, None) == _lib.AC_ERR_INVALID
 
 
+def test_arm_entry_points_without_a_context():
+    """ac_idle (ABI 5) rejects a NULL context; the test-only arm statistics report -1 for it."""
+    import ctypes
+
+    L = _lib.load()
+    assert L.ac_idle(None) == _lib.AC_ERR_INVALID
+    assert b"ctx" in L.ac_last_error(None)
+    buf = (ctypes.c_uint64 * 4)()
+    assert L.ac_testing_arm_stats(None, buf) == -1
+
+
 def _has_gpu():
     try:
         import torch
