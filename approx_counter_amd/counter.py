@@ -289,17 +289,10 @@ class ApproxCounter:
         return int(self._L.ac_exact_path(self._h))
 
     def idle(self) -> None:
-        """ac_idle: cancel the armed launch, if any (the next jobs call's kernel, enqueued by a repeated
-        call of one shape and waiting for it) -- before device-wide synchronisation or other GPU work."""
+        """ac_idle (ABI >= 5): since ABI 6 no call leaves device work behind it, so this only checks
+        the context (kept for callers written against ABI 5's armed launches)."""
         if hasattr(self._L, "ac_idle"):
             check(self._L.ac_idle(self._h), self._h)
-
-    def arm_stats(self) -> tuple:
-        """ac_testing_arm_stats: armed launches (enqueued, taken over, expired, cancelled)."""
-        buf = (ctypes.c_uint64 * 4)()
-        if not hasattr(self._L, "ac_testing_arm_stats") or self._L.ac_testing_arm_stats(self._h, buf) != 0:
-            return (0, 0, 0, 0)
-        return tuple(int(x) for x in buf)
 
     def stage_mode(self) -> int:
         """ac_stage_mode: the last jobs call's stage -- 2 early launch (the count kernel copies each

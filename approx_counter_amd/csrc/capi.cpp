@@ -34,17 +34,6 @@ static_assert(AC_MAX_JOBS <= AC_MAX_SEGS, "every job of ac_error_count_jobs is o
 // packing and DMA overlap the previous part's kernel.
 #define AC_STAGE_MAX_PARTS 4
 
-// What an early launch's kernel arguments depend on besides the data (k, the jobs' window ranges and
-// candidate counts, the slot layout, equal-window / record decisions, chunks, copier count): two
-// calls with one signature launch the same kernel on the same slot layout, so the next call's launch
-// can be enqueued before the call (the armed launch).
-struct LaunchSig {
-    uint64_t w[96] = {};
-    uint32_t n = 0;
-    void add(uint64_t v) { w[n < 96 ? n++ : 95] = v; }
-    bool operator==(const LaunchSig& o) const { return n == o.n && n < 96 && std::memcmp(w, o.w, sizeof(uint64_t) * n) == 0; }
-};
-
 struct ac_ctx {
     int device = 0;
     int cu_count = 256;
@@ -133,19 +122,6 @@ struct ac_ctx {
     uint32_t early_flip = 0;         // early-launch calls alternate between staging slots 0 and 1
     int exact_path = -1;             // the last exact count's path: 1 partitioned, 0 hash table
     int last_mode = -1;  // ac_stage_mode: 2 the last jobs call was an early launch, 0 the DMA path
-    // Armed launch: a synchronous early-launch call whose signature repeats the
-    // previous call's enqueues the NEXT call's staged kernel (other slot, next generation) while it
-    // waits for its own, so the next call finds its kernel's waves resident and polling.  A call
-    // with that signature takes it over; anything else cancels it first (disarm).
-    struct Arm {
-        bool live = false;
-        int slot = 0;
-        uint32_t gen = 0, n = 0;
-        LaunchSig sig;
-    } arm;
-    LaunchSig last_sig;  // the last synchronous early-launch call's
-    bool last_sig_ok = false;
-    uint64_t arm_stats[4] = {0, 0, 0, 0};  // armed launches: enqueued, taken over, expired, cancelled
     // Warm-up started by ac_create on a thread of its own (ensure_warm joins it before the first count
     // launch): the count kernels' code object is loaded by the occupancy queries, so the first launch
     // -- the CLI's one approximate count per run -- does not pay for it; it overlaps the caller's FASTA
@@ -157,7 +133,6 @@ struct ac_ctx {
 namespace {
 
 thread_local std::string g_err;
-void disarm(ac_ctx* ctx);
 
 ac_status fail(ac_ctx* ctx, ac_status st, const std::string& msg) {
     if (ctx) ctx->err = msg;
@@ -318,7 +293,6 @@ struct StageLaunch {
     uint32_t tag = 0;              // tagged completion (wm_count.h LaunchArgs::tag)
     uint64_t* grp_err = nullptr;   // its per-group error words (device-visible pinned address)
     uint32_t copiers = 0;          // copier workgroups (wm_count.h LaunchArgs::copier_wgs; 0: every workgroup)
-    uint32_t arm_ticks = 0;        // an armed launch's idle limit (wm_count.h LaunchArgs::arm_ticks; 0: not armed)
 };
 
 // Who stages a staged launch (wm_count.h LaunchArgs::copier_wgs): a few copier workgroups stage
@@ -528,7 +502,6 @@ ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hi
         a.grp_err = stage->grp_err;
         const uint64_t blocks = (wave + AC_WAVES_PER_BLOCK - 1) / AC_WAVES_PER_BLOCK;
         a.copier_wgs = (uint32_t)std::min<uint64_t>(blocks, stage->copiers);
-        a.arm_ticks = stage->arm_ticks;
     }
     // the equal-window instantiation when every live segment has equal windows (their fit in the
     // image checked above)
@@ -711,12 +684,6 @@ ac_status ac_create(ac_ctx** out, int device) {
 
 void ac_destroy(ac_ctx* ctx) {
     if (!ctx) return;
-    if (ctx->arm.live) {  // cancelled, and finished before its buffers go
-        disarm(ctx);
-        (void)hipSetDevice(ctx->device);
-        (void)hipStreamSynchronize(ctx->stream);
-        if (ctx->part_stream[1]) (void)hipStreamSynchronize(ctx->part_stream[1]);  // (slot 1's, slot_stream)
-    }
     if (ctx->warm.joinable()) ctx->warm.join();
     for (ac_ctx* p : ctx->peers) ac_destroy(p);
     (void)hipSetDevice(ctx->device);
@@ -757,7 +724,6 @@ void ac_destroy(ac_ctx* ctx) {
 
 ac_status ac_error_count_device(ac_ctx* ctx, uint32_t k, const ac_segment* segments, uint32_t n_segments,
                                 void* hip_stream) {
-    disarm(ctx);  // (an armed launch waits for the next jobs call only)
     if (!ctx) return fail(nullptr, AC_ERR_INVALID, "ctx is NULL");
     AC_HIP(ctx, hipSetDevice(ctx->device));
     return launch(ctx, k, segments, n_segments, (hipStream_t)hip_stream, true);
@@ -765,7 +731,6 @@ ac_status ac_error_count_device(ac_ctx* ctx, uint32_t k, const ac_segment* segme
 
 ac_status ac_error_count_device_accumulate(ac_ctx* ctx, uint32_t k, const ac_segment* segments,
                                            uint32_t n_segments, void* hip_stream) {
-    disarm(ctx);  // (an armed launch waits for the next jobs call only)
     if (!ctx) return fail(nullptr, AC_ERR_INVALID, "ctx is NULL");
     AC_HIP(ctx, hipSetDevice(ctx->device));
     return launch(ctx, k, segments, n_segments, (hipStream_t)hip_stream, false);
@@ -773,7 +738,6 @@ ac_status ac_error_count_device_accumulate(ac_ctx* ctx, uint32_t k, const ac_seg
 
 ac_status ac_error_count_device_equal(ac_ctx* ctx, uint32_t k, const ac_segment* segments,
                                       const uint32_t* window_len, uint32_t n_segments, void* hip_stream) {
-    disarm(ctx);  // (an armed launch waits for the next jobs call only)
     if (!ctx) return fail(nullptr, AC_ERR_INVALID, "ctx is NULL");
     if (n_segments && !window_len) return fail(ctx, AC_ERR_INVALID, "window_len is NULL");
     if (n_segments > AC_MAX_SEGS) return fail(ctx, AC_ERR_INVALID, "too many segments in one launch (max 4)");
@@ -942,7 +906,6 @@ extern "C" {
 
 ac_status ac_error_count(ac_ctx* ctx, uint32_t k, const uint64_t* kmers, uint32_t n_kmers,
                          const ac_windows* sample, uint64_t* counts) {
-    disarm(ctx);  // (an armed launch waits for the next jobs call only)
     if (!ctx) return fail(nullptr, AC_ERR_INVALID, "ctx is NULL");
     if (ac_status st = check_k(ctx, k)) return st;
     if (n_kmers == 0) return AC_OK;
@@ -952,7 +915,6 @@ ac_status ac_error_count(ac_ctx* ctx, uint32_t k, const uint64_t* kmers, uint32_
 }
 
 ac_status ac_error_count_images(ac_ctx* ctx, uint32_t k, const ac_sample_job* jobs, uint32_t n_jobs) {
-    disarm(ctx);  // (an armed launch waits for the next jobs call only)
     if (n_jobs && !jobs) return fail(ctx, AC_ERR_INVALID, "jobs is NULL");
     return count_images(ctx, k, jobs, n_jobs);
 }
@@ -980,7 +942,6 @@ ac_status ac_create_multi(ac_ctx** out, int n_gpus) {
 ac_status ac_count(ac_ctx* ctx, uint32_t k, const uint64_t* kmers, uint32_t n_kmers, const uint32_t* win_bits,
                    const uint32_t* win_nmask, const uint64_t* win_word_offset, const uint16_t* win_len,
                    uint32_t n_windows, uint64_t* counts_out) {
-    disarm(ctx);  // (an armed launch waits for the next jobs call only)
     if (!ctx) return fail(nullptr, AC_ERR_INVALID, "ctx is NULL");
     if (n_windows && (!win_bits || !win_nmask || !win_word_offset || !win_len))
         return fail(ctx, AC_ERR_INVALID, "NULL window array");
@@ -999,7 +960,6 @@ ac_status ac_count(ac_ctx* ctx, uint32_t k, const uint64_t* kmers, uint32_t n_km
 }
 
 ac_status ac_sample_upload_slot(ac_ctx* ctx, int slot, const ac_windows* host, ac_windows* dev) {
-    disarm(ctx);  // (an armed launch waits for the next jobs call only)
     if (!ctx || !dev) return fail(ctx, AC_ERR_INVALID, "ctx or dev is NULL");
     if (slot < 0 || slot >= AC_MAX_JOBS) return fail(ctx, AC_ERR_INVALID, "upload slot outside [0, AC_MAX_JOBS)");
     if (ac_status st = check_sample(ctx, host)) return st;
@@ -1049,7 +1009,6 @@ ac_status ac_sample_upload_slot(ac_ctx* ctx, int slot, const ac_windows* host, a
 }
 
 ac_status ac_sample_upload(ac_ctx* ctx, const ac_windows* host, ac_windows* dev) {
-    disarm(ctx);  // (an armed launch waits for the next jobs call only)
     return ac_sample_upload_slot(ctx, 0, host, dev);
 }
 
@@ -1057,7 +1016,6 @@ ac_status ac_exact_count_device(ac_ctx* ctx, uint32_t k, const ac_windows* dev, 
                                 const uint64_t* forbidden, uint32_t n_forbidden, uint64_t limit, uint64_t solid,
                                 uint64_t* kmers_out, uint64_t* counts_out, uint64_t capacity, uint64_t* n_out,
                                 uint64_t* n_distinct, uint64_t* had_n) {
-    disarm(ctx);  // (an armed launch waits for the next jobs call only)
     if (!ctx) return fail(nullptr, AC_ERR_INVALID, "ctx is NULL");
     if (ac_status st = check_k(ctx, k)) return st;
     if (ac_status st = check_sample(ctx, dev)) return st;
@@ -1273,7 +1231,6 @@ ac_status ac_exact_count(ac_ctx* ctx, uint32_t k, const ac_windows* host, float 
                          const uint64_t* forbidden, uint32_t n_forbidden, uint64_t limit, uint64_t solid,
                          uint64_t* kmers_out, uint64_t* counts_out, uint64_t capacity, uint64_t* n_out,
                          uint64_t* n_distinct, uint64_t* had_n) {
-    disarm(ctx);  // (an armed launch waits for the next jobs call only)
     if (!ctx) return fail(nullptr, AC_ERR_INVALID, "ctx is NULL");
     if (ac_status st = check_k(ctx, k)) return st;
     ac_windows dev;
@@ -1283,7 +1240,6 @@ ac_status ac_exact_count(ac_ctx* ctx, uint32_t k, const ac_windows* host, float 
 }
 
 ac_status ac_error_count_samples(ac_ctx* ctx, uint32_t k, const ac_sample_job* jobs, uint32_t n_jobs) {
-    disarm(ctx);  // (an armed launch waits for the next jobs call only)
     if (!ctx) return fail(nullptr, AC_ERR_INVALID, "ctx is NULL");
     if (ac_status st = check_k(ctx, k)) return st;
     if (n_jobs > AC_MAX_JOBS) return fail(ctx, AC_ERR_INVALID, "too many jobs in one call (max 4)");
@@ -1347,7 +1303,6 @@ ac_status ac_error_count_samples(ac_ctx* ctx, uint32_t k, const ac_sample_job* j
 
 ac_status ac_error_count_sample(ac_ctx* ctx, uint32_t k, const uint64_t* kmers, uint32_t n_kmers,
                                 const ac_windows* dev, uint64_t* counts) {
-    disarm(ctx);  // (an armed launch waits for the next jobs call only)
     if (!ctx) return fail(nullptr, AC_ERR_INVALID, "ctx is NULL");
     if (!dev) return fail(ctx, AC_ERR_INVALID, "NULL argument");
     const ac_sample_job job{kmers, n_kmers, *dev, counts};
@@ -1386,7 +1341,6 @@ ac_status ac_pack_windows(const uint8_t* dna5, const uint64_t* seq_start, const 
 }
 
 ac_status ac_check(ac_ctx* ctx, void* hip_stream) {
-    disarm(ctx);  // (an armed launch waits for the next jobs call only)
     if (!ctx) return fail(nullptr, AC_ERR_INVALID, "ctx is NULL");
     AC_HIP(ctx, hipSetDevice(ctx->device));
     hipStream_t st = (hipStream_t)hip_stream;
@@ -1414,7 +1368,6 @@ ac_status ac_comm_unique_id(ac_ctx* ctx, void* id_out) {
 }
 
 ac_status ac_comm_init(ac_ctx* ctx, int n_ranks, int rank, const void* id) {
-    disarm(ctx);  // (an armed launch waits for the next jobs call only)
     if (!ctx || !id) return fail(ctx, AC_ERR_INVALID, "ctx or id is NULL");
     if (n_ranks < 1 || rank < 0 || rank >= n_ranks) return fail(ctx, AC_ERR_INVALID, "rank outside [0, n_ranks)");
     if (!ctx->peers.empty()) return fail(ctx, AC_ERR_INVALID, "ac_comm_init needs a single-device context");
@@ -1432,7 +1385,6 @@ ac_status ac_comm_init(ac_ctx* ctx, int n_ranks, int rank, const void* id) {
 }
 
 ac_status ac_allreduce_counts(ac_ctx* ctx, uint32_t* d_counts, uint64_t n, void* hip_stream) {
-    disarm(ctx);  // (an armed launch waits for the next jobs call only)
     if (!ctx) return fail(ctx, AC_ERR_INVALID, "ctx is NULL");
     if (!ctx->comm) return fail(ctx, AC_ERR_INVALID, "no communicator: call ac_comm_init first");
     if (n == 0) return AC_OK;
@@ -1539,11 +1491,10 @@ struct JobPlan {
     uint32_t gen = 0;    // its generation (the header flags and the tagged counts carry it)
     int slot = 0;     // staging slot (set by the caller: a synchronous part q uses slot q, a submit part its set's)
     int scratch = 0;  // count-kernel scratch set (ac_ctx::sc)
-    // early launch: what the launch was made of (the armed launch of the next call repeats it)
+    // early launch: what the launch is made of
     uint32_t ulen[AC_MAX_JOBS] = {}, chunks[AC_MAX_JOBS] = {}, codes_off[AC_MAX_JOBS] = {};
     bool nrec[AC_MAX_JOBS] = {};
     uint32_t pre = 0, copiers = 0;
-    LaunchSig sig;
 };
 
 // Calls whose pack and DMA take hundreds of
@@ -1616,21 +1567,6 @@ int stage_early() {
 // runs out (the synchronous call then retries through the DMA path); AC_TESTING_ALL_AHEAD sends every
 // job ahead of the staged launch (the staged kernel on resident input, a diagnostic of its own cost).
 std::atomic<uint32_t> g_test_hooks{0};
-
-// Cancels the armed launch, if there is one: every segment of it flagged with an
-// abort, so its waves skip and finish; the slot's event, recorded after it, says when.  Every entry
-// point that is not the call the armed launch waits for runs this first.
-void disarm(ac_ctx* ctx) {
-    if (!ctx || !ctx->arm.live) return;
-    ctx->arm.live = false;
-    ++ctx->arm_stats[3];
-    uint32_t* hdr = ctx->slot[ctx->arm.slot].hdr;
-    for (uint32_t j = 0; j < ctx->arm.n; ++j) {
-        uint32_t* line = hdr + j * AC_QUEUE_LINE;
-        line[AC_HDR_INFO] = AC_HDR_INFO_ABORT;
-        __atomic_store_n(&line[AC_HDR_FLAG], ctx->arm.gen, __ATOMIC_RELEASE);
-    }
-}
 
 // Some job has candidates and windows (a launch with work, so tagged counts to wait for).
 bool live_work(const ac_job* jobs, uint32_t n_jobs) {
@@ -1725,21 +1661,10 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
     static const uint64_t min_task = (uint64_t)std::max(1, env_int("AC_TASK_WINDOWS", 1280));
     const uint64_t per = std::max<uint64_t>(
         min_task, std::min<uint64_t>(p.early ? std::max<uint64_t>(2048, min_task) : 65536, total_w / (4ull * pool.size()) + 1));
-    // An armed launch's waves are already waiting when the call starts: each job's first windows go
-    // out as a small head task of their own (AC_HEAD_WINDOWS, default 256: ~0.6 us of packing), so
-    // the first codes are published -- and the first windows counted -- that much sooner.  (A launch
-    // made by this call arrives after the first full task is packed anyway.)
-    static const uint64_t head = (uint64_t)std::max(0, env_int("AC_HEAD_WINDOWS", 256));
-    const uint64_t head_w = (p.early && ctx->arm.live && head && head < per) ? head : 0;
     std::vector<Task> tasks;
     for (uint32_t j = 0; j < p.n; ++j) {
         if (!jobs[j].n_kmers) continue;  // nothing to count: its windows are not needed
-        uint64_t w = p.lo[j];
-        if (head_w && p.hi[j] - w > head_w) {
-            tasks.push_back({j, (uint32_t)w, (uint32_t)(w + head_w), 0, 0, 0u, 0u});
-            w += head_w;
-        }
-        for (; w < p.hi[j]; w += per)
+        for (uint64_t w = p.lo[j]; w < p.hi[j]; w += per)
             tasks.push_back({j, (uint32_t)w, (uint32_t)std::min<uint64_t>(p.hi[j], w + per), 0, 0, 0u, 0u});
     }
     const std::function<void(uint32_t)> span_of = [&](uint32_t t) {
@@ -1829,11 +1754,8 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
         nrec[j] = ulen[j] != AC_NO_ULEN && acamd::nrec_bits(ulen[j]) != 0u;
     }
     // Early launch: what the launch is made of -- the first `pre` jobs sent ahead of it (AC_STAGE_EARLY=2:
-    // the first; a test hook: all), each job's region and chunks, the copier workgroups -- and its
-    // signature; the armed launch enqueued during the previous call is this call's
-    // when the signatures match, and is cancelled otherwise.
+    // the first; a test hook: all), each job's region and chunks, the copier workgroups.
     size_t region[AC_MAX_JOBS] = {};
-    bool use_arm = false;
     if (p.early) {
         const uint32_t hooks = g_test_hooks.load(std::memory_order_relaxed);
         p.pre = (hooks & AC_TESTING_ALL_AHEAD) ? p.n : (stage_early() == 2 && p.n > 1) ? 1u : 0u;
@@ -1849,28 +1771,10 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
         uint64_t tickets = 0;
         for (uint32_t j = 0; j < p.n; ++j) tickets += p.chunks[j] ? p.chunks[j] + 1u : 0u;
         p.copiers = stage_copiers(tickets, ctx->resident[P]);
-        LaunchSig& g = p.sig;
-        g = LaunchSig();
-        for (uint64_t v : {(uint64_t)k, (uint64_t)p.n, (uint64_t)p.tag, (uint64_t)p.pre, (uint64_t)p.copiers,
-                           (uint64_t)p.off_err, (uint64_t)p.off_gerr, (uint64_t)p.n_gerr, (uint64_t)p.total})
-            g.add(v);
-        for (uint32_t j = 0; j < p.n; ++j)
-            for (uint64_t v : {(uint64_t)jobs[j].n_kmers, (uint64_t)p.lo[j], (uint64_t)p.hi[j], p.n_bases[j],
-                               (uint64_t)ulen[j], (uint64_t)nrec[j], (uint64_t)p.chunks[j], (uint64_t)p.codes_off[j],
-                               (uint64_t)p.off_kmers[j], (uint64_t)p.off_codes[j], (uint64_t)p.off_nmask[j],
-                               (uint64_t)p.off_start[j], (uint64_t)p.off_len[j], (uint64_t)p.off_counts[j]})
-                g.add(v);
-        if (ctx->arm.live) {
-            use_arm = p.tag && p.pre == 0 && ctx->arm.slot == p.slot && ctx->arm.sig == p.sig;
-            if (!use_arm) disarm(ctx);
-        }
-    } else {
-        disarm(ctx);
     }
-    // The slot: wait until the launch that last read it has finished, grow it.  (Taken over from an
-    // armed launch: that launch is the slot's pending work, and it waits for this call.)
+    // The slot: wait until the launch that last read it has finished, grow it.
     ac_ctx::Slot& sl = ctx->slot[p.slot];
-    if (sl.pending && !use_arm) {
+    if (sl.pending) {
         AC_HIP(ctx, hipEventSynchronize(sl.ev));
         sl.pending = false;
     }
@@ -1896,8 +1800,8 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
     }
     *(uint32_t*)(h + p.off_err) = 0u;
     // tagged completion: no count or error word may carry this call's generation before the kernel
-    // writes it (the slot last held other data; an armed launch's slot was cleared when it was armed)
-    if (p.tag && !use_arm) std::memset(h + p.off_counts[0], 0, p.total - p.off_counts[0]);
+    // writes it (the slot last held other data)
+    if (p.tag) std::memset(h + p.off_counts[0], 0, p.total - p.off_counts[0]);
     // early launch: flags cleared before the launch (the slot's last
     // launch has finished: its event was waited for above)
     const size_t hdr_bytes = sizeof(uint32_t) * AC_QUEUE_LINE * AC_HDR_LINES;
@@ -1906,7 +1810,7 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
         AC_HIP(ctx, hipHostGetDevicePointer((void**)&sl.hdr_d, sl.hdr, 0));
     }
     uint32_t* hdr = sl.hdr;
-    if (p.early && !use_arm) std::memset(hdr, 0, hdr_bytes);
+    if (p.early) std::memset(hdr, 0, hdr_bytes);
     mark(1);
     // per task: does the job need its N bitmap for these windows (an N, or with records an
     // overflowed record)
@@ -1961,12 +1865,8 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
         // 0.144 vs 0.134 ms per cfg2 step -- each end's last chunk waits for its final header,
         // which then came ~27 us into the kernel for both; profiles/r03_stage/r03_early12_step3.log.)
         StageLaunch stg;
-        if (use_arm) {
-            p.gen = stg.gen = ctx->arm.gen;  // the armed launch's generation
-        } else {
-            if (++ctx->gen == 0) ++ctx->gen;
-            p.gen = stg.gen = ctx->gen;
-        }
+        if (++ctx->gen == 0) ++ctx->gen;
+        p.gen = stg.gen = ctx->gen;
         stg.host_hdr = sl.hdr_d;
         stg.err_out = d_counts ? ctx->d_err : nullptr;  // a submit reports through ac_check
         stg.tag = p.tag ? 1u : 0u;
@@ -2036,39 +1936,9 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
         };
         // the k-mers are in place already (copied with the layout)
         for (uint32_t j = 0; j < p.n; ++j) publish(j, p.off_codes[j] - p.off_kmers[j]);
-        if (use_arm) {
-            // The armed launch's handshake (wm_count.hip stage_arm_wait): the first records are out;
-            // if its poller has begun to give up, its outcome is waited for.
-            std::atomic_thread_fence(std::memory_order_seq_cst);
-            const uint64_t* aw = (const uint64_t*)(hdr + AC_HDR_ARM);
-            uint64_t e = __atomic_load_n(aw, __ATOMIC_ACQUIRE);
-            const auto t_arm = std::chrono::steady_clock::now();
-            while ((uint32_t)e == p.gen && (uint32_t)(e >> 32) == AC_ARM_EXPIRING &&
-                   std::chrono::steady_clock::now() - t_arm < std::chrono::seconds(1)) {
-                __builtin_ia32_pause();
-                e = __atomic_load_n(aw, __ATOMIC_ACQUIRE);
-            }
-            ctx->arm.live = false;
-            if ((uint32_t)e == p.gen && (uint32_t)(e >> 32) != AC_ARM_GO) {
-                // it expired before the call: its waves skip everything and finish; this call
-                // launches its own kernel (a new generation, the slot cleared again)
-                ++ctx->arm_stats[2];
-                use_arm = false;
-                AC_HIP(ctx, hipEventSynchronize(sl.ev));
-                sl.pending = false;
-                if (p.tag) std::memset(h + p.off_counts[0], 0, p.total - p.off_counts[0]);
-                std::memset(hdr, 0, hdr_bytes);
-                if (++ctx->gen == 0) ++ctx->gen;
-                p.gen = stg.gen = ctx->gen;
-                for (uint32_t j = 0; j < p.n; ++j) publish(j, p.off_codes[j] - p.off_kmers[j]);
-            } else {
-                ++ctx->arm_stats[1];
-                launched = true;  // (its event is recorded after the publishing, like a launch's)
-            }
-        }
         // the workers start packing job 0 while this thread launches the kernel
         pool.begin((uint32_t)tasks.size(), pack_counted);
-        if (pre == 0 && !use_arm)
+        if (pre == 0)
             if (ac_status st = go()) {
                 pool.finish();
                 return st;
@@ -2242,110 +2112,6 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
     return AC_OK;
 }
 
-// Early-launch slot s runs on its own stream with its own count-kernel scratch set (slot 0: the
-// context's stream and set 0, slot 1: part stream 1 and set 1), so a call's kernel can start while
-// the previous call's kernel -- whose counts are already back -- still drains its last waves and
-// retires: consecutive calls overlap on the device by that tail instead of queueing behind it.  (The
-// DMA path's part 1 uses the same stream and set, stream-ordered behind any early call of slot 1.)
-// Opt-in, AC_SLOT_STREAMS=1: built at the end of round 4 and not yet measured on the GPU (DESIGN.md
-// §8); by default both slots run on the context's stream with scratch set 0, as measured.
-ac_status slot_stream(ac_ctx* ctx, int slot, hipStream_t* stream, int* scratch) {
-    static const bool own = env_int("AC_SLOT_STREAMS", 0) != 0;
-    *stream = ctx->stream;
-    *scratch = 0;
-    if (!own || slot == 0) return AC_OK;
-    if (!ctx->part_stream[1]) AC_HIP(ctx, hipStreamCreateWithFlags(&ctx->part_stream[1], hipStreamNonBlocking));
-    *stream = ctx->part_stream[1];
-    *scratch = 1;
-    return AC_OK;
-}
-
-// Armed launch: called by a synchronous early-launch call right after its own launch
-// and publishing, while its kernel runs.  When this call's signature repeats the previous call's, the
-// NEXT call's staged kernel is enqueued now, behind this one on the stream: the other early-launch
-// slot, the next generation, the same layout, and LaunchArgs::arm_ticks set -- so it waits for the
-// k-mers' progress records too, and gives up after AC_ARM_US microseconds without a call.  Opt-in
-// (AC_ARM_US > 0, e.g. 100): at cfg2 it measured no faster than launching in the call.  The next call with the same signature takes it over (stage_and_launch: no launch, its
-// waves already resident and polling); anything else cancels it (disarm).
-ac_status maybe_arm(ac_ctx* ctx, uint32_t k, const ac_job* jobs, const JobPlan& p) {
-    // 0: never armed; at most 0.1 s (below the staged waits' 0.5 s bound, which an armed launch's
-    // waves waiting for their k-mers must not reach while it waits for the call)
-    static const int arm_us = std::min(env_int("AC_ARM_US", 0), 100000);
-    const bool repeat = ctx->last_sig_ok && ctx->last_sig == p.sig;
-    ctx->last_sig = p.sig;
-    ctx->last_sig_ok = true;
-    if (arm_us <= 0 || !repeat || !p.tag || p.pre != 0 || !ctx->peers.empty() || ctx->arm.live) return AC_OK;
-    const int s2 = p.slot ^ 1;  // the next early-launch call's slot (ctx->early_flip)
-    hipStream_t stream = nullptr;
-    int scratch = 0;
-    if (ac_status st = slot_stream(ctx, s2, &stream, &scratch)) return st;
-    ac_ctx::Slot& sl = ctx->slot[s2];
-    if (sl.pending) {  // the call before this one (its kernel ran before this call's)
-        AC_HIP(ctx, hipEventSynchronize(sl.ev));
-        sl.pending = false;
-    }
-    if (!sl.ev) AC_HIP(ctx, hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming));
-    if (sl.h_cap < p.total) {
-        if (sl.h) (void)hipHostFree(sl.h);
-        sl.h = nullptr;
-        sl.hd = nullptr;
-        sl.h_cap = 0;
-        const size_t cap = p.total + p.total / 4;
-        AC_HIP(ctx, hipHostMalloc(&sl.h, cap, hipHostMallocDefault));
-        sl.h_cap = cap;
-        AC_HIP(ctx, hipHostGetDevicePointer(&sl.hd, sl.h, 0));
-    }
-    if (ac_status st = grow(ctx, &sl.d, &sl.d_cap, p.total)) return st;
-    const size_t hdr_bytes = sizeof(uint32_t) * AC_QUEUE_LINE * AC_HDR_LINES;
-    if (!sl.hdr) {
-        AC_HIP(ctx, hipHostMalloc((void**)&sl.hdr, hdr_bytes, hipHostMallocCoherent | hipHostMallocMapped));
-        AC_HIP(ctx, hipHostGetDevicePointer((void**)&sl.hdr_d, sl.hdr, 0));
-    }
-    std::memset(sl.hdr, 0, hdr_bytes);
-    char* h = (char*)sl.h;
-    char* hd = (char*)sl.hd;
-    char* d = (char*)sl.d;
-    std::memset(h + p.off_counts[0], 0, p.total - p.off_counts[0]);  // (tagged: no word carries the gen yet)
-    if (++ctx->gen == 0) ++ctx->gen;
-    StageLaunch stg;
-    stg.gen = ctx->gen;
-    stg.host_hdr = sl.hdr_d;
-    stg.tag = 1u;
-    stg.grp_err = (uint64_t*)(hd + p.off_gerr);
-    stg.copiers = p.copiers;
-    stg.arm_ticks = (uint32_t)std::min<uint64_t>(arm_us * 100ull, 1ull << 31);  // s_memrealtime: 100 MHz
-    ac_segment segs[AC_MAX_JOBS];
-    bool no_n[AC_MAX_JOBS] = {};
-    for (uint32_t j = 0; j < p.n; ++j) {
-        stg.src[j] = (const uint8_t*)(hd + p.off_kmers[j]);
-        stg.dst[j] = (uint8_t*)(d + p.off_kmers[j]);
-        stg.chunks[j] = p.chunks[j];
-        stg.codes_off[j] = p.codes_off[j];
-        const uint32_t nw = jobs[j].n_kmers ? p.hi[j] - p.lo[j] : 0;
-        ac_segment& g = segs[j];
-        g.kmers = (const uint64_t*)(d + p.off_kmers[j]);
-        g.n_kmers = jobs[j].n_kmers;
-        g.sample = ac_windows{(const uint32_t*)(d + p.off_codes[j]), (const uint32_t*)(d + p.off_nmask[j]),
-                              (const uint64_t*)(d + p.off_start[j]), (const uint32_t*)(d + p.off_len[j]), nw,
-                              p.n_bases[j]};
-        g.counts = (uint32_t*)(hd + p.off_counts[j]);
-    }
-    // behind this call's kernel, as on one stream (slot_stream: the slots' own streams), so its idle
-    // clock starts when this kernel is done
-    AC_HIP(ctx, hipStreamWaitEvent(stream, ctx->slot[p.slot].ev, 0));
-    if (ac_status st = launch(ctx, k, segs, p.n, stream, true, nullptr, scratch, 0, no_n, p.ulen, &stg, p.nrec))
-        return st;
-    AC_HIP(ctx, hipEventRecord(sl.ev, stream));
-    sl.pending = true;
-    ctx->arm.live = true;
-    ctx->arm.slot = s2;
-    ctx->arm.gen = stg.gen;
-    ctx->arm.n = p.n;
-    ctx->arm.sig = p.sig;
-    ++ctx->arm_stats[0];
-    return AC_OK;
-}
-
 // Shard g of G of job windows [0, n): contiguous, balanced by bases (the rule
 // of ac_error_count's multi-device split and approx_counter_amd/shard.py).
 // All G + 1 cut points of job windows [0, n) in one pass (shard g = [cut[g], cut[g + 1])).
@@ -2452,7 +2218,6 @@ ac_status count_jobs_sync(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint32_t 
                 u.plan.early = true;
                 u.plan.slot = (int)ctx->early_flip;
                 ctx->early_flip ^= 1u;
-                if (ac_status st = slot_stream(ctx, u.plan.slot, &u.stream, &u.plan.scratch)) return st;
             }
             for (uint32_t j = 0; j < n_jobs; ++j) {
                 u.plan.lo[j] = cuts[j][q];
@@ -2468,16 +2233,6 @@ ac_status count_jobs_sync(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint32_t 
         AC_HIP(u.c, hipSetDevice(u.c->device));
         if (ac_status st = stage_and_launch(u.c, k, jobs, u.plan, u.stream, nullptr, u.part, u.wave_div))
             return u.c != ctx ? fail(ctx, st, "shard " + std::to_string(g) + ": " + u.c->err) : st;
-    }
-    // the next call's armed launch, enqueued behind this call's kernel while it runs (DESIGN.md §4c;
-    // not this call's business if it cannot be made: the next call then launches its own)
-    if (units.size() == 1 && units[0].plan.early && units[0].c == ctx) {
-        const double ta = g_trace.on ? now_us() : 0.0;
-        if (maybe_arm(ctx, k, jobs, units[0].plan) != AC_OK) ctx->err.clear();
-        if (g_trace.on) {  // (AC_STAGE_TRACE: in "d2h_enq", which an early launch does not use)
-            g_trace.sum[5] += now_us() - ta;
-            g_trace.cur[5] += now_us() - ta;
-        }
     }
     for (uint32_t j = 0; j < n_jobs; ++j)
         for (uint32_t i = 0; i < jobs[j].n_kmers; ++i) jobs[j].counts[i] = 0;
@@ -2558,21 +2313,15 @@ ac_status ac_error_count_jobs(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint3
 
 uint32_t ac_testing_stage_hooks(uint32_t flags) { return g_test_hooks.exchange(flags); }
 
-int ac_testing_arm_stats(const ac_ctx* ctx, uint64_t* stats) {
-    if (!ctx || !stats) return -1;
-    for (int i = 0; i < 4; ++i) stats[i] = ctx->arm_stats[i];
-    return 0;
-}
-
+// (ABI 5's armed launch was removed in ABI 6 -- measured no faster at any configuration,
+// DESIGN.md §4c -- so nothing is ever left waiting for a next call: ac_idle only checks its argument.)
 ac_status ac_idle(ac_ctx* ctx) {
     if (!ctx) return fail(nullptr, AC_ERR_INVALID, "ctx is NULL");
-    disarm(ctx);
     return AC_OK;
 }
 
 ac_status ac_error_count_jobs_submit(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint32_t n_jobs,
                                      uint32_t* d_counts, void* hip_stream) {
-    disarm(ctx);  // (an armed launch waits for the next jobs call only)
     if (ac_status st = check_jobs(ctx, k, jobs, n_jobs)) return st;
     if (!ctx->peers.empty())
         return fail(ctx, AC_ERR_INVALID, "ac_error_count_jobs_submit needs a single-device context");

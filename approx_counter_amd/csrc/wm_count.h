@@ -50,14 +50,6 @@ constexpr int waves_per_simd(int W) { return W == 2 ? AC_W2_WAVES : 8; }
                          //   the host gave up on the call (the waves skip the segment)
 #define AC_HDR_INFO_HAS_N 0x80000000u
 #define AC_HDR_INFO_ABORT 0xffffffffu
-// Armed launch (a staged launch enqueued before its call): segment 0's header line
-// also holds, at words 4-5, one 8-byte word the kernel stores {generation, AC_ARM_*} into when it
-// gives up waiting for the call -- the two sides' handshake (the host publishes, then reads it; the
-// kernel stores it, then reads the header once more).
-#define AC_HDR_ARM 4
-#define AC_ARM_EXPIRING 1u
-#define AC_ARM_GO 2u
-#define AC_ARM_EXPIRED 3u
 #define AC_HDR_LINES AC_MAX_SEGS
 #define AC_STAGE_CHUNK 4096u  // bytes one wave copies per claimed chunk (64 lanes x 16 B x 4)
 #define AC_STAGE_REPL 32      // replicas of a segment's done counter (pollers spread over lines)
@@ -69,12 +61,10 @@ constexpr int waves_per_simd(int W) { return W == 2 ? AC_W2_WAVES : 8; }
 // AC_STAGE_REPL replicas of the N-free bytes available so far, AC_STAGE_REPL
 // done replicas (every workgroup polls one replica of each: ~1000 waves
 // polling one line slowed the chunk copies).
-// Then the armed launch's decision (0 waiting, 1 the call came, 2 expired: every segment skips).
 #define AC_STAGE_L_ERR 0
 #define AC_STAGE_SEG_LINES (4 + 2 * AC_STAGE_REPL)
 #define AC_STAGE_L_SEG(s) (1 + (s) * AC_STAGE_SEG_LINES)
-#define AC_STAGE_L_ARM (1 + AC_MAX_SEGS * AC_STAGE_SEG_LINES)
-#define AC_STAGE_LINES (AC_STAGE_L_ARM + 1)
+#define AC_STAGE_LINES (1 + AC_MAX_SEGS * AC_STAGE_SEG_LINES)
 // 0.5 s of s_memrealtime (100 MHz) WITHOUT PROGRESS: every wait is bounded, and its clock restarts
 // whenever the words it waits on advance (a large call may take far longer than this to pack)
 #define AC_STAGE_TIMEOUT_TICKS 50000000ull
@@ -153,10 +143,6 @@ struct LaunchArgs {
     // the rest (large calls: thousands of chunks arrive over the whole packing time, and a
     // workgroup holding a ticket would hold its waves until its chunk is packed)
     uint32_t copier_wgs;
-    // staged: nonzero = an armed launch, enqueued before its call: its segments' k-mers are not in the
-    // pinned block yet (they wait for the progress records like the codes), and segment 0's poller
-    // gives up after arm_ticks of s_memrealtime with no record (every segment then skipped)
-    uint32_t arm_ticks;
     uint32_t n_segs;
     uint32_t eq;  // every live segment has equal windows (ulen), checked on the host to fit its image
     uint32_t m;  // k-mer length

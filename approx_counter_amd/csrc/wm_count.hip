@@ -332,63 +332,11 @@ struct StageClock {
     }
 };
 
-// Armed launch (LaunchArgs::arm_ticks): waits for the call, seen through the header line `rh` of
-// segment si.  Segment 0's poller decides once, in the launch's device word `dec`: the call came (its
-// first progress record or final header is out: 1) or, after `arm` ticks of s_memrealtime without
-// one, expired (2).  Expiring is a handshake with the host through the ARM word of segment 0's header
-// (wm_count.h): the poller stores EXPIRING, reads the header once more and stores the outcome; the
-// host publishes its first records, then reads the word -- so of a call published just then and an
-// expiry, at least one side sees the other, and the host waits for the outcome when it sees
-// EXPIRING.  The other segments' pollers follow the decision.  True: the call came.
-__device__ __forceinline__ bool stage_arm_wait(__amdgpu_buffer_rsrc_t rh, uint32_t* hdr, uint32_t* dec, uint32_t gen,
-                                               uint32_t si, uint32_t arm, StageClock& clk, bool& late) {
-    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-    const uint32_t lane = threadIdx.x & 63u;
-    late = false;
-    if (si != 0u) {
-        for (;;) {
-            const uint32_t d = wave_load(dec);
-            if (d) return d == 1u;
-            if (clk.late()) {
-                late = true;
-                return false;
-            }
-            __builtin_amdgcn_s_sleep(8);
-        }
-    }
-    auto called = [&]() {
-        const v4u hv = __builtin_amdgcn_raw_buffer_load_b128(rh, 0, 0, 17);  // sc0 sc1: system scope
-        return __builtin_amdgcn_readfirstlane(hv.x) == gen || __builtin_amdgcn_readfirstlane(hv.z) == gen;
-    };
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    bool came = true;
-    while (!called()) {
-        if (__builtin_amdgcn_s_memrealtime() - t0 > arm) {
-            uint64_t* aw = (uint64_t*)(hdr + AC_HDR_ARM);
-            if (lane == 0)
-                __hip_atomic_store(aw, ((uint64_t)AC_ARM_EXPIRING << 32) | gen, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_SYSTEM);
-            // the store is out before the header is read again (system-scope fence, vector memory only)
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            came = called();
-            if (lane == 0)
-                __hip_atomic_store(aw, ((uint64_t)(came ? AC_ARM_GO : AC_ARM_EXPIRED) << 32) | gen,
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            break;
-        }
-        __builtin_amdgcn_s_sleep(8);
-    }
-    wave_store(dec, came ? 1u : 2u);
-    return came;
-}
-
 // Claims and serves tickets until none is left; false on timeout.  Chunks below `pre_chunks` (the
 // k-mer section, in place in the pinned block before the launch) are copied without waiting.
-// `arm`: LaunchArgs::arm_ticks (an armed launch's pollers first wait for the call, stage_arm_wait).
 __device__ __attribute__((noinline)) bool stage_copy(const uint8_t* src, uint8_t* dst, uint32_t chunks,
                                                      uint32_t pre_chunks, uint32_t* hdr, uint32_t* words,
-                                                     uint32_t* chunk_gen, uint32_t gen, uint32_t si, uint32_t arm) {
+                                                     uint32_t* chunk_gen, uint32_t gen, uint32_t si) {
     const uint32_t lane = threadIdx.x & 63u;
     const StageWords sw = stage_words(words);
     StageClock clk;
@@ -406,20 +354,6 @@ __device__ __attribute__((noinline)) bool stage_copy(const uint8_t* src, uint8_t
             static_assert(AC_HDR_PGEN == 0 && AC_HDR_READY == 1 && AC_HDR_FLAG == 2 && AC_HDR_INFO == 3,
                           "header layout");
             const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc((void*)hdr, 0, 16, 0x00020000);
-            if (arm) {
-                bool late = false;
-                if (!stage_arm_wait(rh, hdr, words + (AC_STAGE_L_ARM - AC_STAGE_L_SEG(si)) * AC_QUEUE_LINE, gen, si,
-                                    arm, clk, late)) {
-                    // expired (or, never expected, no decision): every wave skips the segment
-                    wave_store(sw.verdict, ~0u);
-                    wave_store(sw.bytes, 0u);
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    wave_store(sw.fin, 1u);
-                    if (late) return false;
-                    continue;
-                }
-                clk.progress();
-            }
             uint32_t published = 0;
             for (;;) {
                 const v4u hv = __builtin_amdgcn_raw_buffer_load_b128(rh, 0, 0, 17);  // sc0 sc1: system scope
@@ -708,9 +642,8 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
     uint32_t* st_words = nullptr;
     if (STAGED && sg.stage_chunks) {  // (a segment sent ahead of a staged launch has no chunks)
         st_words = a.stage + AC_STAGE_L_SEG(si) * AC_QUEUE_LINE;
-        // the k-mer section fills whole chunks and is in the pinned block before the launch (an armed
-        // launch's: not yet, its k-mers wait for the progress records like the codes)
-        const uint32_t pre_bytes = a.arm_ticks ? 0u : sg.stage_codes_off, pre_chunks = pre_bytes / AC_STAGE_CHUNK;
+        // the k-mer section fills whole chunks and is in the pinned block before the launch
+        const uint32_t pre_bytes = sg.stage_codes_off, pre_chunks = pre_bytes / AC_STAGE_CHUNK;
         if (a.copier_wgs && blockIdx.x < a.copier_wgs) {
             // Copier workgroup of a large call: every wave serves every segment's tickets, starting
             // with segment (workgroup mod segments) -- the host packs a large call's jobs interleaved,
@@ -720,9 +653,9 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
                 const SegDev& c2 = a.seg[s2];
                 if (!c2.stage_chunks) continue;
                 if (!__builtin_amdgcn_readfirstlane((uint32_t)stage_copy(
-                        c2.stage_src, c2.stage_dst, c2.stage_chunks, a.arm_ticks ? 0u : c2.stage_codes_off / AC_STAGE_CHUNK,
+                        c2.stage_src, c2.stage_dst, c2.stage_chunks, c2.stage_codes_off / AC_STAGE_CHUNK,
                         a.host_hdr + s2 * AC_QUEUE_LINE, a.stage + AC_STAGE_L_SEG(s2) * AC_QUEUE_LINE, c2.stage_gen,
-                        a.gen, s2, a.arm_ticks)))
+                        a.gen, s2)))
                     if (lane == 0) atomicOr(a.err, AC_DEVERR_STAGE);
             }
         }
@@ -736,7 +669,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
                 !__builtin_amdgcn_readfirstlane(
                     (uint32_t)stage_copy(sg.stage_src, sg.stage_dst, sg.stage_chunks, pre_chunks,
                                          a.host_hdr + (uint32_t)si * AC_QUEUE_LINE, st_words, sg.stage_gen, a.gen,
-                                         (uint32_t)si, a.arm_ticks))) {
+                                         (uint32_t)si))) {
                 if (lane == 0) atomicOr(a.err, AC_DEVERR_STAGE);
             } else if (equal) {
                 // only the k-mers (the ~Eq table) are needed before counting starts

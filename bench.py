@@ -208,6 +208,26 @@ def load_pmc(workload: str):
     return best
 
 
+def stage_text(stage_path: str, world: int) -> str:
+    """config.stage: what one timed step runs, from host Dna5 buffers to counts."""
+    if stage_path == "early-launch":
+        body = ("1 fused count launch issued first in the call, then both read ends packed (host pool, pinned; "
+                "N positions inline in each window's slot) with progress records; 16 copier workgroups of the "
+                "kernel pull each 4 KB chunk into HBM as it is packed while the others count a window as soon "
+                "as its chunk is in")
+    else:
+        body = ("per part (>= 2^17 windows: 2 parts, >= 2^19: 4): pack (host pool, pinned), copy-engine DMA into "
+                "HBM while the previous part counts")
+    if world > 1:
+        tail = " -> RCCL all-reduce -> counts D2H"
+    elif stage_path == "early-launch":
+        tail = (" -> counts tagged with the call's generation stored to pinned host memory by each candidate "
+                "group, polled")
+    else:
+        tail = " -> counts stored to pinned host memory by the kernel"
+    return "Dna5 host buffers -> " + body + " (both ends)" + tail
+
+
 def build_workload(args, rank, world):
     """This rank's {end: {kmers, windows}} and the units of the whole job per step."""
     from approx_counter_amd.shard import shard_bounds
@@ -279,10 +299,6 @@ def main():
     units_rank = sum(n * b for n, b in zip(n_c, bases))
     jobs = ac.Jobs([(wl[e]["kmers"], ac.Dna5Sample.from_windows(wl[e]["windows"])) for e in ends])
     counter = ac.ApproxCounter(local)
-    pool_participants, pool_cpus = host_pool_cpus()  # planned by the first ac_create
-    if world > 1:
-        print(f"[bench] rank {rank} (local {local}): host pool {pool_participants} participants on CPUs "
-              f"{_ranges(pool_cpus)}", file=sys.stderr, flush=True)
     stream = torch.cuda.current_stream(dev)
     d_counts = torch.zeros(max(1, jobs.n_counts), dtype=torch.int32, device=dev)
     h_counts = torch.zeros(max(1, jobs.n_counts), dtype=torch.int32).pin_memory()
@@ -402,21 +418,21 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    # (back-to-back calls of one shape keep the next call's kernel enqueued -- the armed launch,
-    # DESIGN.md §4c; no call follows here, so it is cancelled before the device-wide sync)
-    counter.idle()
+    # the pool that packs the timed steps: made by the first stage call (its size is the plan's, or
+    # AC_HOST_THREADS when set), so read after that call, not from the plan before it
+    pool_participants, pool_cpus = host_pool_cpus()
+    if world > 1:
+        print(f"[bench] rank {rank} (local {local}): host pool {pool_participants} participants on CPUs "
+              f"{_ranges(pool_cpus)}", file=sys.stderr, flush=True)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    arm0 = counter.arm_stats()
     t0 = time.perf_counter()
     marks = []
     for _ in range(args.steps):
         step()
         marks.append(time.perf_counter())
-    counter.idle()  # (the armed launch of a step K + 1 that never comes)
-    arm1 = counter.arm_stats()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -456,19 +472,7 @@ def main():
             "data": DATA_NOTE,
             "config": {"workload": workload_name, "k": args.k, "sn": args.sn, "sl": args.sl, "lim": args.lim,
                        "candidates": n_c, "kmer_bp_per_step": units_job, "kmer_bp_per_rank_step": units_rank,
-                       "stage": ("Dna5 host buffers -> "
-                                 + ("1 fused count launch (enqueued during the previous step when the shape repeats "
-                                    "-- the armed launch -- else issued first), then both read ends packed (host pool, "
-                                    "pinned; N positions inline in each window's slot) with progress records; 16 "
-                                    "copier workgroups of the kernel pull each 4 KB chunk into HBM as it is packed "
-                                    "while the others count a window as soon as its chunk is in" if stage_path == "early-launch"
-                                    else ("per part (>= 2^17 windows: 2 parts, >= 2^19: 4): pack (host pool, pinned), "
-                                          "copy-engine DMA into HBM while the previous part counts"))
-                                 + " (both ends)"
-                                 + (" -> RCCL all-reduce -> counts D2H" if world > 1 else
-                                    (" -> counts tagged with the call's generation stored to pinned host memory by "
-                                     "each candidate group, polled" if stage_path == "early-launch"
-                                     else " -> counts stored to pinned host memory by the kernel"))),
+                       "stage": stage_text(stage_path, world),
                        "stage_path": stage_path,
                        "parallelism": (f"{args.scaling} window shards x{world}, "
                                        f"{'RCCL' if backend == 'nccl' else backend} all-reduce of counts")
@@ -477,15 +481,13 @@ def main():
         }
         if world == 1:  # each step is synchronous at N = 1: its own duration
             d = np.diff(np.array([t0] + marks)) * 1e3
-            out["step_ms"] = {"min": float(d.min()), "p50": float(np.median(d)), "max": float(d.max())}
+            out["step_ms"] = {"min": float(d.min()), "p50": float(np.median(d)), "p99": float(np.percentile(d, 99)),
+                              "p99.9": float(np.percentile(d, 99.9)), "max": float(d.max())}
         out["stage_cold_call_ms"] = cold_ms
-        out["armed_launch"] = {"enqueued": arm1[0] - arm0[0], "taken_over": arm1[1] - arm0[1],
-                               "expired": arm1[2] - arm0[2], "cancelled": arm1[3] - arm0[3],
-                               "note": "timed steps: each step's count kernel enqueued by the step before it "
-                                       "(DESIGN.md 4c; ac_idle cancels the one left after the last step)"}
         out["host_pool"] = {"participants": pool_participants, "cpus": _ranges(pool_cpus),
-                            "note": "rank 0's pack pool: GPU-local CPUs split among the local ranks, at most its "
-                                    "share of the cgroup CPU quota (ac_host_pool_cpus)"}
+                            "note": "rank 0's pack pool as it ran the timed steps (read after the first stage call "
+                                    "made it): GPU-local CPUs split among the local ranks, at most its share of the "
+                                    "cgroup CPU quota, or AC_HOST_THREADS when set (ac_host_pool_cpus)"}
         out["stage_path_choice"] = {"path": stage_path, "untimed_calls": tune_calls,
                                     "note": "ac_stage_mode: the early launch at every size since round 4 (DMA parts "
                                             "only with AC_STAGE_EARLY=0)"}

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define AC_ABI_VERSION 5
+#define AC_ABI_VERSION 6
 
 typedef int32_t ac_status;
 #define AC_OK 0
@@ -294,19 +294,11 @@ typedef struct ac_job {
 ac_status ac_error_count_jobs(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint32_t n_jobs);
 
 /*
- * Armed launches (ABI 5; opt-in: the environment variable AC_ARM_US > 0, read
- * once per process): once two consecutive ac_error_count_jobs calls on ctx
- * have the same shape (k, the jobs' candidate and window counts, window
- * lengths), each such call also enqueues the NEXT call's count kernel behind
- * its own, on the other staging slot.  Its waves start as soon as this call's
- * kernel ends and wait for the next call's inputs, so that call pays no launch
- * latency; a call of another shape, or any other entry point, cancels it
- * first, and it gives up by itself after AC_ARM_US microseconds without a call
- * (at most 100000).  While it waits it holds the device's
- * compute units, so a caller that makes no further call soon -- and is about to
- * synchronise the device or run other GPU work -- cancels it with ac_idle.
- * The reference makes one errorCount call per read end per run
- * (approx_counter.cpp:922); repeated calls are a serving loop's pattern.
+ * ABI 5 added armed launches (opt-in: the next synchronous call's kernel
+ * enqueued during the current one) and ac_idle to cancel them.  They measured
+ * no faster at any configuration and were removed in ABI 6, so
+ * no call leaves device work behind it; ac_idle is kept for callers built
+ * against ABI 5 and only checks its argument (AC_ERR_INVALID for NULL).
  */
 ac_status ac_idle(ac_ctx* ctx);
 

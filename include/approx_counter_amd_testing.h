@@ -34,10 +34,6 @@ extern "C" {
 /* Sets the hooks (an OR of the flags above); returns the previous value. */
 uint32_t ac_testing_stage_hooks(uint32_t flags);
 
-/* Armed launches of ctx so far (ac_idle, include/approx_counter_amd.h): stats[0]
- * enqueued, [1] taken over by their call, [2] expired before their call came
- * (the call launched its own kernel), [3] cancelled.  Returns 0, -1 if ctx is NULL. */
-int ac_testing_arm_stats(const ac_ctx* ctx, uint64_t* stats);
 
 #ifdef __cplusplus
 }

@@ -27,7 +27,7 @@ def test_library_targets_gfx950():
 
 
 def test_abi_version():
-    assert _lib.load().ac_abi_version() == 5
+    assert _lib.load().ac_abi_version() == 6
 
 
 def test_pack_layout():
@@ -69,15 +69,13 @@ def test_comm_entry_points_without_a_context():
     assert L.ac_allreduce_counts(None, None, 0, None) == _lib.AC_ERR_INVALID
 
 
-def test_arm_entry_points_without_a_context():
-    """ac_idle (ABI 5) rejects a NULL context; the test-only arm statistics report -1 for it."""
-    import ctypes
-
+def test_idle_without_a_context():
+    """ac_idle (kept from ABI 5; a no-op since the armed launch was removed in ABI 6) rejects a NULL
+    context, and the removed test-only arm statistics are no longer exported."""
     L = _lib.load()
     assert L.ac_idle(None) == _lib.AC_ERR_INVALID
     assert b"ctx" in L.ac_last_error(None)
-    buf = (ctypes.c_uint64 * 4)()
-    assert L.ac_testing_arm_stats(None, buf) == -1
+    assert not hasattr(L, "ac_testing_arm_stats")
 
 
 def _has_gpu():

@@ -41,3 +41,14 @@ def test_cpu_share_reports_nproc():
     n, quota = bench.cpu_share()
     assert n == len(os.sched_getaffinity(0))
     assert quota is None or quota > 0
+
+
+def test_stage_text_says_what_runs():
+    """config.stage describes the timed step as it runs: the count launch is issued first in each
+    call (the armed launch, which enqueued it during the previous step, was removed in ABI 6)."""
+    for world in (1, 2):
+        t = bench.stage_text("early-launch", world)
+        assert "issued first in the call" in t
+        assert "armed" not in t and "previous step" not in t
+    assert "DMA" in bench.stage_text("dma", 1)
+    assert bench.stage_text("early-launch", 2).endswith("RCCL all-reduce -> counts D2H")

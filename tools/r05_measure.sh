@@ -1,0 +1,74 @@
+#!/bin/bash
+# Round-5 measurement batch on the GPU box (one box acquisition per call).  Every step has its
+# own time limit; a test failure (rc 1) lets the next step run, anything else stops the batch.
+# usage: tools/r05_measure.sh OUTDIR part...
+#   slots     AC_SLOT_STREAMS=1 vs default: cfg2 stage x3 interleaved, cfg3 / cfg5 / cfg4 once each,
+#             and the jobs tests on two slot streams
+#   long      2,000 cfg2 steps with the host pool at 16 / 15 / 14 participants (step-time tail)
+#   stamps    per-wave timelines of the resident cfg2 launch (-DAC_STAMPS build in build/var/stamps)
+#   suite     the whole -m gpu suite
+#   configs   bench lines at cfg2-cfg5 (stage traces on)
+#   prof      kernel trace of bench.py at cfg2
+#   pmc       SQ issue/wait counters, WRITE/FETCH_SIZE and a kernel trace of the resident cfg2 kernel
+set -u
+OUT=$1; shift
+case $OUT in /*) ;; *) OUT=${GRAFT_REPO_ROOT:-$(pwd)}/$OUT ;; esac
+mkdir -p "$OUT"
+run() {  # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  echo "== $name" | tee -a "$OUT/summary.log"
+  timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "   rc=$rc" | tee -a "$OUT/summary.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after rc=$rc"; tail -20 "$OUT/$name.log"; exit $rc; fi
+  grep -h 'passed\|failed\|"ms_per_step"' "$OUT/$name.log" \
+    | sed -e 's/.*"value": \([0-9.e+]*\).*"ms_per_step": \([0-9.]*\).*"step_ms": \({[^}]*}\).*/value \1 ms_per_step \2 \3/' \
+    | cut -c1-300 | tee -a "$OUT/summary.log"
+}
+PYT="python3 -u -m pytest -x -v --timeout 300 --timeout-method thread -p no:cacheprovider"
+BQ="--no-cpu-baseline --no-pipelined"
+B="python3 bench.py --steps 400 --warmup 20 --no-cpu-baseline --no-pipelined --no-kernel-leg"
+for part in "$@"; do
+case $part in
+slots)
+  for rep in 1 2 3; do
+    run ab_one_$rep 120 $B
+    run ab_slots_$rep 120 env AC_SLOT_STREAMS=1 $B
+  done
+  for c in cfg3 cfg5 cfg4; do
+    run ab_one_$c 200 python3 bench.py --config $c --steps 20 --warmup 5 $BQ --no-kernel-leg
+    run ab_slots_$c 200 env AC_SLOT_STREAMS=1 python3 bench.py --config $c --steps 20 --warmup 5 $BQ --no-kernel-leg
+  done
+  run tests_jobs_slots 400 env AC_SLOT_STREAMS=1 $PYT -m gpu tests/test_gpu_jobs.py tests/test_gpu_bench_path.py ;;
+long)
+  for t in 16 15 14; do
+    run long_t$t 200 env AC_HOST_THREADS=$t python3 bench.py --steps 2000 --warmup 20 $BQ --no-kernel-leg
+  done ;;
+stamps)
+  run stamps_resident 120 env APPROX_COUNTER_AMD_LIB=build/var/stamps/libapprox_counter_amd.so python3 tools/stamps.py
+  run stamps_staged 120 env APPROX_COUNTER_AMD_LIB=build/var/stamps/libapprox_counter_amd.so python3 tools/stage_stamps.py --calls 40 ;;
+suite)
+  run suite 1100 $PYT -m gpu tests ;;
+configs)
+  for c in cfg2 cfg3 cfg5 cfg4; do
+    run bench_$c 300 env AC_STAGE_TRACE=1 python3 bench.py --config $c --steps 20 --warmup 5 $BQ
+  done ;;
+prof)
+  ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_bench" -o run -- \
+    python3 "$GRAFT_REPO_ROOT/bench.py" --steps 100 --warmup 10 --no-cpu-baseline --no-pipelined --kernel-launches 100 ) \
+    > "$OUT/prof_bench.log" 2>&1 || { echo "prof failed"; exit 6; }
+  tail -2 "$OUT/prof_bench.log" | cut -c1-300 ;;
+pmc)
+  for c in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_SALU SQ_ACTIVE_INST_LDS" \
+           "SQ_WAIT_INST_LDS SQ_ACTIVE_INST_SCA SQ_INSTS_VALU SQ_WAVES SQ_INSTS_SALU SQ_INSTS_LDS SQ_LEVEL_WAVES SQ_BUSY_CU_CYCLES" \
+           "WRITE_SIZE" "FETCH_SIZE"; do
+    n=$(echo $c | cut -d' ' -f1)
+    ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 60 rocprofv3 --pmc $c -d "$OUT/pmc_$n" -o run -- \
+      python3 "$GRAFT_REPO_ROOT/tools/kernel_run.py" --config cfg2 --launches 20 ) > "$OUT/pmc_$n.log" 2>&1 || { echo "pmc $n failed"; exit 3; }
+    echo "== pmc $n ok" | tee -a "$OUT/summary.log"
+  done
+  ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 90 rocprofv3 --kernel-trace --stats -d "$OUT/trace_cfg2" -o run -- \
+    python3 "$GRAFT_REPO_ROOT/tools/kernel_run.py" --config cfg2 --launches 50 --warmup 150 ) > "$OUT/trace_cfg2.log" 2>&1 || exit 4
+  echo "== trace ok" | tee -a "$OUT/summary.log" ;;
+esac
+done
