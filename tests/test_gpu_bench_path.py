@@ -83,3 +83,24 @@ def test_bench_cfg4_rank_shard_submit_bit_exact(rank):
         sync = c.count_jobs(16, jobs)
         for g, x in zip(sync, exp):
             assert np.array_equal(g, x)
+
+
+def test_bench_line_reports_the_pool_that_ran():
+    """bench.py's host_pool record is read after the first stage call made the pool, so a pool sized
+    by AC_HOST_THREADS is reported as such (the shard projection's line said 16 for a
+    2-thread pool), and config.stage names the launch as issued first in the call."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, AC_HOST_THREADS="3")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "3", "--warmup", "1",
+                        "--no-cpu-baseline", "--no-pipelined", "--no-kernel-leg"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["host_pool"]["participants"] == 3
+    assert "issued first in the call" in line["config"]["stage"]
+    assert "armed_launch" not in line

@@ -49,6 +49,14 @@ stamps)
   run stamps_staged 120 env APPROX_COUNTER_AMD_LIB=build/var/stamps/libapprox_counter_amd.so python3 tools/stage_stamps.py --calls 40 ;;
 suite)
   run suite 1100 $PYT -m gpu tests ;;
+tests)
+  run tests_bench_path 400 $PYT -m gpu tests/test_gpu_bench_path.py
+  run tests_jobs 400 $PYT -m gpu tests/test_gpu_jobs.py ;;
+sweep)  # kernel time against windows per wave (sample size), default item sizes and forced 2 / 4 windows per item
+  for v in main chunk2 chunk4; do
+    L=$([ $v = main ] && echo "" || echo "APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so")
+    run sweep_$v 300 env $L python3 tools/kernel_sweep.py --sn 10000,20000,40000,100000
+  done ;;
 configs)
   for c in cfg2 cfg3 cfg5 cfg4; do
     run bench_$c 300 env AC_STAGE_TRACE=1 python3 bench.py --config $c --steps 20 --warmup 5 $BQ
