@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--sn", default="10000,20000,40000,100000")
     ap.add_argument("--lim", type=int, default=500)
     ap.add_argument("--k", type=int, default=16)
+    ap.add_argument("--sl", type=int, default=100)
     ap.add_argument("--launches", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=150)
     a = ap.parse_args()
@@ -31,7 +32,7 @@ def main():
     import bench
 
     sns = [int(x) for x in a.sn.split(",")]
-    sys.argv = ["bench.py", "--sn", str(max(sns)), "--lim", str(a.lim), "--k", str(a.k)]
+    sys.argv = ["bench.py", "--sn", str(max(sns)), "--lim", str(a.lim), "--k", str(a.k), "--sl", str(a.sl)]
     args = bench.parse()
     full, _ = bench.build_workload(args, 0, 1)
     ends = ("start", "end")

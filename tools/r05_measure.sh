@@ -52,6 +52,22 @@ suite)
 tests)
   run tests_bench_path 400 $PYT -m gpu tests/test_gpu_bench_path.py
   run tests_jobs 400 $PYT -m gpu tests/test_gpu_jobs.py ;;
+ptests)  # the launch tail's pieces: their tests and the parity / bench-path / jobs suites
+  run tests_pieces 600 $PYT -m gpu tests/test_gpu_pieces.py
+  run tests_parity 600 $PYT -m gpu tests/test_gpu_parity.py tests/test_gpu_bench_path.py tests/test_gpu_jobs.py ;;
+pieces)  # kernel and stage A/B of the launch tail's pieces against variants
+  for rep in 1 2; do
+    for v in main nopieces pieces2 pieceshalf; do
+      L=$([ $v = main ] && echo "" || echo "APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so")
+      run ksweep_${v}_$rep 300 env $L python3 tools/kernel_sweep.py --sn 10000,100000 --launches 200
+    done
+  done
+  for v in main nopieces; do
+    L=$([ $v = main ] && echo "" || echo "APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so")
+    run kcfg3_$v 300 env $L python3 tools/kernel_sweep.py --sn 100000 --lim 2000 --launches 30 --warmup 10
+    run kcfg5_$v 300 env $L python3 tools/kernel_sweep.py --sn 100000 --lim 1000 --k 22 --sl 150 --launches 30 --warmup 10
+    run stage_$v 200 env $L $B
+  done ;;
 sweep)  # kernel time against windows per wave (sample size), default item sizes and forced 2 / 4 windows per item
   for v in main chunk2 chunk4; do
     L=$([ $v = main ] && echo "" || echo "APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so")

@@ -30,17 +30,23 @@ def main():
 
     wl, _ = workload.build(n_reads=a.sn, k=a.k, lim=a.lim)
     c = ac.ApproxCounter(0)
-    segs = [ac.DeviceSegment.upload(wl[e]["kmers"], ac.pack_windows(wl[e]["windows"])) for e in ("start", "end")]
+    packed = [ac.pack_windows(wl[e]["windows"]) for e in ("start", "end")]
+    segs = [ac.DeviceSegment.upload(wl[e]["kmers"], packed[i]) for i, e in enumerate(("start", "end"))]
+    # the equal-window launch, as the bench's kernel leg and the stage run it
+    wlen = [p.equal_window_len() for p in packed]
+    wlen = wlen if all(x is not None for x in wlen) else None
     for _ in range(5):
-        c.count_device(a.k, segs)
+        c.count_device(a.k, segs, window_len=wlen)
     torch.cuda.synchronize()
     geo = c.last_launch()
     n = int(geo["waves"])
-    buf = np.zeros(8 * (1 << 18), dtype=np.uint64)
+    N_ST, N_SG, N_WIN = 1 << 21, 64, 1 << 20  # g_stamps, g_stage_stamps, g_win_stamps (wm_count.hip)
+    buf = np.zeros(N_ST + N_SG + N_WIN, dtype=np.uint64)
     L = _lib.load()
     L.ac_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
     assert L.ac_debug_stamps(buf.ctypes.data, buf.nbytes) == 0
     raw = buf[: 8 * n].reshape(n, 8).astype(np.int64)
+    win = buf[N_ST + N_SG:].reshape(1 << 15, 32)[:n].astype(np.int64)
     st = raw[:, :4]
     t0 = st[:, 0].min()
     us = (st - t0) / 100.0  # 100 MHz
@@ -93,8 +99,38 @@ def main():
     for t in (2, 5, 10, 20, 30):
         counting = ((us[:, 1] <= t) & (us[:, 2] > t)).sum() / keys.size
         print(f"t={t:3d} us: counting waves per SIMD {counting:.2f}")
-    print("mean resident waves per SIMD at 10%..90% of the kernel:",
+    print("mean resident waves per SIMD at 10/30/50/70/80/90/95 % of the kernel:",
           [round(float(active[:, int(f * 199)].mean()), 2) for f in (0.1, 0.3, 0.5, 0.7, 0.8, 0.9, 0.95)])
+    # Per-window stamps (the end of each window a wave counted): window durations against the
+    # number of waves resident on the wave's SIMD at the window's midpoint, i.e. the SIMD's
+    # throughput as waves leave it (the launch tail), and the launch an even end would give.
+    if n <= (1 << 15):
+        ends = (win - t0) / 100.0
+        per_n = {}
+        tot_windows = np.zeros(keys.size)
+        for i in range(n):
+            e = ends[i][(ends[i] > us[i, 1]) & (ends[i] <= us[i, 2] + 1e-9)]  # this launch's stamps only
+            e = np.sort(e)
+            if e.size == 0:
+                continue
+            tot_windows[inv[i]] += e.size
+            prev = np.concatenate([[us[i, 1]], e[:-1]])
+            mid = (prev + e) / 2
+            gi = np.clip(np.searchsorted(grid, mid), 0, grid.size - 1)
+            nres = active[inv[i], gi].astype(int)
+            for d, r in zip(e - prev, nres):
+                per_n.setdefault(int(r), []).append(d)
+        print("window durations by waves resident on the SIMD (n: windows, mean us, SIMD windows/us):")
+        for r in sorted(per_n):
+            d = np.array(per_n[r])
+            print(f"  n={r}: {d.size:6d} windows  mean {d.mean():6.2f} us  p50 {np.median(d):6.2f}  "
+                  f"SIMD rate {r / d.mean():.3f} windows/us")
+        if 4 in per_n:
+            r4 = 4 / np.mean(per_n[4])
+            ideal = np.median(first) + np.median(us[:, 1] - us[:, 0]) + tot_windows.mean() / r4
+            print(f"windows per SIMD: mean {tot_windows.mean():.1f}; at the full-residency rate "
+                  f"({r4:.3f}/us) they end at {ideal:.1f} us (even end); SIMDs actually end "
+                  f"p50 {np.median(last):.1f} / max {last.max():.1f} us")
 
 
 if __name__ == "__main__":
