@@ -135,9 +135,6 @@ def load():
     if hasattr(L, "ac_testing_stage_hooks"):  # (an A/B build of an older ABI may lack it)
         L.ac_testing_stage_hooks.argtypes = [ctypes.c_uint32]
         L.ac_testing_stage_hooks.restype = ctypes.c_uint32
-    if hasattr(L, "ac_testing_last_pieces"):
-        L.ac_testing_last_pieces.argtypes = [vp]
-        L.ac_testing_last_pieces.restype = ctypes.c_int64
     if hasattr(L, "ac_idle"):  # (ABI >= 5; A/B builds of older ABIs lack it)
         L.ac_idle.argtypes = [vp]
         L.ac_idle.restype = ctypes.c_int

@@ -80,10 +80,6 @@ struct ac_ctx {
         // staged launches: per-chunk "copied" flags (= the launch's generation once in device memory)
         uint32_t* stage_gen = nullptr;
         uint32_t stage_gen_cap = 0;
-        // the pieces' meeting lines (wm_count.h LaunchArgs::split): two banks of split_cap lines of
-        // 64 u32, banked with the queue counters; split_dirty[b] = lines the last launch on bank b used
-        uint32_t* split = nullptr;
-        uint32_t split_cap = 0, split_dirty[2] = {0, 0};
     } sc[2 * AC_STAGE_MAX_PARTS];
     // streams of parts 1.. of a synchronous jobs call (part 0 runs on `stream`)
     // and of a submit (part 0 runs on the caller's stream), with the events that
@@ -97,7 +93,6 @@ struct ac_ctx {
     // last launch geometry
     uint64_t last_waves = 0;
     uint32_t last_wpw = 0, last_groups = 0;
-    uint64_t last_pieces = 0;  // windows the last launch counted in two pieces (the launch tail)
     // ac_create_multi: contexts of shards 1..n-1 (this context is shard 0)
     std::vector<ac_ctx*> peers;
     // RCCL communicator of a multi-process job (ac_comm_init), or null
@@ -316,36 +311,6 @@ uint32_t stage_copiers(uint64_t tickets, uint64_t /*resident_waves*/) {
     return tickets > (uint64_t)min_tickets ? stage_copier_wgs() : 0u;
 }
 
-// The launch tail's pieces (wm_count.h SegDev::split_n): how many of a candidate group's windows are
-// cut in two, per wave of the group (AC_SPLIT_WAVES_NUM / AC_SPLIT_WAVES_DEN pieces per wave; A/B builds
-// set other ratios, 0 = no pieces).
-#ifndef AC_SPLIT_WAVES_NUM
-#define AC_SPLIT_WAVES_NUM 1
-#endif
-#ifndef AC_SPLIT_WAVES_DEN
-#define AC_SPLIT_WAVES_DEN 1
-#endif
-#ifndef AC_TAIL_SINGLES
-#define AC_TAIL_SINGLES 1  // single-window items after `chunk`-window ones (A/B builds: 0 = none)
-#endif
-// Where a window of `len` bases is cut for k-mers of k bases: piece 1 = [0, cut + k + 1), piece 2 =
-// [cut, len), cut a multiple of 32 (a fetch's N-mask words are 32-base aligned) chosen so the longer
-// piece is shortest; 0 when no cut makes both pieces shorter than the window (or the window spans more
-// than one 256-base fetch).
-uint32_t split_cut_for(uint32_t len, uint32_t k) {
-    if (len == AC_NO_ULEN || len > 256u) return 0;
-    uint32_t best = 0, best_max = len;
-    for (uint32_t cut = 32; cut < len; cut += 32) {
-        const uint32_t a = cut + k + 1u, b = len - cut;
-        if (a >= len) break;
-        if (std::max(a, b) < best_max) {
-            best_max = std::max(a, b);
-            best = cut;
-        }
-    }
-    return best;
-}
-
 // Joins ac_create's warm-up thread (once) and takes the resident-wave counts it queried.
 void ensure_warm(ac_ctx* ctx) {
     if (!ctx->warm.joinable()) return;
@@ -453,31 +418,6 @@ ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hi
             if (zero && s.n_kmers) AC_HIP(ctx, hipMemsetAsync(s.counts, 0, sizeof(uint32_t) * s.n_kmers, stream));
         }
     }
-    // The launch tail: in equal-window launches each live segment's last windows are
-    // counted in two pieces of text each (the kernel's item order: `chunk`-window items, then single
-    // windows, then pieces), about one piece per wave of the candidate group, so the waves' last units
-    // of work are ~2/3 of a window and the SIMDs run out of work together.  After `chunk`-window items,
-    // about chunk / 2 single windows per wave absorb the unevenness of their ends.
-    bool eq_launch = true;
-    for (uint32_t i = 0; i < n; ++i)
-        if (a.seg[i].queue_begin != ~0u && a.seg[i].ulen == AC_NO_ULEN) eq_launch = false;
-    uint32_t split_lines = 0;
-    for (uint32_t i = 0; i < n; ++i) {  // (wpg below: the waves serving one candidate group)
-        acamd::SegDev& d = a.seg[i];
-        d.single_from = d.n_windows;
-        d.split_n = 0;
-        d.split_cut = 0;
-        d.split_begin = split_lines;
-        if (!eq_launch || d.queue_begin == ~0u) continue;
-        const uint64_t wpg = std::max<uint64_t>(1, std::max<uint64_t>(resident, qbegin) * d.subq / std::max(1u, qbegin));
-        const uint32_t cut = split_cut_for(d.ulen, k);
-        const uint64_t pieces = cut ? std::min<uint64_t>(d.n_windows / 4, AC_SPLIT_WAVES_NUM * wpg / AC_SPLIT_WAVES_DEN / 2) : 0;
-        d.split_n = (uint32_t)pieces;
-        d.split_cut = cut;
-        const uint32_t w2 = d.n_windows - d.split_n;
-        d.single_from = (AC_TAIL_SINGLES && chunk > 1) ? w2 - (uint32_t)std::min<uint64_t>(w2, wpg * chunk / 2) : w2;
-        split_lines += d.groups * d.split_n;
-    }
     // The group's last workgroup stores its counts (no memset), unless live
     // segments share count slots (window shards of one candidate set): then
     // zero them once and let every group add.
@@ -529,20 +469,6 @@ ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hi
         sc.bank = 0;
         sc.dirty[0] = sc.dirty[1] = 0;
     }
-    if (split_lines > sc.split_cap) {
-        if (sc.split) AC_HIP(ctx, hipFree(sc.split));
-        sc.split = nullptr;
-        sc.split_cap = 0;
-        const uint32_t cap = std::max<uint32_t>(split_lines, 1024);
-        const size_t bytes = sizeof(uint32_t) * 64 * 2 * (size_t)cap;
-        AC_HIP(ctx, hipMalloc(&sc.split, bytes));
-        AC_HIP(ctx, hipMemsetAsync(sc.split, 0, bytes, stream));
-        sc.split_cap = cap;
-        sc.split_dirty[0] = sc.split_dirty[1] = 0;
-    }
-    a.split = sc.split;
-    a.split_stride = sc.split_cap;
-    a.split_zero = sc.split_dirty[sc.bank ^ 1u];
     a.queue = sc.queue;
     a.qstride = sc.qcap;
     a.bank = sc.bank;
@@ -588,14 +514,10 @@ ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hi
     ctx->last_waves = wave;
     ctx->last_wpw = wpw;
     ctx->last_groups = groups_total;
-    ctx->last_pieces = 0;
-    for (uint32_t i = 0; i < n; ++i) ctx->last_pieces += (uint64_t)a.seg[i].split_n * a.seg[i].groups;
     AC_HIP(ctx, acamd::launch_wm2_count(a, stream));
     if (wave) {  // the launch dequeued from `bank` and zeroed the other one
         sc.dirty[sc.bank] = used;
         sc.dirty[sc.bank ^ 1u] = 0;
-        sc.split_dirty[sc.bank] = split_lines;
-        sc.split_dirty[sc.bank ^ 1u] = 0;
         sc.bank ^= 1u;
     }
     return AC_OK;
@@ -775,7 +697,6 @@ void ac_destroy(ac_ctx* ctx) {
         if (sc.acc) (void)hipFree(sc.acc);
         if (sc.tickets) (void)hipFree(sc.tickets);
         if (sc.stage_gen) (void)hipFree(sc.stage_gen);
-        if (sc.split) (void)hipFree(sc.split);
     }
     for (hipStream_t ps : ctx->part_stream)
         if (ps) (void)hipStreamDestroy(ps);
@@ -2391,8 +2312,6 @@ ac_status ac_error_count_jobs(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint3
 }
 
 uint32_t ac_testing_stage_hooks(uint32_t flags) { return g_test_hooks.exchange(flags); }
-
-int64_t ac_testing_last_pieces(const ac_ctx* ctx) { return ctx ? (int64_t)ctx->last_pieces : -1; }
 
 // (ABI 5's armed launch was removed in ABI 6 -- measured no faster at any configuration,
 // DESIGN.md §4c -- so nothing is ever left waiting for a next call: ac_idle only checks its argument.)

@@ -100,15 +100,6 @@ struct SegDev {
     uint32_t stage_chunks;
     uint32_t stage_codes_off;  // bytes of the region before the codes (k-mers)
     uint32_t* stage_gen;       // per chunk, one line each: = the launch's generation once copied (early counting)
-    // Work units of equal-window segments (EQ launches; DESIGN.md §4, "the launch tail"): windows
-    // [0, single_from) in items of `chunk` windows, [single_from, n_windows - split_n) one window per
-    // item, and the last split_n windows cut in two pieces of text each -- A = bases [0, split_cut + m + 1),
-    // B = [split_cut, ulen) -- whose level bits meet in LaunchArgs::split (split_begin: this segment's
-    // first line there, groups x split_n lines of 64 u32).  split_n = 0: no pieces.
-    uint32_t single_from;
-    uint32_t split_n;
-    uint32_t split_cut;   // a multiple of 32 (the N-mask words of a fetch are 32-base aligned)
-    uint32_t split_begin;
 };
 
 struct LaunchArgs {
@@ -152,11 +143,6 @@ struct LaunchArgs {
     // the rest (large calls: thousands of chunks arrive over the whole packing time, and a
     // workgroup holding a ticket would hold its waves until its chunk is packed)
     uint32_t copier_wgs;
-    // Pieces' meeting lines (SegDev::split_n): two banks of split_stride lines of 64 u32; this launch
-    // uses bank `bank` (zeroed) and zeroes the first split_zero lines of the other bank.
-    uint32_t* split;
-    uint32_t split_stride;
-    uint32_t split_zero;
     uint32_t n_segs;
     uint32_t eq;  // every live segment has equal windows (ulen), checked on the host to fit its image
     uint32_t m;  // k-mer length

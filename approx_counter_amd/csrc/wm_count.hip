@@ -720,19 +720,8 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
     // inline N records (nrec.h): the lane of the fetch holding a window's record word, ~0u: none
     uint32_t rec_lane = sg.nrec ? nrec_word(ulen) : ~0u;
     asm volatile("" : "+s"(rec_lane));
-    const uint32_t m = a.m;
-    // Pieces of the launch's last windows (SegDev::split_n): piece 1 = bases [0, cut + m + 1), piece 2 =
-    // [cut, ulen).  A piece counts the alignments that END inside its own positions exactly except those
-    // starting before it (its NFA starts there): an alignment of <= 2 edits spans at most m + 2 bases, so
-    // every end at or past cut + m + 1 is exact in piece 2, every earlier end in piece 1, and a bit either
-    // piece sets is a real alignment -- the OR of their level bits is the window's.
-    uint32_t split_cut = EQ ? sg.split_cut : 0u;
-    asm volatile("" : "+s"(split_cut));
-    auto desc = [&](uint32_t ww, uint32_t pc, uint64_t& base_out, uint32_t& len_out) __attribute__((always_inline)) {
-        if (EQ) {
-            base_out = (uint64_t)ww * ustride + (pc == 2u ? split_cut : 0u);
-            len_out = pc == 0u ? ulen : (pc == 1u ? split_cut + m + 1u : ulen - split_cut);
-        } else if (ulen != AC_NO_ULEN) {
+    auto desc = [&](uint32_t ww, uint64_t& base_out, uint32_t& len_out) __attribute__((always_inline)) {
+        if (EQ || ulen != AC_NO_ULEN) {
             base_out = (uint64_t)ww * ustride;
             len_out = ulen;
         } else if (STAGED) {
@@ -741,6 +730,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
             load_desc(g_start, g_length, ww, base_out, len_out);
         }
     };
+    const uint32_t m = a.m;
     // An occurrence with <= 2 edits spans >= m - 2 bases: none ends in a window's
     // first m - 3 bases, whose hit accumulation the first block skips (12 of them).
     const bool skip_first = m >= 15u;
@@ -772,11 +762,6 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
         if (lane == 0)
             __hip_atomic_exchange(&a.queue[((a.bank ^ 1u) * (uint64_t)a.qstride + z) * AC_QUEUE_LINE], 0u,
                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // ... and so are the pieces' meeting lines (one store per wave and line; every launch zeroes them,
-    // pieces or not, so the next launch on that bank finds them clean)
-    for (uint64_t z = wave; z < a.split_zero; z += a.total_waves)
-        __hip_atomic_store(&a.split[((a.bank ^ 1u) * (uint64_t)a.split_stride + z) * 64u + lane], 0u,
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
     // Dynamic work queues.  VALU issue on a SIMD goes to the oldest wave, so
     // with a static split the first waves finish early and the last ones run
@@ -793,29 +778,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
     // plain load before claiming.
     const uint32_t S = sg.subq;
     const uint32_t chunk = sg.chunk;
-    // Items in claim order (the launch tail): windows [0, w1) `chunk` at a time, then
-    // [w1, w2) one at a time, then the last n_split windows as two pieces each (EQ launches), so the
-    // waves' last units are short and the SIMDs run out of work together.
-    const uint32_t n_split = EQ ? sg.split_n : 0u;
-    const uint32_t w2 = sg.n_windows - n_split, w1 = EQ ? sg.single_from : w2;
-    const uint32_t n_big = (w1 + chunk - 1u) / chunk, n_solo = n_big + (w2 - w1);
-    const uint32_t n_items = n_solo + 2u * n_split;
-    // item -> its first window, the window after its last, and its piece (0: whole windows)
-    auto item_range = [&](uint32_t it, uint32_t& w0, uint32_t& w_end, uint32_t& pc) __attribute__((always_inline)) {
-        if (it < n_big) {
-            w0 = it * chunk;
-            w_end = min(w1, w0 + chunk);
-            pc = 0u;
-        } else if (it < n_solo) {
-            w0 = w1 + (it - n_big);
-            w_end = w0 + 1u;
-            pc = 0u;
-        } else {
-            w0 = w2 + ((it - n_solo) >> 1);
-            w_end = w0 + 1u;
-            pc = 1u + ((it - n_solo) & 1u);
-        }
-    };
+    const uint32_t n_items = (sg.n_windows + chunk - 1u) / chunk;
     uint32_t jc = j;  // sub-queue currently served
     auto counter = [&](uint32_t jj) {
         return g_queue + (uint64_t)jj * AC_QUEUE_LINE;
@@ -875,21 +838,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
     };
     uint32_t item = (j < n_items && eb_ok && !skip) ? item_of(rank) : n_items;
     uint32_t pending = 0;
-    uint32_t w = 0, item_end = 0, npc = 0;  // npc: the piece of the next window to count
-    if (item < n_items) item_range(item, w, item_end, npc);
-    // A piece's level bits (bit 3q + e: candidate slot q has an alignment with <= e edits) are OR-ed into
-    // the window's meeting line with the piece-done bit; the second piece of a window finds that bit in
-    // the returned word and counts the window.  The returned word is read one piece later (or after
-    // the loop), so the atomic's round trip is not waited for.
-    uint32_t* split_line = EQ ? a.split + ((uint64_t)a.bank * a.split_stride + sg.split_begin + (uint64_t)g * n_split) * 64u
-                              : nullptr;
-    uint32_t pend_old = 0, pend_hits = 0;  // the last piece's returned word (0: none) and level bits
-    auto settle = [&]() __attribute__((always_inline)) {  // the second piece of a window counts it
-        const uint32_t all = (pend_old | pend_hits) & (0u - (pend_old >> 31));
-#pragma unroll
-        for (int q = 0; q < Q; ++q) cnt[q] += (uint32_t)__builtin_popcount((all >> (3 * q)) & 7u);
-        pend_old = 0;
-    };
+    uint32_t w = item * chunk, item_end = min(sg.n_windows, w + chunk);
 
     // Window pipeline: the next window's first segment is fetched while the current one is counted.
     // (written so that no sum wraps: a start near 2^64 must not pass)
@@ -949,7 +898,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
     const uint32_t lane_off = (lane < 16u ? lane : (lane - 16u) & 7u) << 2;  // this lane's word of a segment, in bytes
     auto fetch_next = [&](uint64_t b) __attribute__((always_inline)) { tid_fetch(nf, im, b, lane, lane_off); };
     if (item < n_items) {
-        desc(w, npc, nbase, nlen);
+        desc(w, nbase, nlen);
         // (staged: after the table barrier -- a wave waiting for its first window must not hold
         // its workgroup's other waves at the barrier)
         if (!STAGED && fetchable(nbase, nlen)) fetch_next(nbase);
@@ -998,7 +947,6 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
     while (item < n_items) {
         const uint64_t base = nbase;
         const uint32_t len = nlen;
-        const uint32_t pc = npc;
         // Wait for this window's words here, before the next window's fetch is
         // issued: inside the chunk loop hipcc would otherwise wait for both.
         uint32_t f0 = tid_word(nf, lane);
@@ -1007,7 +955,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
         const bool last = wn >= item_end;  // the item's last window: claim the next item
         uint32_t nitem = n_items;
         if (!last) {
-            desc(wn, 0u, nbase, nlen);
+            desc(wn, nbase, nlen);
         } else {
             pending = dequeue_issue();
         }
@@ -1016,9 +964,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
         // Inline N record (nrec.h): the window's N-mask words (lanes 16-23) built from its N
         // positions; an overflowed record takes the N bitmap's words instead.
         if (rec_lane != ~0u && ok) {
-            // (piece 2's fetch starts cut bases into the window: its record word sits cut / 16 lanes lower)
-            const uint32_t pcut = pc == 2u ? split_cut : 0u;
-            const uint32_t rw = __builtin_amdgcn_readlane(f0, rec_lane - (pcut >> 4));
+            const uint32_t rw = __builtin_amdgcn_readlane(f0, rec_lane);
             const uint32_t c = rw >> 29;
             if (c == NREC_OVERFLOW) {
                 bool have = false;
@@ -1050,7 +996,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
                 uint32_t add = 0;
                 for (uint32_t i = 0; i < c; ++i) {
                     const uint32_t pos = (rw >> nrec_pos_shift(pb, i)) & pm;
-                    if (pos >= pcut && wi == ((pos - pcut) >> 5)) add |= 1u << (pos & 31u);  // (pcut: 32-aligned)
+                    if (wi == (pos >> 5)) add |= 1u << (pos & 31u);
                 }
                 f0 |= add;
             }
@@ -1085,9 +1031,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
         if (last) {
             nitem = __builtin_amdgcn_readfirstlane(item_of(jc_waves + __builtin_amdgcn_readfirstlane(pending)));
             if (nitem < n_items) {
-                uint32_t w0, we;
-                item_range(nitem, w0, we, npc);
-                desc(w0, npc, nbase, nlen);
+                desc(nitem * chunk, nbase, nlen);
             }
         } else if (fetchable(nbase, nlen)) {
             if (gate(nbase, nlen)) fetch_next(nbase);
@@ -1123,30 +1067,13 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
                 asm volatile("" : "+v"(f));
                 segment(f, sb, 0u);
             }
-            if (!EQ || pc == 0u) {
 #pragma unroll
-                for (int w = 0; w < W; ++w)
+            for (int w = 0; w < W; ++w)
 #pragma unroll
-                    for (int p = 0; p < P; ++p) {
-                        const uint32_t lb = 31u - ((m - 1u) * P + (uint32_t)p);
-                        cnt[w * P + p] += 3u - ((s[w].a0 >> lb) & 1u) - ((s[w].a1 >> lb) & 1u) - ((s[w].a2 >> lb) & 1u);
-                    }
-            } else {
-                uint32_t hits = 0;
-#pragma unroll
-                for (int w = 0; w < W; ++w)
-#pragma unroll
-                    for (int p = 0; p < P; ++p) {
-                        const uint32_t lb = 31u - ((m - 1u) * P + (uint32_t)p);
-                        const uint32_t miss = ((s[w].a0 >> lb) & 1u) | (((s[w].a1 >> lb) & 1u) << 1) |
-                                              (((s[w].a2 >> lb) & 1u) << 2);
-                        hits |= (miss ^ 7u) << (3 * (w * P + p));
-                    }
-                settle();
-                pend_hits = hits;
-                pend_old = __hip_atomic_fetch_or(split_line + (uint64_t)(w - w2) * 64u + lane, hits | 0x80000000u,
-                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
+                for (int p = 0; p < P; ++p) {
+                    const uint32_t lb = 31u - ((m - 1u) * P + (uint32_t)p);
+                    cnt[w * P + p] += 3u - ((s[w].a0 >> lb) & 1u) - ((s[w].a1 >> lb) & 1u) - ((s[w].a2 >> lb) & 1u);
+                }
         }
         stamp_win(wave, n_win++);
         // advance the cursor; at an item boundary move to the claimed item
@@ -1156,20 +1083,20 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
             if (item >= n_items && S > 1) {
                 item = __builtin_amdgcn_readfirstlane(steal());
                 if (item < n_items) {
-                    uint32_t w0, we;
-                    item_range(item, w0, we, npc);
-                    desc(w0, npc, nbase, nlen);
+                    desc(item * chunk, nbase, nlen);
                     if (fetchable(nbase, nlen)) {
                         if (gate(nbase, nlen)) fetch_next(nbase);
                         else stage_ok = false;
                     }
                 }
             }
-            if (item < n_items) item_range(item, w, item_end, npc);
+            if (item < n_items) {
+                w = item * chunk;
+                item_end = min(sg.n_windows, w + chunk);
+            }
         }
         if (STAGED && !stage_ok) break;  // the segment is skipped (the error word says so)
     }
-    if (EQ) settle();
 
     stamp(wave, 2);
     stamp_val(wave, 6, ((uint64_t)si << 32) | ((uint64_t)g << 16) | j);

@@ -34,10 +34,6 @@ extern "C" {
 /* Sets the hooks (an OR of the flags above); returns the previous value. */
 uint32_t ac_testing_stage_hooks(uint32_t flags);
 
-/* (window, candidate group) pairs the last count launch on ctx counted as two pieces of text (the
- * launch tail of equal-window launches); -1 if ctx is NULL. */
-int64_t ac_testing_last_pieces(const ac_ctx* ctx);
-
 
 #ifdef __cplusplus
 }

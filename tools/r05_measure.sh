@@ -67,7 +67,9 @@ pieces)  # kernel and stage A/B of the launch tail's pieces against variants
     run kcfg3_$v 300 env $L python3 tools/kernel_sweep.py --sn 100000 --lim 2000 --launches 30 --warmup 10
     run kcfg5_$v 300 env $L python3 tools/kernel_sweep.py --sn 100000 --lim 1000 --k 22 --sl 150 --launches 30 --warmup 10
     run stage_$v 200 env $L $B
-  done ;;
+  done
+  run stage_cfg5_early 200 python3 bench.py --config cfg5 --steps 20 --warmup 5 $BQ --no-kernel-leg
+  run stage_cfg5_dma 200 env AC_STAGE_EARLY=0 python3 bench.py --config cfg5 --steps 20 --warmup 5 $BQ --no-kernel-leg ;;
 sweep)  # kernel time against windows per wave (sample size), default item sizes and forced 2 / 4 windows per item
   for v in main chunk2 chunk4; do
     L=$([ $v = main ] && echo "" || echo "APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so")
@@ -94,5 +96,20 @@ pmc)
   ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 90 rocprofv3 --kernel-trace --stats -d "$OUT/trace_cfg2" -o run -- \
     python3 "$GRAFT_REPO_ROOT/tools/kernel_run.py" --config cfg2 --launches 50 --warmup 150 ) > "$OUT/trace_cfg2.log" 2>&1 || exit 4
   echo "== trace ok" | tee -a "$OUT/summary.log" ;;
+tail)  # late claims in the launch tail x pieces: tests of the new default, then cfg2 kernel A/B, cfg3 / cfg5
+  run tests_tail 600 $PYT -m gpu tests/test_gpu_pieces.py tests/test_gpu_parity.py tests/test_gpu_bench_path.py
+  for rep in 1 2 3; do
+    for v in main latenop nopieces piecesonly; do
+      L=$([ $v = main ] && echo "" || echo "APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so")
+      run ksweep_${v}_$rep 300 env $L python3 tools/kernel_sweep.py --sn 10000 --launches 300
+    done
+  done
+  for v in main latenop nopieces; do
+    L=$([ $v = main ] && echo "" || echo "APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so")
+    run kcfg3_$v 300 env $L python3 tools/kernel_sweep.py --sn 100000 --lim 2000 --launches 30 --warmup 10
+  done ;;
+stamps2)  # per-wave timelines: the default and the round-4 item order
+  run stamps_main 120 env APPROX_COUNTER_AMD_LIB=build/var/stamps/libapprox_counter_amd.so python3 tools/stamps.py
+  run stamps_nop 120 env APPROX_COUNTER_AMD_LIB=build/var/stamps_nop/libapprox_counter_amd.so python3 tools/stamps.py ;;
 esac
 done

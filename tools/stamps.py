@@ -107,6 +107,7 @@ def main():
     if n <= (1 << 15):
         ends = (win - t0) / 100.0
         per_n = {}
+        by_t = {}  # 10-us bins of the window's start: (durations with 4 waves resident)
         tot_windows = np.zeros(keys.size)
         for i in range(n):
             e = ends[i][(ends[i] > us[i, 1]) & (ends[i] <= us[i, 2] + 1e-9)]  # this launch's stamps only
@@ -118,13 +119,40 @@ def main():
             mid = (prev + e) / 2
             gi = np.clip(np.searchsorted(grid, mid), 0, grid.size - 1)
             nres = active[inv[i], gi].astype(int)
-            for d, r in zip(e - prev, nres):
+            for d, r, p0 in zip(e - prev, nres, prev):
                 per_n.setdefault(int(r), []).append(d)
+                if r == 4:
+                    by_t.setdefault(int(p0 // 10), []).append(d)
+        print("4-wave SIMD rate by the window's start time (10-us bins): " + " ".join(
+            f"{b * 10}:{4 / np.mean(v):.3f}" for b, v in sorted(by_t.items()) if len(v) > 200))
         print("window durations by waves resident on the SIMD (n: windows, mean us, SIMD windows/us):")
         for r in sorted(per_n):
             d = np.array(per_n[r])
             print(f"  n={r}: {d.size:6d} windows  mean {d.mean():6.2f} us  p50 {np.median(d):6.2f}  "
                   f"SIMD rate {r / d.mean():.3f} windows/us")
+        # per SIMD: its waves' exits in order (intra-SIMD spread: the last wave alone after the others)
+        ex = {}
+        for i in range(n):
+            ex.setdefault(inv[i], []).append(us[i, 3])
+        ex = {kk: sorted(v) for kk, v in ex.items()}
+        lone = np.array([v[-1] - v[-2] for v in ex.values() if len(v) > 1])
+        spread = np.array([v[-1] - v[0] for v in ex.values()])
+        print("per SIMD: last exit - second-to-last exit (the last wave alone)", pct(lone))
+        print("per SIMD: last exit - first exit                              ", pct(spread))
+        print("per SIMD: windows counted                                     ", pct(tot_windows))
+        cc = np.corrcoef(tot_windows, last)[0, 1]
+        print(f"corr(windows on the SIMD, SIMD end) = {cc:.2f}")
+        # per group: the last window start (~ the moment its queue ran dry) and its last exit
+        print("per group: last window start / last main end / last exit (us)")
+        for gv in np.unique(grp):
+            sel = np.nonzero(grp == gv)[0]
+            starts = []
+            for i in sel:
+                e = np.sort(ends[i][(ends[i] > us[i, 1]) & (ends[i] <= us[i, 2] + 1e-9)])
+                prev = np.concatenate([[us[i, 1]], e[:-1]])
+                if prev.size:
+                    starts.append(prev.max())
+            print(f"  {int(gv):#8x}  {max(starts):7.1f} {us[sel, 2].max():7.1f} {us[sel, 3].max():7.1f}")
         if 4 in per_n:
             r4 = 4 / np.mean(per_n[4])
             ideal = np.median(first) + np.median(us[:, 1] - us[:, 0]) + tot_windows.mean() / r4
