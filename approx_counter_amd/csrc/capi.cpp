@@ -73,10 +73,9 @@ struct ac_ctx {
         // counters of bank b used by the last launch on it (zeroed by the next launch)
         uint32_t* queue = nullptr;
         uint32_t qcap = 0, bank = 0, dirty[2] = {0, 0};
-        // count hand-off scratch: per-group sums and tickets (zero between launches)
-        uint32_t* acc = nullptr;
-        uint32_t* tickets = nullptr;
-        uint32_t acc_cap = 0, ticket_cap = 0;
+        // count hand-off scratch: per-slot arrivals and sums, (workgroups << 32) + sum (zero between launches)
+        uint64_t* acc = nullptr;
+        uint32_t acc_cap = 0;
         // staged launches: per-chunk "copied" flags (= the launch's generation once in device memory)
         uint32_t* stage_gen = nullptr;
         uint32_t stage_gen_cap = 0;
@@ -407,7 +406,7 @@ ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hi
         }
         d.queue_begin = qbegin;
         d.acc_begin = acc_slots;
-        d.ticket_begin = groups_total;
+        d.group_begin = groups_total;
         if (s.n_kmers && s.sample.n_windows) {
             qbegin += d.groups * d.subq;
             acc_slots += d.groups * cpw;
@@ -437,21 +436,11 @@ ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hi
         if (sc.acc) AC_HIP(ctx, hipFree(sc.acc));
         sc.acc = nullptr;
         sc.acc_cap = 0;
-        AC_HIP(ctx, hipMalloc(&sc.acc, sizeof(uint32_t) * acc_slots));
-        AC_HIP(ctx, hipMemsetAsync(sc.acc, 0, sizeof(uint32_t) * acc_slots, stream));
+        AC_HIP(ctx, hipMalloc(&sc.acc, sizeof(uint64_t) * acc_slots));
+        AC_HIP(ctx, hipMemsetAsync(sc.acc, 0, sizeof(uint64_t) * acc_slots, stream));
         sc.acc_cap = acc_slots;
     }
-    if (groups_total > sc.ticket_cap) {
-        if (sc.tickets) AC_HIP(ctx, hipFree(sc.tickets));
-        sc.tickets = nullptr;
-        sc.ticket_cap = 0;
-        const size_t bytes = sizeof(uint32_t) * AC_QUEUE_LINE * (size_t)groups_total;
-        AC_HIP(ctx, hipMalloc(&sc.tickets, bytes));
-        AC_HIP(ctx, hipMemsetAsync(sc.tickets, 0, bytes, stream));
-        sc.ticket_cap = groups_total;
-    }
     a.acc = sc.acc;
-    a.tickets = sc.tickets;
     a.err = err ? err : ctx->d_err;
     const uint32_t n_counters = qbegin;
     if (n_counters) wave = std::max<uint64_t>(resident, n_counters);
@@ -672,10 +661,9 @@ ac_status ac_create(ac_ctx** out, int device) {
             *p = nullptr;
             return false;
         };
-        constexpr uint32_t QCAP = 2048, ACC = 64 * 256, TICKETS = 64, CHUNKS = 1024;
+        constexpr uint32_t QCAP = 2048, ACC = 64 * 256, CHUNKS = 1024;
         if (zeroed((void**)&sc.queue, sizeof(uint32_t) * AC_QUEUE_LINE * 2 * QCAP)) sc.qcap = QCAP;
-        if (zeroed((void**)&sc.acc, sizeof(uint32_t) * ACC)) sc.acc_cap = ACC;
-        if (zeroed((void**)&sc.tickets, sizeof(uint32_t) * AC_QUEUE_LINE * TICKETS)) sc.ticket_cap = TICKETS;
+        if (zeroed((void**)&sc.acc, sizeof(uint64_t) * ACC)) sc.acc_cap = ACC;
         if (zeroed((void**)&sc.stage_gen, sizeof(uint32_t) * AC_QUEUE_LINE * CHUNKS)) sc.stage_gen_cap = CHUNKS;
     });
     *out = ctx;
@@ -695,7 +683,6 @@ void ac_destroy(ac_ctx* ctx) {
     for (auto& sc : ctx->sc) {
         if (sc.queue) (void)hipFree(sc.queue);
         if (sc.acc) (void)hipFree(sc.acc);
-        if (sc.tickets) (void)hipFree(sc.tickets);
         if (sc.stage_gen) (void)hipFree(sc.stage_gen);
     }
     for (hipStream_t ps : ctx->part_stream)

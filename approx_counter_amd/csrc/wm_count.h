@@ -86,7 +86,7 @@ struct SegDev {
     uint32_t queue_begin; // index of this segment's first sub-queue (groups x subq of them)
     uint32_t subq;        // sub-queues per candidate group (proportional to n_windows; a multiple of AC_WAVES_PER_BLOCK)
     uint32_t acc_begin;   // this segment's first slot in LaunchArgs::acc (groups x cands_per_wave slots)
-    uint32_t ticket_begin;  // this segment's first group ticket in LaunchArgs::tickets
+    uint32_t group_begin;  // launch-wide index of this segment's first candidate group (LaunchArgs::grp_err)
     uint32_t has_n;       // 0: the image holds no N (its N bitmap is not read; every word reads as 0)
     uint32_t ulen;        // AC_NO_ULEN, or every window has this length and window w starts at base
                           // w * ceil32(ulen) (start / length are not read)
@@ -115,13 +115,12 @@ struct LaunchArgs {
     uint32_t zero_count;
     uint32_t n_queues;  // sub-queues over all segments (a multiple of AC_WAVES_PER_BLOCK); wave w of
                         // workgroup b serves sub-queue (b % (n_queues / AC_WAVES_PER_BLOCK)) * AC_WAVES_PER_BLOCK + w
-    // Count hand-off: workgroups add their sums into `acc` and
-    // take a ticket of their candidate group; the group's last workgroup moves
-    // the group's sums to the segment's counts (stored, or added when
-    // `add_counts`) and zeroes its acc slots and ticket for the next launch, so
-    // a launch needs no memset of the counts.
-    uint32_t* acc;
-    uint32_t* tickets;  // one per AC_QUEUE_LINE u32
+    // Count hand-off: each workgroup adds (1 << 32) + its sum into every `acc` slot of
+    // its candidate group with one returning 64-bit atomic per slot; the workgroup whose add finds
+    // every other workgroup's arrival in the high half is the slot's last, writes the slot's total
+    // to the segment's counts (stored, or added when `add_counts`) and zeroes the slot for the next
+    // launch, so a launch needs no memset of the counts and no ticket round trip.
+    uint64_t* acc;
     uint32_t* err;      // AC_DEVERR_* bits, or-ed in by the kernel
     uint32_t add_counts;
     // Staged launch (nonzero): inputs copied in by the kernel once the host flags each segment in

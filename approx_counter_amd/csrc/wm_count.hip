@@ -1106,71 +1106,64 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
         stamp_val(wave, 5, gate_calls);
     }
 #endif
-    // The workgroup's waves sum their counts in LDS; one wave adds the sums to
-    // the group's slots in `acc`, so each slot takes 1/AC_WAVES_PER_BLOCK of the
-    // same-address atomics (they serialise at the L2: ~10 us of launch tail at
-    // cfg2 with one atomic per wave; profiles/r01_kernel_log.md).  Then the
-    // group's last workgroup (ticket) moves the sums to the counts.
+    // The workgroup's waves sum their counts in LDS; one wave adds the sums to the group's slots in
+    // `acc`, so each slot takes 1/AC_WAVES_PER_BLOCK of the same-address atomics (they serialise at
+    // the memory side: ~10 us of launch tail at cfg2 with one atomic per wave; profiles/r01_kernel_log.md).
+    // Each add is 64-bit, (1 << 32) + the sum: the returned word says how many workgroups of the group
+    // have added before this one, so the last to add -- per slot -- knows the total at once and moves it
+    // to the counts.  One device-scope round trip at the launch's end (round 4 had three: the adds, a
+    // group ticket taken after them, the slots read back and zeroed).  No fences: the arrival count and
+    // the sum change in one atomic.
 #pragma unroll
     for (int q = 0; q < Q; ++q)
         if (cnt[q]) __hip_atomic_fetch_add(&lds.cnt[q * 64 + lane], cnt[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    // (every wave's error-word atomics are performed before its workgroup's ticket: a staged
-    // launch's last group reads the word)
+    // (every wave's error-word atomics are performed before its workgroup's adds: the staged launch's
+    // last workgroup of a slot reads the word)
     if (STAGED) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (wib == 0) {
-        uint32_t* acc = a.acc + sg.acc_begin + g * (64u * Q);
-        // Returning atomics, their results consumed before the ticket: every add
-        // has been performed (device-coherent) before this workgroup's ticket.
-        // No release/acquire fence: at agent scope those write back the whole
-        // XCD L2 (measured: +28 us at cfg2).
-        uint32_t sink = 0;
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            const uint32_t v = lds.cnt[q * 64 + lane];
-            if (v) sink |= __hip_atomic_fetch_add(&acc[q * 64 + lane], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        asm volatile("" ::"v"(sink));
+        uint64_t* acc = a.acc + sg.acc_begin + g * (64u * Q);
         // Workgroups serving group g: those dealt to its subq / WPB block-queues.
         const uint32_t qb0 = (sg.queue_begin + g * sg.subq) / WAVES_PER_BLOCK, nq = sg.subq / WAVES_PER_BLOCK;
         uint32_t n_wg = 0;
         for (uint32_t i = 0; i < nq; ++i) n_wg += wgs_of(qb0 + i);
-        uint32_t* ticket = a.tickets + (uint64_t)(sg.ticket_begin + g) * AC_QUEUE_LINE;
-        uint32_t t = 0;
-        if (lane == 0) t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        t = __builtin_amdgcn_readfirstlane(t);
-        if (t == n_wg - 1u) {  // every other workgroup of the group has added its sums
+        uint32_t mine[Q];
+        uint64_t old[Q];
 #pragma unroll
-            for (int q = 0; q < Q; ++q) {
-                const uint32_t v = __hip_atomic_exchange(&acc[q * 64 + lane], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (cand[q] < sg.n_kmers) {
-                    if (a.add_counts) {
-                        if (v) atomicAdd(&sg.counts[cand[q]], v);
-                    } else if (STAGED && a.tag) {  // host memory, each count tagged with the launch's generation
-                        __hip_atomic_store((uint64_t*)sg.counts + cand[q], ((uint64_t)a.gen << 32) | v, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_SYSTEM);
-                    } else {  // (device memory: read after the stream has completed)
-                        sg.counts[cand[q]] = v;
-                    }
+        for (int q = 0; q < Q; ++q) {
+            mine[q] = lds.cnt[q * 64 + lane];
+            old[q] = __hip_atomic_fetch_add(&acc[q * 64 + lane], (1ull << 32) | mine[q], __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+        }
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            if ((uint32_t)(old[q] >> 32) != n_wg - 1u) continue;  // not the slot's last workgroup
+            const uint32_t v = (uint32_t)old[q] + mine[q];
+            __hip_atomic_store(&acc[q * 64 + lane], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (cand[q] < sg.n_kmers) {
+                if (a.add_counts) {
+                    if (v) atomicAdd(&sg.counts[cand[q]], v);
+                } else if (STAGED && a.tag) {  // host memory, each count tagged with the launch's generation
+                    __hip_atomic_store((uint64_t*)sg.counts + cand[q], ((uint64_t)a.gen << 32) | v, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_SYSTEM);
+                } else {  // (device memory: read after the stream has completed)
+                    sg.counts[cand[q]] = v;
                 }
             }
-            if (lane == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (STAGED) {
-                // The group's error snapshot holds every bit its waves set (each wave's atomics were
-                // performed before its workgroup's ticket); all groups' snapshots together hold the
-                // launch's.  Tagged completion (synchronous calls): the host waits until every count
-                // and every group's word carries this launch's generation, so no completion word, no
-                // wait for the counts' stores and no launch-wide counter sit on the path to the host.
-                // Submits (counts in device memory): the bits go to the context's word (ac_check).
-                uint32_t e = 0;
-                if (lane == 0) e = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (a.tag) {
-                    if (lane == 0)
-                        __hip_atomic_store(a.grp_err + sg.ticket_begin + g, ((uint64_t)a.gen << 32) | e,
-                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                } else if (lane == 0 && e && a.err_out) {
+            if (STAGED && q == 0 && lane == 0) {
+                // The group's error snapshot, by slot (0, lane 0)'s last workgroup: every workgroup's waves
+                // performed their error atomics before that workgroup's add to the slot, so the word holds
+                // every bit the group set; all groups' snapshots together hold the launch's.  Tagged
+                // completion (synchronous calls): the host waits until every count and every group's word
+                // carries this launch's generation, so no completion word, no wait for the counts' stores
+                // and no launch-wide counter sit on the path to the host.  Submits (counts in device
+                // memory): the bits go to the context's word (ac_check).
+                const uint32_t e = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (a.tag)
+                    __hip_atomic_store(a.grp_err + sg.group_begin + g, ((uint64_t)a.gen << 32) | e, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_SYSTEM);
+                else if (e && a.err_out)
                     atomicOr(a.err_out, e);
-                }
             }
         }
     }

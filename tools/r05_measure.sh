@@ -111,5 +111,19 @@ tail)  # late claims in the launch tail x pieces: tests of the new default, then
 stamps2)  # per-wave timelines: the default and the round-4 item order
   run stamps_main 120 env APPROX_COUNTER_AMD_LIB=build/var/stamps/libapprox_counter_amd.so python3 tools/stamps.py
   run stamps_nop 120 env APPROX_COUNTER_AMD_LIB=build/var/stamps_nop/libapprox_counter_amd.so python3 tools/stamps.py ;;
+handoff)  # the one-atomic count hand-off: tests, then cfg2 kernel / stage A/B against the previous commit
+  run tests_handoff 900 $PYT -m gpu tests/test_gpu_parity.py tests/test_gpu_bench_path.py tests/test_gpu_jobs.py tests/test_gpu_scale.py
+  for rep in 1 2 3; do
+    for v in main prev; do
+      L=$([ $v = main ] && echo "" || echo "APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so")
+      run ksweep_${v}_$rep 300 env $L python3 tools/kernel_sweep.py --sn 10000 --launches 300
+    done
+  done
+  for rep in 1 2; do
+    for v in main prev; do
+      L=$([ $v = main ] && echo "" || echo "APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so")
+      run stage_${v}_$rep 200 env $L $B
+    done
+  done ;;
 esac
 done
