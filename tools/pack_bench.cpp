@@ -3,6 +3,8 @@
 // (tasks in job order, the caller helping), timing when job 0 and job 1 are complete.
 //   g++ -O3 -std=c++17 -pthread -Iapprox_counter_amd/csrc tools/pack_bench.cpp \
 //       approx_counter_amd/csrc/host_pack.cpp -o /tmp/pack_bench && /tmp/pack_bench [n] [iters] [per] [records]
+// AC_PACK_CPUS=<cpulist> pins the pool to those CPUs (a rank's share of the host, as ac_plan_host_cpus
+// plans it; tools/pack8.py runs eight such processes at once); AC_HOST_THREADS sizes the pool.
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -23,6 +25,11 @@ int main(int argc, char** argv) {
     const uint32_t per_arg = argc > 3 ? (uint32_t)std::atoi(argv[3]) : 0;
     // records = 1: the stage's equal-window form (inline N records, no descriptors), 0.1 % N bases
     const bool records = argc > 4 ? std::atoi(argv[4]) != 0 : true;
+    if (const char* c = std::getenv("AC_PACK_CPUS")) {
+        acamd::HostPlan plan;
+        plan.cpus = acamd::parse_cpulist(c);
+        (void)acamd::set_host_plan(plan);
+    }
     acamd::WorkPool& pool = acamd::host_pool();
     std::mt19937 rng(1);
     struct Job {
@@ -90,5 +97,7 @@ int main(int argc, char** argv) {
                 n, (int)records);
     std::printf("job 0 packed: p10 %.1f p50 %.1f p90 %.1f max %.1f us\n", q(d0, .1), q(d0, .5), q(d0, .9), d0.back());
     std::printf("both packed:  p10 %.1f p50 %.1f p90 %.1f max %.1f us\n", q(d1, .1), q(d1, .5), q(d1, .9), d1.back());
+    std::printf("{\"participants\": %u, \"n\": %u, \"both_p50_us\": %.2f, \"both_p90_us\": %.2f, \"both_max_us\": %.2f, "
+                "\"job0_p50_us\": %.2f}\n", pool.size(), n, q(d1, .5), q(d1, .9), d1.back(), q(d0, .5));
     return 0;
 }

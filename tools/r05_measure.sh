@@ -125,5 +125,39 @@ handoff)  # the one-atomic count hand-off: tests, then cfg2 kernel / stage A/B a
       run stage_${v}_$rep 200 env $L $B
     done
   done ;;
+pack8)  # eight concurrent pack-only processes on their planned CPU shares (the 8-GPU host side)
+  run pack8 600 python3 tools/pack8.py
+  run pack8_again 600 python3 tools/pack8.py ;;
+shard)  # one rank's 1/8 cfg4 shard alone, pool at 2 (a 16-CPU quota split 8 ways) and at 16 participants
+  for t in 2 16; do
+    run shard_t$t 300 env AC_HOST_THREADS=$t AC_STAGE_TRACE=1 python3 bench.py --config cfg4 --shard 0/8 --steps 30 --warmup 5 $BQ
+  done ;;
+prio)  # raised priority for the holders of the last round's items: tests, kernel and stage A/B
+  run tests_prio 900 $PYT -m gpu tests/test_gpu_parity.py tests/test_gpu_bench_path.py
+  for rep in 1 2 3; do
+    for v in main noprio prio2; do
+      L=$([ $v = main ] && echo "" || echo "APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so")
+      run ksweep_${v}_$rep 300 env $L python3 tools/kernel_sweep.py --sn 10000 --launches 300
+    done
+  done
+  for rep in 1 2; do
+    for v in main noprio; do
+      L=$([ $v = main ] && echo "" || echo "APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so")
+      run stage_${v}_$rep 200 env $L $B
+    done
+  done
+  for v in main noprio; do
+    L=$([ $v = main ] && echo "" || echo "APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so")
+    run kcfg3_$v 300 env $L python3 tools/kernel_sweep.py --sn 100000 --lim 2000 --launches 30 --warmup 10
+  done ;;
+p1)  # k = 22 (P = 1): the early launch's staged kernel with one lane word (default) or two, and the DMA path
+  for rep in 1 2; do
+    run cfg5_stage_main_$rep 200 python3 bench.py --config cfg5 --steps 20 --warmup 5 $BQ --no-kernel-leg
+    run cfg5_stage_words2_$rep 200 env APPROX_COUNTER_AMD_LIB=build/var/words2/libapprox_counter_amd.so python3 bench.py --config cfg5 --steps 20 --warmup 5 $BQ --no-kernel-leg
+    run cfg5_stage_dma_$rep 200 env AC_STAGE_EARLY=0 python3 bench.py --config cfg5 --steps 20 --warmup 5 $BQ --no-kernel-leg
+  done
+  run kcfg5_main 300 python3 tools/kernel_sweep.py --sn 100000 --lim 1000 --k 22 --sl 150 --launches 30 --warmup 10
+  run kcfg5_words2 300 env APPROX_COUNTER_AMD_LIB=build/var/words2/libapprox_counter_amd.so python3 tools/kernel_sweep.py --sn 100000 --lim 1000 --k 22 --sl 150 --launches 30 --warmup 10
+  run tests_words2 600 env APPROX_COUNTER_AMD_LIB=build/var/words2/libapprox_counter_amd.so $PYT -m gpu tests/test_gpu_parity.py -k "every_k or equal or edge" ;;
 esac
 done
