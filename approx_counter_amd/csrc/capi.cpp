@@ -88,7 +88,7 @@ struct ac_ctx {
     hipEvent_t sub_ev[AC_STAGE_MAX_PARTS] = {};
     hipEvent_t sub_zero_ev = nullptr;
     // resident waves of the count kernel per pattern pack P (0 = not queried yet)
-    uint32_t resident[AC_MAX_PACK + 1] = {0, 0, 0, 0, 0};
+    uint32_t resident[2][AC_MAX_PACK + 1] = {};  // [staged][P]
     // last launch geometry
     uint64_t last_waves = 0;
     uint32_t last_wpw = 0, last_groups = 0;
@@ -126,7 +126,7 @@ struct ac_ctx {
     // -- the CLI's one approximate count per run -- does not pay for it; it overlaps the caller's FASTA
     // parsing and exact count instead.
     std::thread warm;
-    uint32_t warm_resident[AC_MAX_PACK + 1] = {0, 0, 0, 0, 0};
+    uint32_t warm_resident[2][AC_MAX_PACK + 1] = {};
 };
 
 namespace {
@@ -314,8 +314,9 @@ uint32_t stage_copiers(uint64_t tickets, uint64_t /*resident_waves*/) {
 void ensure_warm(ac_ctx* ctx) {
     if (!ctx->warm.joinable()) return;
     ctx->warm.join();
-    for (uint32_t P = 1; P <= AC_MAX_PACK; ++P)
-        if (!ctx->resident[P]) ctx->resident[P] = ctx->warm_resident[P];
+    for (int st = 0; st < 2; ++st)
+        for (uint32_t P = 1; P <= AC_MAX_PACK; ++P)
+            if (!ctx->resident[st][P]) ctx->resident[st][P] = ctx->warm_resident[st][P];
 }
 
 ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hipStream_t stream,
@@ -328,7 +329,8 @@ ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hi
     if (n > AC_MAX_SEGS) return fail(ctx, AC_ERR_INVALID, "too many segments in one launch (max 4)");
     if (n && !segs) return fail(ctx, AC_ERR_INVALID, "segments is NULL");
     const uint32_t P = acamd::pack_factor(k);
-    const uint32_t cpw = acamd::cands_per_wave(P);
+    const bool staged = stage != nullptr;
+    const uint32_t cpw = acamd::cands_per_wave(P, staged);
     acamd::LaunchArgs a;
     std::memset(&a, 0, sizeof a);
     a.n_segs = n;
@@ -357,10 +359,11 @@ ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hi
     // to its windows, so every sub-queue holds about the same work.  Workgroups
     // of AC_WAVES_PER_BLOCK waves are dealt round-robin over blocks of that many
     // consecutive sub-queues (one candidate group each).
-    if (!ctx->resident[P]) AC_HIP(ctx, acamd::resident_waves(P, ctx->cu_count, &ctx->resident[P]));
-    const uint64_t resident = wave_cap ? std::max<uint64_t>(AC_WAVES_PER_BLOCK, std::min<uint64_t>(wave_cap, ctx->resident[P]) /
+    uint32_t& res_p = ctx->resident[staged][P];
+    if (!res_p) AC_HIP(ctx, acamd::resident_waves(P, staged, ctx->cu_count, &res_p));
+    const uint64_t resident = wave_cap ? std::max<uint64_t>(AC_WAVES_PER_BLOCK, std::min<uint64_t>(wave_cap, res_p) /
                                                                   AC_WAVES_PER_BLOCK * AC_WAVES_PER_BLOCK)
-                                       : ctx->resident[P];
+                                       : res_p;
     const uint32_t wpw = (uint32_t)std::max<uint64_t>(1, (items + resident - 1) / resident);
 #ifdef AC_FORCE_CHUNK  // A/B builds (tools/variants.sh): fixed item size
     const uint32_t chunk = AC_FORCE_CHUNK;
@@ -652,7 +655,8 @@ ac_status ac_create(ac_ctx** out, int device) {
     ctx->warm = std::thread([ctx] {
         if (hipSetDevice(ctx->device) != hipSuccess) return;
         for (uint32_t P = 1; P <= AC_MAX_PACK; ++P)
-            (void)acamd::resident_waves(P, ctx->cu_count, &ctx->warm_resident[P]);
+            for (int st = 0; st < 2; ++st)
+                (void)acamd::resident_waves(P, st != 0, ctx->cu_count, &ctx->warm_resident[st][P]);
         ac_ctx::Scratch& sc = ctx->sc[0];
         auto zeroed = [](void** p, size_t bytes) {
             if (hipMalloc(p, bytes) != hipSuccess) return false;
@@ -1715,7 +1719,7 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
     p.off_gerr = off;
     p.n_gerr = 0;
     if (p.tag) {
-        const uint32_t cpw = acamd::cands_per_wave(acamd::pack_factor(k));
+        const uint32_t cpw = acamd::cands_per_wave(acamd::pack_factor(k), true);  // (tagged: a staged launch)
         for (uint32_t j = 0; j < p.n; ++j)
             if (jobs[j].n_kmers && p.hi[j] > p.lo[j]) p.n_gerr += (jobs[j].n_kmers + cpw - 1) / cpw;
         off = align256(off + sizeof(uint64_t) * p.n_gerr);
@@ -1754,10 +1758,10 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
         }
         ensure_warm(ctx);
         const uint32_t P = acamd::pack_factor(k);
-        if (!ctx->resident[P]) AC_HIP(ctx, acamd::resident_waves(P, ctx->cu_count, &ctx->resident[P]));
+        if (!ctx->resident[1][P]) AC_HIP(ctx, acamd::resident_waves(P, true, ctx->cu_count, &ctx->resident[1][P]));
         uint64_t tickets = 0;
         for (uint32_t j = 0; j < p.n; ++j) tickets += p.chunks[j] ? p.chunks[j] + 1u : 0u;
-        p.copiers = stage_copiers(tickets, ctx->resident[P]);
+        p.copiers = stage_copiers(tickets, ctx->resident[1][P]);
     }
     // The slot: wait until the launch that last read it has finished, grow it.
     ac_ctx::Slot& sl = ctx->slot[p.slot];
@@ -2086,8 +2090,8 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
     uint64_t cap = 0;
     if (wave_div > 1) {
         const uint32_t P = acamd::pack_factor(k);
-        if (!ctx->resident[P]) AC_HIP(ctx, acamd::resident_waves(P, ctx->cu_count, &ctx->resident[P]));
-        cap = ctx->resident[P] / wave_div;
+        if (!ctx->resident[0][P]) AC_HIP(ctx, acamd::resident_waves(P, false, ctx->cu_count, &ctx->resident[0][P]));
+        cap = ctx->resident[0][P] / wave_div;
     }
     if (ac_status st = launch(ctx, k, segs, p.n, stream, zero, d_counts ? nullptr : (uint32_t*)(hd + p.off_err),
                               p.scratch, cap, no_n, ulen, nullptr, nrec))

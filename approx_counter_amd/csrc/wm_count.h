@@ -17,11 +17,18 @@
 // Two words for P = 2 (k = 11-16): cfg2 kernel 107-108 -> 102-103 us, cfg3 equal; one word for
 // P = 1, where two were 0.8 % slower at cfg5 (profiles/r03_dual_ab.log).  P = 3-4 (k <= 10) are
 // unmeasured and keep one.  -DAC_WORDS=1 / 2 forces one choice for every P (A/B builds).
-constexpr int words_for(int P) {
+// Round 5: the early launch's staged kernel takes two words for P = 1 as well -- with one word (8 resident
+// waves, 78 SGPRs per wave) its staging state spilled 140+ SGPRs inside the count loop, with two (4
+// waves, 106 SGPRs) 52: cfg5 stage 4.568-4.570 vs 4.669-4.687 ms, same box (profiles/r05_m12), while
+// the plain P = 1 kernel stays at one word (4.248 vs 4.362 ms on resident input).
+#ifndef AC_P1_STAGED_WORDS
+#define AC_P1_STAGED_WORDS 2
+#endif
+constexpr int words_for(int P, bool staged = false) {
 #ifdef AC_WORDS
-    return (void)P, AC_WORDS;
+    return (void)P, (void)staged, AC_WORDS;
 #else
-    return P == 2 ? 2 : 1;
+    return P == 2 ? 2 : (P == 1 && staged) ? AC_P1_STAGED_WORDS : 1;
 #endif
 }
 // resident count-kernel waves per SIMD, set by the LDS allocation (<= 64 VGPRs with one word)
@@ -149,10 +156,11 @@ struct LaunchArgs {
 };
 
 inline uint32_t pack_factor(uint32_t k) { return (32u / k) < AC_MAX_PACK ? (32u / k) : AC_MAX_PACK; }
-inline uint32_t cands_per_wave(uint32_t P) { return 64u * P * (uint32_t)words_for((int)P); }
+// candidates per wave of the plain (staged = false) or the early launch's staged kernel
+inline uint32_t cands_per_wave(uint32_t P, bool staged) { return 64u * P * (uint32_t)words_for((int)P, staged); }
 
 // Waves of the count kernel for pattern pack P that fit on the device at once.
-hipError_t resident_waves(uint32_t P, int cu_count, uint32_t* waves);
+hipError_t resident_waves(uint32_t P, bool staged, int cu_count, uint32_t* waves);
 
 #ifdef AC_STAMPS
 hipError_t debug_stamps(void* host, size_t bytes);

@@ -590,8 +590,8 @@ __device__ __forceinline__ void tid_tail(TidNfa* s, uint32_t code, uint32_t nm, 
 // fit the image): window places by arithmetic, no descriptor arrays or per-window range checks held
 // in registers (the staged kernel spilled SGPRs inside the count loop without this).
 template <int P, bool STAGED, bool EQ>
-__device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_for(P)>& lds) {
-    constexpr int W = words_for(P);
+__device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_for(P, STAGED)>& lds) {
+    constexpr int W = words_for(P, STAGED);
     const uint32_t lane = threadIdx.x & 63u;
     // Workgroup b serves one block-queue (all its waves on one candidate
     // group); its waves take the block-queue's AC_WAVES_PER_BLOCK sub-queues.
@@ -1173,24 +1173,24 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
 }  // namespace
 
 template <int P, bool STAGED, bool EQ>
-__global__ __launch_bounds__(64 * WAVES_PER_BLOCK, waves_per_simd(words_for(P))) void wm2_count_kernel(LaunchArgs a) {
+__global__ __launch_bounds__(64 * WAVES_PER_BLOCK, waves_per_simd(words_for(P, STAGED))) void wm2_count_kernel(LaunchArgs a) {
     // The LDS allocation also caps residency at waves_per_simd waves per SIMD
     // (one word: 8, faster than 6 or 10, profiles/r01_kernel_log.md; two words: 4).
-    constexpr int W = words_for(P);
+    constexpr int W = words_for(P, STAGED);
     constexpr int kBlocksPerCu = 4 * waves_per_simd(W) / WAVES_PER_BLOCK;
     __shared__ BlockLds<W> lds[(160 * 1024 / kBlocksPerCu) / sizeof(BlockLds<W>)];
     count_body<P, STAGED, EQ>(a, lds[0]);
 }
 
 namespace {
-template <int P>
+template <int P, bool STAGED>
 hipError_t occupancy(int cu_count, uint32_t* waves) {
     int blocks = 0;
     hipError_t e =
-        // (queried on the equal-window kernel, the one the bench's kernel leg and the CLI launch: the
-        // query loads the kernel's code, and that load then is not paid again at its first launch --
-        // every instantiation has the same LDS allocation, so the same residency)
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, wm2_count_kernel<P, false, true>, 64 * WAVES_PER_BLOCK, 0);
+        // (queried on the equal-window kernel, the one the bench's kernel leg, the CLI and the stage launch:
+        // the query loads the kernel's code, and that load then is not paid again at its first launch --
+        // the instantiations of one word count have the same LDS allocation, so the same residency)
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, wm2_count_kernel<P, STAGED, true>, 64 * WAVES_PER_BLOCK, 0);
     if (e != hipSuccess) return e;
     if (blocks < 1) blocks = 1;
     *waves = (uint32_t)blocks * WAVES_PER_BLOCK * (uint32_t)cu_count;
@@ -1213,14 +1213,17 @@ hipError_t debug_stamps(void* host, size_t bytes) {
 }
 #endif
 
-hipError_t resident_waves(uint32_t P, int cu_count, uint32_t* waves) {
+hipError_t resident_waves(uint32_t P, bool staged, int cu_count, uint32_t* waves) {
+#define AC_OCC(PP) \
+    case PP: return staged ? occupancy<PP, true>(cu_count, waves) : occupancy<PP, false>(cu_count, waves);
     switch (P) {
-        case 1: return occupancy<1>(cu_count, waves);
-        case 2: return occupancy<2>(cu_count, waves);
-        case 3: return occupancy<3>(cu_count, waves);
-        case 4: return occupancy<4>(cu_count, waves);
+        AC_OCC(1)
+        AC_OCC(2)
+        AC_OCC(3)
+        AC_OCC(4)
         default: return hipErrorInvalidValue;
     }
+#undef AC_OCC
 }
 
 hipError_t launch_wm2_count(const LaunchArgs& args, hipStream_t stream) {

@@ -93,6 +93,10 @@ def parse():
     ap.add_argument("--shard", metavar="R/N",
                     help="rehearsal on one GPU: time rank R's shard of an N-rank strong-scaling run alone "
                          "(the projection basis for N GPUs; never the default line)")
+    ap.add_argument("--step-form", choices=("auto", "submit"), default="auto",
+                    help="submit: at N = 1 run the N > 1 step form (ac_error_count_jobs_submit, the library's RCCL "
+                         "all-reduce on a one-rank communicator, counts copied back, stream synchronised) -- a "
+                         "rehearsal of the multi-GPU step's own costs, never the default line")
     ap.add_argument("--kernel-launches", type=int, default=100,
                     help="launches of the kernel-only leg (at least --steps); it runs before the stage, so the "
                          "device is at its sustained clock when the stage's warmup starts (DESIGN.md 4c)")
@@ -384,10 +388,12 @@ def main():
     # (ac_comm_init, id from rank 0 over the process group); if it cannot be set up, torch's
     # RCCL process group does the same all-reduce and the line says so.
     allreduce_by = None
-    if world > 1 and backend == "nccl":
+    submit_form = world > 1 or args.step_form == "submit"
+    if submit_form and backend == "nccl":
         try:
             uid = [counter.comm_unique_id() if rank == 0 else None]
-            dist.broadcast_object_list(uid, src=0)
+            if world > 1:
+                dist.broadcast_object_list(uid, src=0)
             counter.comm_init(world, rank, uid[0])
             allreduce_by = "library (ac_allreduce_counts, RCCL)"
         except Exception as exc:  # noqa: BLE001 -- reported on the line, the run continues on torch's RCCL
@@ -397,7 +403,7 @@ def main():
         allreduce_by = f"torch.distributed {backend} on host copies (rehearsal)"
 
     # ---- the stage (value): host Dna5 buffers -> host counts ---------------------------------
-    if world == 1:
+    if not submit_form:
         def step():
             counter.count_jobs(args.k, jobs)  # pack, one fused launch, counts back (synchronous)
     else:
@@ -479,6 +485,9 @@ def main():
                        if world > 1 else "1 GPU"},
             **({"allreduce": allreduce_by} if allreduce_by else {}),
         }
+        if world == 1 and submit_form:
+            out["step_form"] = ("submit: the N > 1 step (ac_error_count_jobs_submit -> RCCL all-reduce on a one-rank "
+                                "communicator -> counts D2H -> stream sync) on one GPU: a rehearsal of its costs")
         if world == 1:  # each step is synchronous at N = 1: its own duration
             d = np.diff(np.array([t0] + marks)) * 1e3
             out["step_ms"] = {"min": float(d.min()), "p50": float(np.median(d)), "p99": float(np.percentile(d, 99)),

@@ -158,6 +158,18 @@ p1)  # k = 22 (P = 1): the early launch's staged kernel with one lane word (defa
   done
   run kcfg5_main 300 python3 tools/kernel_sweep.py --sn 100000 --lim 1000 --k 22 --sl 150 --launches 30 --warmup 10
   run kcfg5_words2 300 env APPROX_COUNTER_AMD_LIB=build/var/words2/libapprox_counter_amd.so python3 tools/kernel_sweep.py --sn 100000 --lim 1000 --k 22 --sl 150 --launches 30 --warmup 10
+  for rep in 1 2; do
+    run cfg2_sync_$rep 200 $B
+    run cfg2_submitform_$rep 200 $B --step-form submit
+  done
   run tests_words2 600 env APPROX_COUNTER_AMD_LIB=build/var/words2/libapprox_counter_amd.so $PYT -m gpu tests/test_gpu_parity.py -k "every_k or equal or edge" ;;
+p1b)  # the staged P = 1 kernel on two words (the new default): tests, cfg5 stage; the N > 1 step form
+  run tests_p1b 900 $PYT -m gpu tests/test_gpu_jobs.py tests/test_gpu_scale.py tests/test_gpu_bench_path.py
+  for rep in 1 2; do
+    run cfg5_stage_main_$rep 200 python3 bench.py --config cfg5 --steps 20 --warmup 5 $BQ --no-kernel-leg
+    run cfg5_stage_dma_$rep 200 env AC_STAGE_EARLY=0 python3 bench.py --config cfg5 --steps 20 --warmup 5 $BQ --no-kernel-leg
+    run cfg2_sync_$rep 200 $B
+    run cfg2_submitform_$rep 200 $B --step-form submit
+  done ;;
 esac
 done
