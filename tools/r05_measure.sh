@@ -171,5 +171,18 @@ p1b)  # the staged P = 1 kernel on two words (the new default): tests, cfg5 stag
     run cfg2_sync_$rep 200 $B
     run cfg2_submitform_$rep 200 $B --step-form submit
   done ;;
+chunks)  # windows per claim at cfg2: 1 (default) / 2 / 4, kernel x3 and stage x2
+  for rep in 1 2 3; do
+    for v in main chunk2 chunk4; do
+      L=$([ $v = main ] && echo "" || echo "APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so")
+      run ksweep_${v}_$rep 300 env $L python3 tools/kernel_sweep.py --sn 10000 --launches 300
+    done
+  done
+  for rep in 1 2; do
+    for v in main chunk2 chunk4; do
+      L=$([ $v = main ] && echo "" || echo "APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so")
+      run stage_${v}_$rep 200 env $L $B
+    done
+  done ;;
 esac
 done
