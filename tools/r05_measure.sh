@@ -184,5 +184,16 @@ chunks)  # windows per claim at cfg2: 1 (default) / 2 / 4, kernel x3 and stage x
       run stage_${v}_$rep 200 env $L $B
     done
   done ;;
+final)  # what the driver runs at round end: the GPU suite, smoke, the default bench line
+  run suite 1100 $PYT -m gpu tests
+  run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"
+  run bench_default 600 python3 bench.py ;;
+stepform)  # the N > 1 step's way back, rehearsed on one GPU (one-rank RCCL communicator)
+  for rep in 1 2 3; do
+    run sf_sync_$rep 200 $B
+    run sf_submit_$rep 200 $B --step-form submit
+    run sf_host0_$rep 200 $B --step-form submit-host0
+    run sf_host1_$rep 200 $B --step-form submit-host1
+  done ;;
 esac
 done
