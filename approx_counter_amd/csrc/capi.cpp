@@ -291,7 +291,7 @@ struct StageLaunch {
     uint32_t* err_out = nullptr;  // device word the launch's error bits are also or-ed into (submits: ac_check)
     uint32_t tag = 0;              // tagged completion (wm_count.h LaunchArgs::tag)
     uint64_t* grp_err = nullptr;   // its per-group error words (device-visible pinned address)
-    uint32_t copiers = 0;          // copier workgroups (wm_count.h LaunchArgs::copier_wgs; 0: every workgroup)
+    uint32_t copiers = 0;          // copier workgroups (wm_count.h LaunchArgs::copier_wgs; 0: nothing to stage)
 };
 
 // Who stages a staged launch (wm_count.h LaunchArgs::copier_wgs): a few copier workgroups stage
@@ -300,15 +300,9 @@ struct StageLaunch {
 // such wave held its workgroup's other three waves at the table barrier until its chunk was in (the
 // p90 workgroup started counting ~30 us into a cfg2 launch, profiles/r04_m1/stamps_staged.log), and a
 // large call's chunks arrive over the whole packing time.  Copier workgroups at cfg2: stage p50
-// 0.1143-0.1146 vs 0.1189-0.1193 ms (same box, profiles/r04_m7/ab_table.txt).  AC_COPIER_MIN_TICKETS
-// keeps the round-3 scheme up to that many tickets (A/B runs).
-uint32_t stage_copiers(uint64_t tickets, uint64_t /*resident_waves*/) {
-    static const int64_t min_tickets = [] {
-        const char* e = std::getenv("AC_COPIER_MIN_TICKETS");
-        return e ? (int64_t)std::atoll(e) : (int64_t)0;
-    }();
-    return tickets > (uint64_t)min_tickets ? stage_copier_wgs() : 0u;
-}
+// 0.1143-0.1146 vs 0.1189-0.1193 ms (same box, profiles/r04_m7/ab_table.txt); the round-3 scheme was
+// removed in round 5.
+uint32_t stage_copiers(uint64_t tickets) { return tickets ? stage_copier_wgs() : 0u; }
 
 // Joins ac_create's warm-up thread (once) and takes the resident-wave counts it queried.
 void ensure_warm(ac_ctx* ctx) {
@@ -1761,7 +1755,7 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
         if (!ctx->resident[1][P]) AC_HIP(ctx, acamd::resident_waves(P, true, ctx->cu_count, &ctx->resident[1][P]));
         uint64_t tickets = 0;
         for (uint32_t j = 0; j < p.n; ++j) tickets += p.chunks[j] ? p.chunks[j] + 1u : 0u;
-        p.copiers = stage_copiers(tickets, ctx->resident[1][P]);
+        p.copiers = stage_copiers(tickets);
     }
     // The slot: wait until the launch that last read it has finished, grow it.
     ac_ctx::Slot& sl = ctx->slot[p.slot];

@@ -143,11 +143,9 @@ struct LaunchArgs {
     // and each candidate group stores its error snapshot (generation << 32 | bits) at grp_err[ticket index]
     uint32_t tag;
     uint64_t* grp_err;
-    // staged: 0 = wave 0 of every workgroup claims staging tickets of its own segment before it
-    // counts (small calls: the tickets run out after a few hundred workgroups); n > 0 = only
-    // workgroups 0 .. n-1 stage, every wave of them, every segment in order, then they count like
-    // the rest (large calls: thousands of chunks arrive over the whole packing time, and a
-    // workgroup holding a ticket would hold its waves until its chunk is packed)
+    // staged: workgroups 0 .. n-1 stage, every wave of them, every segment in order, then they count
+    // like the rest (a workgroup's wave holding a ticket would hold its other waves until its chunk
+    // is packed); a staged launch with chunks always has n > 0 (0 is reported as a staging error)
     uint32_t copier_wgs;
     uint32_t n_segs;
     uint32_t eq;  // every live segment has equal windows (ulen), checked on the host to fit its image

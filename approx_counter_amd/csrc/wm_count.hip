@@ -188,37 +188,28 @@ struct TidTable {
     uint32_t e[W * 5 * 64];  // lane word w's table at e[w * 320]
 };
 
-// Lane `lane`'s word of window bases [sb, sb + 256): lanes 0-15 the 16 code
-// words, lanes 16-23 the 8 N-mask words, with the index clamped to the window's
-// last word (always inside the image): a word past the window is never read as
-// text (the chunk loop stops at the window length), and a branch-free load
-// keeps hipcc from waiting on it before the window that uses it.
-// Code lanes and N-mask lanes load through buffer descriptors of the
-// segment's two arrays (SGPRs) under complementary exec masks; the byte offset
-// is the window's (an SGPR) plus a per-lane constant (lane_off = 4 * word
-// within the segment).  The descriptors' range check (num_records = the
-// array's bytes, voffset included) returns 0 for a word past the image, so no
-// clamp: words past the window are never read as text (the chunk loop stops
-// at the window length).  One v_add per lane group and window.
+// A window fetch: bases [pos, pos + 256) -- 16 code words and 8 N-mask words -- through buffer
+// descriptors of the segment's two arrays (SGPRs); the byte offset is the window's (an SGPR) plus a
+// per-lane constant.  The descriptors' range check (num_records = the array's bytes, voffset
+// included) returns 0 for a word past the image, so no clamp: words past the window are never read
+// as text (the chunk loop stops at the window length).  The consumer (tid_word) takes lanes 0-15's
+// code words and lanes 16-23's N-mask words.
 struct Image {
     __amdgpu_buffer_rsrc_t codes, nmask;
 };
-// The two halves land in separate registers (merged by the consumer, tid_word):
-// one register for both would make the second load's address wait for the
-// first load to complete (the register is still being written for the other lanes).
 struct Fetch {
     uint32_t c, n;
 };
 __device__ __forceinline__ void tid_fetch(Fetch& f, const Image& im, uint64_t pos, uint32_t lane, uint32_t lane_off) {
-    // (the two asm markers differ, so hipcc cannot merge the loads into one through a per-lane
-    // selected descriptor, which it would wrap in a waterfall loop)
-    if (lane < 16u) {
-        f.c = __builtin_amdgcn_raw_buffer_load_b32(im.codes, (uint32_t)(pos >> 2) + lane_off, 0, 0);
-        asm volatile("; code words");
-    } else {
-        f.n = __builtin_amdgcn_raw_buffer_load_b32(im.nmask, (uint32_t)(pos >> 3) + lane_off, 0, 0);
-        asm volatile("; N-mask words");
-    }
+    // Every lane loads both words -- code word (lane & 15) and N-mask word (lane & 7) of the segment;
+    // lanes past 16 / 8 repeat addresses of the same lines, which the load coalesces -- so both results
+    // are whole registers.  (Round 4 loaded each half under its own exec mask: hipcc then merged the
+    // halves with the previous window's values, copying them back after a wait for both loads
+    // -- s_waitcnt vmcnt(0) right after every prefetch inside multi-window items -- and computed the
+    // second offset into the first load's destination, another wait.)
+    (void)lane;
+    f.c = __builtin_amdgcn_raw_buffer_load_b32(im.codes, (uint32_t)(pos >> 2) + (lane_off & 63u), 0, 0);
+    f.n = __builtin_amdgcn_raw_buffer_load_b32(im.nmask, (uint32_t)(pos >> 3) + (lane_off >> 8), 0, 0);
 }
 __device__ __forceinline__ uint32_t tid_word(const Fetch& f, uint32_t lane) { return lane < 16u ? f.c : f.n; }
 
@@ -650,9 +641,9 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
     if (STAGED && sg.stage_chunks) {  // (a segment sent ahead of a staged launch has no chunks)
         st_words = a.stage + AC_STAGE_L_SEG(si) * AC_QUEUE_LINE;
         // the k-mer section fills whole chunks and is in the pinned block before the launch
-        const uint32_t pre_bytes = sg.stage_codes_off, pre_chunks = pre_bytes / AC_STAGE_CHUNK;
-        if (a.copier_wgs && blockIdx.x < a.copier_wgs) {
-            // Copier workgroup of a large call: every wave serves every segment's tickets, starting
+        const uint32_t pre_bytes = sg.stage_codes_off;
+        if (blockIdx.x < a.copier_wgs) {
+            // Copier workgroup: every wave serves every segment's tickets, starting
             // with segment (workgroup mod segments) -- the host packs a large call's jobs interleaved,
             // so all segments arrive together -- before the workgroup counts like the others.
             for (uint32_t i2 = 0; i2 < a.n_segs; ++i2) {
@@ -669,14 +660,9 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
         if (wib == 0) {
             uint32_t r = ~0u;
             const bool equal = sg.ulen != AC_NO_ULEN && sg.n_kmers;
-            // (serving a chunk that has to wait for the host after the table barrier instead, so the
-            // workgroup's other waves start counting, measured slower: its copy starts later,
-            // profiles/r03_stage2/defer_ab.log)
-            if (!a.copier_wgs &&
-                !__builtin_amdgcn_readfirstlane(
-                    (uint32_t)stage_copy(sg.stage_src, sg.stage_dst, sg.stage_chunks, pre_chunks,
-                                         a.host_hdr + (uint32_t)si * AC_QUEUE_LINE, st_words, sg.stage_gen, a.gen,
-                                         (uint32_t)si))) {
+            // (the copier workgroups stage every chunk: a launch with chunks has them, capi.cpp
+            // stage_copiers; round 3's wave-0 tickets in every workgroup were removed in round 5)
+            if (!a.copier_wgs) {
                 if (lane == 0) atomicOr(a.err, AC_DEVERR_STAGE);
             } else if (equal) {
                 // only the k-mers (the ~Eq table) are needed before counting starts
@@ -745,9 +731,11 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
     for (int p = 0; p < P; ++p) first |= 1u << (31 - p);
     // Initial rows (empty text): R1 has character 0 set, R2 characters 0 and 1.
     const uint32_t d1_init = ~first, d2_init = ~(first | (first >> P));
+    const TidInit ini = {~0u >> P, d1_init >> P, d2_init >> P, d1_init, d2_init};  // (loop-invariant registers)
     uint32_t cnt[Q];
 #pragma unroll
-    for (int q = 0; q < Q; ++q) cnt[q] = 0;
+    for (int q = 0; q < Q; ++q) cnt[q] = 0;  // (P <= 2: misses, until the loop's end)
+    uint32_t n_counted = 0;                   // (wave-uniform) windows whose levels were counted
     const uint32_t eb = __builtin_amdgcn_readfirstlane(
         (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)(&lds.tab.e[0]));
     // The eb0 blocks address the table from LDS 0.  Never expected otherwise;
@@ -895,7 +883,8 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
     uint64_t nbase = 0;
     uint32_t nlen = 0;
     Fetch nf = {0u, 0u};
-    const uint32_t lane_off = (lane < 16u ? lane : (lane - 16u) & 7u) << 2;  // this lane's word of a segment, in bytes
+    // this lane's code word (bits 0-5) and N-mask word (bits 8+) of a segment, in bytes
+    const uint32_t lane_off = ((lane & 15u) << 2) | ((lane & 7u) << 10);
     auto fetch_next = [&](uint64_t b) __attribute__((always_inline)) { tid_fetch(nf, im, b, lane, lane_off); };
     if (item < n_items) {
         desc(w, nbase, nlen);
@@ -1006,10 +995,14 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
         }
         const uint32_t nb0 = ok ? min(SEG, len) : 0u;
         const uint32_t nfull0 = nb0 >> 4;
+        // The initial state: read by the first block from ini's registers where a
+        // window starts with one (no per-window copy), written here otherwise.
         TidNfa s[W];
+        if (!(nfull0 >= 2u && skip_first)) {
 #pragma unroll
-        for (int w = 0; w < W; ++w)
-            s[w] = TidNfa{~0u, d1_init, d2_init, ~0u >> P, d1_init >> P, d2_init >> P, ~0u, d1_init, d2_init};
+            for (int w = 0; w < W; ++w)
+                s[w] = TidNfa{~0u, ini.d1, ini.d2, ini.s0, ini.s1, ini.s2, ~0u, ini.d1, ini.d2};
+        }
         auto block32 = [&](uint32_t f, uint32_t ch) __attribute__((always_inline)) {
             const uint32_t code = __builtin_amdgcn_readlane(f, ch);
             const uint32_t code2 = __builtin_amdgcn_readlane(f, ch + 1u);
@@ -1023,7 +1016,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
                 const uint32_t code = __builtin_amdgcn_readlane(f0, 0u);
                 const uint32_t code2 = __builtin_amdgcn_readlane(f0, 1u);
                 const uint32_t nm = __builtin_amdgcn_readlane(f0, 16u);
-                AC_NFA_FIRST(s, code, code2, nm, eb);
+                AC_NFA_FIRST(s, ini, code, code2, nm, eb);
             } else {
                 block32(f0, 0u);
             }
@@ -1067,13 +1060,25 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
                 asm volatile("" : "+v"(f));
                 segment(f, sb, 0u);
             }
+            // P <= 2: counted as misses (cnt = 3 x the windows counted - misses, at the end).  The levels nest
+            // (a row-r match is one of row r+1: a2 <= a1 <= a0 bitwise, by induction over the
+            // recurrence), so a candidate's misses b0 + b1 + b2 = 2 * b1 + (b0 ^ b1 ^ b2): one XOR3
+            // per lane word, then two bit extractions, a shift and an ADD3 per candidate (was 3 + 3).
 #pragma unroll
-            for (int w = 0; w < W; ++w)
+            for (int w = 0; w < W; ++w) {
+                const uint32_t px = P <= 2 ? __builtin_amdgcn_bitop3_b32(s[w].a0, s[w].a1, s[w].a2, 0x96) : 0u;
 #pragma unroll
                 for (int p = 0; p < P; ++p) {
                     const uint32_t lb = 31u - ((m - 1u) * P + (uint32_t)p);
-                    cnt[w * P + p] += 3u - ((s[w].a0 >> lb) & 1u) - ((s[w].a1 >> lb) & 1u) - ((s[w].a2 >> lb) & 1u);
+                    if constexpr (P <= 2) {
+                        const uint32_t b1 = __builtin_amdgcn_ubfe(s[w].a1, lb, 1u), bp = __builtin_amdgcn_ubfe(px, lb, 1u);
+                        cnt[w * P + p] += (b1 << 1) + bp;
+                    } else {  // (P = 3, 4, 64 VGPRs at 8 waves per SIMD: hits, the round-4 form, spills least)
+                        cnt[w * P + p] += 3u - ((s[w].a0 >> lb) & 1u) - ((s[w].a1 >> lb) & 1u) - ((s[w].a2 >> lb) & 1u);
+                    }
                 }
+            }
+            if (P <= 2) ++n_counted;
         }
         stamp_win(wave, n_win++);
         // advance the cursor; at an item boundary move to the claimed item
@@ -1114,6 +1119,9 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
     // to the counts.  One device-scope round trip at the launch's end (round 4 had three: the adds, a
     // group ticket taken after them, the slots read back and zeroed).  No fences: the arrival count and
     // the sum change in one atomic.
+#pragma unroll
+    for (int q = 0; q < Q; ++q)
+        if (P <= 2) cnt[q] = 3u * n_counted - cnt[q];
 #pragma unroll
     for (int q = 0; q < Q; ++q)
         if (cnt[q]) __hip_atomic_fetch_add(&lds.cnt[q * 64 + lane], cnt[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);

@@ -383,9 +383,9 @@ int ac_plan_host_cpus(const char* const* rank_cpulists, int n_ranks, int rank, c
  * soon as it is packed, the kernel copies the flagged job into device memory
  * itself and counts it while later jobs are still being packed, and each
  * candidate group's last workgroup stores its counts and error bits, tagged with
- * the call's generation, into pinned memory, which the host polls.  Large calls
- * (more staging chunks than half the workgroups) are staged by a few copier
- * workgroups while the others count.  0 = the DMA path (AC_STAGE_EARLY=0: calls
+ * the call's generation, into pinned memory, which the host polls.  A few copier
+ * workgroups of the kernel do the copying (every early-launch call) while the
+ * others count.  0 = the DMA path (AC_STAGE_EARLY=0: calls
  * of >= 2^17 windows cut into 2-4 parts, each packed and copied by the copy
  * engine while the previous part counts; a multi-device context; a staging
  * region of 2^31 bytes or more; the retry of a timed-out early launch).  Either

@@ -48,7 +48,7 @@ def m0_setup(j, with_n, eb0):
     return s
 
 
-def block(nb, with_n, eb0, skip=0, W=1):
+def block(nb, with_n, eb0, skip=0, W=1, init=False):
     """Skewed (software-pipelined) schedule: step s runs row 0 of base s, row 1 of
     base s-1 and row 2 of base s-2 -- three independent dependency chains per wave.
     Row r of base i needs row r of base i-1 and row r-1 of bases i-1 and i, all
@@ -56,15 +56,23 @@ def block(nb, with_n, eb0, skip=0, W=1):
     slot 3 is the operand register, so blocks of a multiple of 4 bases end in place.
     W = 2: two lane words per wave (2 x P candidates per lane) share each base's SALU
     work; word w reads its own ~Eq table (LDS offset w * 1280 B) and its ops are
-    interleaved with the other word's, six dependency chains per wave."""
+    interleaved with the other word's, six dependency chains per wave.
+    init: a window's first block reads the NFA's initial state from loop-invariant
+    input registers (%[id1], %[is0] ...; d0 = a0 = ~0 is the inline constant -1)
+    and only writes the state operands, so no per-window copy of the initial
+    state into them precedes it."""
 
     def pre(w):
         return "" if W == 1 else f"w{w}"
 
     def D(w, r, i):
+        if init and i == -1:
+            return "-1" if r == 0 else f"%[id{r}]"
         return f"%[{pre(w)}d{r}]" if i % 4 == 3 else f"%[{pre(w)}D{r}{i % 4}]"
 
     def T(w, r, i):
+        if init and i == -1:
+            return f"%[is{r}]"
         return f"%[{pre(w)}s{r}]" if i % 4 == 3 else f"%[{pre(w)}T{r}{i % 4}]"
 
     def E(w, i):
@@ -120,10 +128,18 @@ def block(nb, with_n, eb0, skip=0, W=1):
             if i < skip:  # a window's first bases: no occurrence can end there (skip <= k - 3)
                 continue
             for w in range(W):
-                if i % 2 == 1:
+                if init and i == skip + 1:  # the accumulator's first AND: from the initial a_r
+                    assert skip % 2 == 0 and i < nb
+                    if r == 0:
+                        L.append(f"v_and_b32 {A(w, r)}, {D(w, r, i - 1)}, {D(w, r, i)}")
+                    else:
+                        L.append(f"v_bitop3_b32 {A(w, r)}, %[id{r}], {D(w, r, i - 1)}, {D(w, r, i)} bitop3:0x80")
+                elif i % 2 == 1:
                     L.append(f"v_bitop3_b32 {A(w, r)}, {A(w, r)}, {D(w, r, i - 1)}, {D(w, r, i)} bitop3:0x80")
                 elif i == nb - 1:  # unpaired last base (odd nb)
                     L.append(f"v_and_b32 {A(w, r)}, {A(w, r)}, {D(w, r, i)}")
+    if init:
+        assert skip > 0 and (nb - 1) % 4 == 3 and nb > skip + 1  # every state operand is written
     if (nb - 1) % 4 != 3:  # final state not in the operand slot
         for w in range(W):
             for r in range(3):
@@ -132,18 +148,18 @@ def block(nb, with_n, eb0, skip=0, W=1):
     return L
 
 
-def body(nb, eb0, skip=0, W=1):
+def body(nb, eb0, skip=0, W=1, init=False):
     """Whole statement text: N-free chunks take the fast path, chunks with an N
     the N-aware one (same registers, so hipcc sees one statement)."""
     L = ["s_mov_b32 %[keep], m0", "s_cmp_lg_u32 %[nm], 0", "s_cbranch_scc1 .Lnpath%="]
-    L += block(nb, False, eb0, skip, W)
+    L += block(nb, False, eb0, skip, W, init)
     L += ["s_branch .Lend%=", ".Lnpath%=:"]
-    L += block(nb, True, eb0, skip, W)
+    L += block(nb, True, eb0, skip, W, init)
     L += [".Lend%=:", "s_mov_b32 m0, %[keep]"]
     return "\n".join(f'            "{ln}\\n\\t"' for ln in L)
 
 
-def emit(nb, skip=0, name=None, W=1):
+def emit(nb, skip=0, name=None, W=1, init=False):
     extra = [f"code{i}" for i in range(2, (nb + 15) // 16 + 1)]
     code2_in = "".join(f', [{c}] "s"({c})' for c in extra)
     code2_arg = "".join(f", uint32_t {c}" for c in extra)
@@ -157,18 +173,22 @@ def emit(nb, skip=0, name=None, W=1):
     states = []
     for w, p in enumerate(pres):
         sv = "s" if W == 1 else f"s{w}"
-        states.append(", ".join(f'[{p}{f}] "+v"({sv}.{f})' for f in ("d0", "d1", "d2", "s0", "s1", "s2", "a0", "a1", "a2")))
-    if W == 1:  # (the one-word text exactly as before W existed)
+        mode = "=&v" if init else "+v"
+        states.append(", ".join(f'[{p}{f}] "{mode}"({sv}.{f})' for f in ("d0", "d1", "d2", "s0", "s1", "s2", "a0", "a1", "a2")))
+    if W == 1 and not init:  # (the one-word text exactly as before W existed)
         state_ops = """[d0] "+v"(s.d0), [d1] "+v"(s.d1), [d2] "+v"(s.d2), [s0] "+v"(s.s0), [s1] "+v"(s.s1),
               [s2] "+v"(s.s2), [a0] "+v"(s.a0), [a1] "+v"(s.a1), [a2] "+v"(s.a2)"""
         sig = "TidNfa& s"
     else:
         state_ops = ",\n              ".join(states)
-        sig = ", ".join(f"TidNfa& s{w}" for w in range(W))
+        sig = "TidNfa& s" if W == 1 else ", ".join(f"TidNfa& s{w}" for w in range(W))
+    init_in = "".join(f', [{v}] "v"(ini.{v[1:]})' for v in ("is0", "is1", "is2", "id1", "id2")) if init else ""
+    if init:
+        sig += ", const TidInit& ini"
     operands = f"""            : {state_ops},
               {outs},
               [t] "=&s"(t), [keep] "=&s"(keep)
-            : [code] "s"(code){code2_in}, [nm] "s"(nm), [eb] "s"(eb), [P] "n"(P)
+            : [code] "s"(code){code2_in}, [nm] "s"(nm), [eb] "s"(eb), [P] "n"(P){init_in}
             : "memory", "scc");"""
     return f"""template <int P, bool EB0>
 __device__ __forceinline__ void {name or f"tid_block{nb}"}({sig}, uint32_t code{code2_arg}, uint32_t nm, uint32_t eb) {{
@@ -176,11 +196,11 @@ __device__ __forceinline__ void {name or f"tid_block{nb}"}({sig}, uint32_t code{
     uint32_t t, keep;
     if constexpr (EB0) {{
         asm volatile(
-{body(nb, True, skip, W)}
+{body(nb, True, skip, W, init)}
 {operands}
     }} else {{
         asm volatile(
-{body(nb, False, skip, W)}
+{body(nb, False, skip, W, init)}
 {operands}
     }}
 }}
@@ -197,7 +217,9 @@ def main():
         "// GENERATED by tools/gen_tid_blocks.py -- do not edit.  Inline-asm blocks of the\n"
         "// table-driven count loop (wm_count.hip, DESIGN.md §4).\n"
         "// TidNfa: d* complemented NFA rows, s* = d* >> P, a* AND of the rows over the window.\n"
-        "struct TidNfa {\n    uint32_t d0, d1, d2, s0, s1, s2, a0, a1, a2;\n};\n\n"
+        "struct TidNfa {\n    uint32_t d0, d1, d2, s0, s1, s2, a0, a1, a2;\n};\n"
+        "// The initial state a window's first block reads (d0 = a0 = ~0, a1 = d1, a2 = d2).\n"
+        "struct TidInit {\n    uint32_t s0, s1, s2, d1, d2;\n};\n\n"
     ]
     for nb in (32, 16, 8, 4, 2, 1):  # 64-base blocks measured no faster (r01_kernel_log.md)
         parts.append(emit(nb))
@@ -205,12 +227,12 @@ def main():
     # occurrence with <= 2 edits spans >= k - 2 bases, so none ends before base
     # k - 3 (valid for k >= 15; wm_count.hip picks it then).
     parts.append("// tid_block32 for a window's first 32 bases, k >= 15: no hit accumulation over bases 0-11.")
-    parts.append(emit(32, skip=FIRST_SKIP, name="tid_block32_first"))
+    parts.append(emit(32, skip=FIRST_SKIP, name="tid_block32_first", init=True))
     # Two lane words per wave (AC_WORDS = 2 builds, wm_count.hip): the same blocks over two states.
     parts.append("// Two lane words per wave (AC_WORDS == 2): both words' NFAs, one base's SALU work shared.")
     for nb in (32, 16, 8, 4, 2, 1):
         parts.append(emit(nb, W=2, name=f"tid2_block{nb}"))
-    parts.append(emit(32, skip=FIRST_SKIP, name="tid2_block32_first", W=2))
+    parts.append(emit(32, skip=FIRST_SKIP, name="tid2_block32_first", W=2, init=True))
     with open(OUT, "w") as fh:
         fh.write("\n".join(parts))
     print("wrote", OUT)

@@ -195,5 +195,16 @@ stepform)  # the N > 1 step's way back, rehearsed on one GPU (one-rank RCCL comm
     run sf_host0_$rep 200 $B --step-form submit-host0
     run sf_host1_$rep 200 $B --step-form submit-host1
   done ;;
+fetch)  # split tail (main; split2: two rounds) over cur (whole-register fetch + init registers + nested-level count + no round-3 staging) over fetch (the fetch alone) over HEAD (prev)
+  run tests_fetch 900 $PYT -m gpu tests/test_gpu_parity.py tests/test_gpu_bench_path.py tests/test_gpu_jobs.py
+  for rep in 1 2; do
+    for v in main split2 cur fetch prev; do
+      L=$([ $v = main ] && echo "" || echo "APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so")
+      run ksweep_${v}_$rep 300 env $L python3 tools/kernel_sweep.py --sn 10000 --launches 300
+      run kcfg3_${v}_$rep 300 env $L python3 tools/kernel_sweep.py --sn 100000 --lim 2000 --launches 30 --warmup 10
+      run kcfg5_${v}_$rep 300 env $L python3 tools/kernel_sweep.py --sn 100000 --lim 1000 --k 22 --sl 150 --launches 30 --warmup 10
+      run stage_${v}_$rep 200 env $L $B
+    done
+  done ;;
 esac
 done
