@@ -703,6 +703,16 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
     uint32_t ulen = sg.ulen;
     asm volatile("" : "+s"(ulen));
     const uint32_t ustride = ulen == AC_NO_ULEN ? 0u : (ulen + 31u) & ~31u;
+    // The segment's fields read inside the window loop, pinned: under the staged kernel's SGPR
+    // pressure hipcc otherwise reloaded them from the kernel arguments at every item and gate call --
+    // scalar loads, which count in lgkmcnt, so the NFA blocks' LDS waits waited for them too (staged
+    // kernel on resident input +4.7 % wave-cycles at cfg3, 11x the SMEM instructions,
+    // profiles/r05_m22).  Spilled to VGPR lanes instead, a reload is one VALU op.
+    uint32_t seg_nw = sg.n_windows, seg_chunk = sg.chunk, seg_qb = sg.queue_begin;
+    asm volatile("" : "+s"(seg_nw), "+s"(seg_chunk), "+s"(seg_qb));
+    uint32_t st_codes_off = STAGED ? sg.stage_codes_off : 0u, st_nchunks = STAGED ? sg.stage_chunks : 0u;
+    uint32_t* st_gen = STAGED ? sg.stage_gen : nullptr;
+    if constexpr (STAGED) asm volatile("" : "+s"(st_codes_off), "+s"(st_nchunks), "+s"(st_gen));
     // inline N records (nrec.h): the lane of the fetch holding a window's record word, ~0u: none
     uint32_t rec_lane = sg.nrec ? nrec_word(ulen) : ~0u;
     asm volatile("" : "+s"(rec_lane));
@@ -765,14 +775,14 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
     // the same candidate group (same lane masks), probing each counter with a
     // plain load before claiming.
     const uint32_t S = sg.subq;
-    const uint32_t chunk = sg.chunk;
-    const uint32_t n_items = (sg.n_windows + chunk - 1u) / chunk;
+    const uint32_t chunk = seg_chunk;
+    const uint32_t n_items = (seg_nw + chunk - 1u) / chunk;
     uint32_t jc = j;  // sub-queue currently served
     auto counter = [&](uint32_t jj) {
         return g_queue + (uint64_t)jj * AC_QUEUE_LINE;
     };
     auto waves_in = [&](uint32_t jj) {  // waves dealt to sub-queue (g, jj): their first items are static
-        const uint32_t qq = sg.queue_begin + g * sg.subq + jj;
+        const uint32_t qq = seg_qb + g * S + jj;
         const uint32_t qb = qq / WAVES_PER_BLOCK;  // one wave of every workgroup dealt to block-queue qb
         return wgs_of(qb);
     };
@@ -826,7 +836,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
     };
     uint32_t item = (j < n_items && eb_ok && !skip) ? item_of(rank) : n_items;
     uint32_t pending = 0;
-    uint32_t w = item * chunk, item_end = min(sg.n_windows, w + chunk);
+    uint32_t w = item * chunk, item_end = min(seg_nw, w + chunk);
 
     // Window pipeline: the next window's first segment is fetched while the current one is counted.
     // (written so that no sum wraps: a start near 2^64 must not pass)
@@ -853,15 +863,15 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
         if constexpr (STAGED) {
             if (!partial) return true;
             const uint64_t end = min(base + (((uint64_t)len + 255u) & ~255ull), g_nbases);
-            const uint32_t r0 = sg.stage_codes_off + (uint32_t)(base >> 2);
-            const uint32_t r1 = sg.stage_codes_off + (uint32_t)(end >> 2);
+            const uint32_t r0 = st_codes_off + (uint32_t)(base >> 2);
+            const uint32_t r1 = st_codes_off + (uint32_t)(end >> 2);
             if (r0 >= v_lo && r1 <= v_hi) return true;
             // (a call's results come back in VGPRs: made wave-uniform again, or everything they
             // touch -- the item cursor, window bases -- would turn divergent)
 #ifdef AC_STAMPS
             const uint64_t tg = __builtin_amdgcn_s_memrealtime();
 #endif
-            const uint64_t g = stage_gate(st_words, sg.stage_gen, sg.stage_chunks, blockIdx.x % AC_STAGE_REPL, a.gen,
+            const uint64_t g = stage_gate(st_words, st_gen, st_nchunks, blockIdx.x % AC_STAGE_REPL, a.gen,
                                           r0, r1, a.err);
 #ifdef AC_STAMPS
             gate_ticks += __builtin_amdgcn_s_memrealtime() - tg;
@@ -959,7 +969,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
                 bool have = false;
                 if constexpr (STAGED) {
                     if (partial) {  // wait for the whole segment (its N bitmap)
-                        const uint64_t g = stage_gate(st_words, sg.stage_gen, sg.stage_chunks, blockIdx.x % AC_STAGE_REPL,
+                        const uint64_t g = stage_gate(st_words, st_gen, st_nchunks, blockIdx.x % AC_STAGE_REPL,
                                                       a.gen, 0u, ~0u, a.err);
                         if (!completed(__builtin_amdgcn_readfirstlane((uint32_t)g))) stage_ok = false;
                     }
@@ -1097,7 +1107,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
             }
             if (item < n_items) {
                 w = item * chunk;
-                item_end = min(sg.n_windows, w + chunk);
+                item_end = min(seg_nw, w + chunk);
             }
         }
         if (STAGED && !stage_ok) break;  // the segment is skipped (the error word says so)

@@ -24,6 +24,10 @@ def main():
                          "sustained clock; kernel traces then leave them out: prof_summary.py --skip)")
     ap.add_argument("--descriptors", action="store_true",
                     help="load every window's start / length (ac_error_count_device) even for equal windows")
+    ap.add_argument("--staged", action="store_true",
+                    help="the early launch's staged instantiation on resident input instead: ac_error_count_jobs "
+                         "with every job sent ahead of the launch (AC_TESTING_ALL_AHEAD), so a kernel trace shows "
+                         "its own cost against the plain kernel's")
     a = ap.parse_args()
     import torch
 
@@ -33,6 +37,21 @@ def main():
     sys.argv = ["bench.py", "--config", a.config]
     args = bench.parse()
     wl, _ = bench.build_workload(args, 0, 1)
+    if a.staged:
+        from approx_counter_amd._lib import load
+
+        L = load()
+        jobs = [(wl[e]["kmers"], ac.Dna5Sample.from_windows(wl[e]["windows"])) for e in ("start", "end")]
+        with ac.ApproxCounter(0) as c:
+            prev = L.ac_testing_stage_hooks(2)  # AC_TESTING_ALL_AHEAD
+            try:
+                for _ in range(a.warmup + a.launches):
+                    c.count_jobs(args.k, jobs)
+            finally:
+                L.ac_testing_stage_hooks(prev)
+            print(f"{a.launches} staged launches of {a.config} on resident input (stage mode {c.stage_mode()}); "
+                  f"geometry {c.last_launch()}")
+        return
     packed = [ac.pack_windows(wl[e]["windows"]) for e in ("start", "end")]
     segs = [ac.DeviceSegment.upload(wl[e]["kmers"], packed[i]) for i, e in enumerate(("start", "end"))]
     arr = ac.ApproxCounter.segment_array(segs)

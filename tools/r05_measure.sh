@@ -195,6 +195,49 @@ stepform)  # the N > 1 step's way back, rehearsed on one GPU (one-rank RCCL comm
     run sf_host0_$rep 200 $B --step-form submit-host0
     run sf_host1_$rep 200 $B --step-form submit-host1
   done ;;
+staged)  # the staged instantiation on resident input (every job sent ahead) against the plain kernel, cfg2-cfg5 kernel traces
+  for c in cfg2 cfg3 cfg5 cfg4; do
+    for m in plain staged; do
+      F=""; [ $m = staged ] && F="--staged"
+      ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$OUT/tr_${c}_$m" -o run -- \
+        python3 "$GRAFT_REPO_ROOT/tools/kernel_run.py" --config $c --launches 20 --warmup 10 $F ) > "$OUT/tr_${c}_$m.log" 2>&1 \
+        || { echo "trace $c $m failed"; tail -5 "$OUT/tr_${c}_$m.log"; exit 5; }
+      echo "== tr $c $m ok" | tee -a "$OUT/summary.log"
+    done
+  done ;;
+profcfg)  # kernel traces of bench.py's stage at cfg3 / cfg5 / cfg4 (the staged kernel inside the timed step)
+  for c in cfg3 cfg5 cfg4; do
+    ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$c" -o run -- \
+      python3 "$GRAFT_REPO_ROOT/bench.py" --config $c --steps 20 --warmup 5 --no-cpu-baseline --no-pipelined --kernel-launches 10 ) \
+      > "$OUT/prof_$c.log" 2>&1 || { echo "prof $c failed"; exit 6; }
+    echo "== prof $c ok" | tee -a "$OUT/summary.log"
+  done ;;
+stagedpmc)  # SQ instruction / wait counters of the staged instantiation on resident input against the plain kernel, cfg3
+  for m in plain staged; do
+    F=""; [ $m = staged ] && F="--staged"
+    ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_SMEM \
+      -d "$OUT/pmc3_$m" -o run -- python3 "$GRAFT_REPO_ROOT/tools/kernel_run.py" --config cfg3 --launches 10 --warmup 5 $F ) > "$OUT/pmc3_$m.log" 2>&1 \
+      || { echo "pmc $m failed"; tail -5 "$OUT/pmc3_$m.log"; exit 3; }
+    echo "== pmc3 $m ok" | tee -a "$OUT/summary.log"
+  done ;;
+pin)  # staged kernel's loop-read segment fields pinned in SGPRs (main) vs HEAD (prev): tests, stage cfg2-cfg5, staged-on-resident traces
+  run tests_pin 900 $PYT -m gpu tests/test_gpu_parity.py tests/test_gpu_bench_path.py tests/test_gpu_jobs.py
+  for rep in 1 2; do
+    for v in main prev; do
+      L=$([ $v = main ] && echo "" || echo "APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so")
+      run stage_${v}_$rep 200 env $L $B
+      for c in cfg3 cfg5 cfg4; do
+        run ${c}_${v}_$rep 300 env $L python3 bench.py --config $c --steps 20 --warmup 5 $BQ --no-kernel-leg
+      done
+    done
+  done
+  for v in main prev; do
+    ( cd /tmp && export TMPDIR=/tmp && { [ $v = main ] || export APPROX_COUNTER_AMD_LIB=$GRAFT_REPO_ROOT/build/var/$v/libapprox_counter_amd.so; } && \
+      timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$OUT/trs_cfg3_$v" -o run -- \
+      python3 "$GRAFT_REPO_ROOT/tools/kernel_run.py" --config cfg3 --launches 20 --warmup 10 --staged ) > "$OUT/trs_cfg3_$v.log" 2>&1 \
+      || { echo "trace $v failed"; tail -5 "$OUT/trs_cfg3_$v.log"; exit 5; }
+    echo "== trs cfg3 $v ok" | tee -a "$OUT/summary.log"
+  done ;;
 fetch)  # split tail (main; split2: two rounds) over cur (whole-register fetch + init registers + nested-level count + no round-3 staging) over fetch (the fetch alone) over HEAD (prev)
   run tests_fetch 900 $PYT -m gpu tests/test_gpu_parity.py tests/test_gpu_bench_path.py tests/test_gpu_jobs.py
   for rep in 1 2; do
