@@ -29,7 +29,7 @@ CLI := $(BINDIR)/adaptFinder
 
 all: $(LIB) $(HOSTLIB) $(CLI) oracle
 
-$(OBJDIR)/wm_count.o: $(CSRC)/wm_count.hip $(CSRC)/wm_tid_blocks.inc $(HDRS)
+$(OBJDIR)/wm_count.o: $(CSRC)/wm_count.hip $(CSRC)/wm_tid_blocks.inc $(CSRC)/wm_window_loop.inc $(HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) $(WM_FLAGS) -Iinclude -I$(CSRC) -c $< -o $@
 
@@ -62,7 +62,7 @@ $(CLI): $(HOSTDIR)/adaptfinder.cpp $(HOST_SRC) $(HOST_HDRS) $(LIB)
 oracle:
 	$(MAKE) -s -C oracle
 
-asm: $(CSRC)/wm_count.hip $(HDRS)
+asm: $(CSRC)/wm_count.hip $(CSRC)/wm_tid_blocks.inc $(CSRC)/wm_window_loop.inc $(HDRS)
 	@mkdir -p build/asm
 	$(HIPCC) $(HIPFLAGS) $(WM_FLAGS) -Iinclude -I$(CSRC) --cuda-device-only -S $< -o build/asm/wm_count.s
 

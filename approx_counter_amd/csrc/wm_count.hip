@@ -943,175 +943,18 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
     // item's last window: claim -> descriptor -> first words; otherwise
     // descriptor -> first words) are spread over the gaps between the window's
     // first 32-base blocks, so none of them stalls the wave between windows.
-    while (item < n_items) {
-        const uint64_t base = nbase;
-        const uint32_t len = nlen;
-        // Wait for this window's words here, before the next window's fetch is
-        // issued: inside the chunk loop hipcc would otherwise wait for both.
-        uint32_t f0 = tid_word(nf, lane);
-        asm volatile("" : "+v"(f0));
-        const uint32_t wn = w + 1;
-        const bool last = wn >= item_end;  // the item's last window: claim the next item
-        uint32_t nitem = n_items;
-        if (!last) {
-            desc(wn, nbase, nlen);
-        } else {
-            pending = dequeue_issue();
-        }
-        bool ok = valid(base, len);  // a malformed window is skipped: never read outside the image
-        if (!ok && lane == 0) atomicOr(a.err, AC_DEVERR_WINDOW);
-        // Inline N record (nrec.h): the window's N-mask words (lanes 16-23) built from its N
-        // positions; an overflowed record takes the N bitmap's words instead.
-        if (rec_lane != ~0u && ok) {
-            const uint32_t rw = __builtin_amdgcn_readlane(f0, rec_lane);
-            const uint32_t c = rw >> 29;
-            if (c == NREC_OVERFLOW) {
-                bool have = false;
-                if constexpr (STAGED) {
-                    if (partial) {  // wait for the whole segment (its N bitmap)
-                        const uint64_t g = stage_gate(st_words, st_gen, st_nchunks, blockIdx.x % AC_STAGE_REPL,
-                                                      a.gen, 0u, ~0u, a.err);
-                        if (!completed(__builtin_amdgcn_readfirstlane((uint32_t)g))) stage_ok = false;
-                    }
-                }
-                if (has_n && stage_ok) {  // this window's N-mask words from the bitmap
-                    Image full = im;
-                    full.nmask = __builtin_amdgcn_make_buffer_rsrc((void*)nmask_p, 0, (int)(uint32_t)(g_nbases >> 3),
-                                                                   0x00020000);
-                    Fetch ff = {0u, 0u};
-                    tid_fetch(ff, full, base, lane, lane_off);
-                    uint32_t v = tid_word(ff, lane);
-                    asm volatile("" : "+v"(v));
-                    if (lane >= 16u) f0 = v;
-                    have = true;
-                }
-                if (!have) {  // no bitmap for an overflowed record: skipped, reported
-                    if (stage_ok && lane == 0) atomicOr(a.err, AC_DEVERR_WINDOW);
-                    ok = false;
-                }
-            } else if (c) {
-                const uint32_t pb = ustride <= 128u ? 7u : 8u, pm = (1u << pb) - 1u;
-                const uint32_t wi = lane - 16u;  // this lane's N-mask word (lanes 16-23)
-                uint32_t add = 0;
-                for (uint32_t i = 0; i < c; ++i) {
-                    const uint32_t pos = (rw >> nrec_pos_shift(pb, i)) & pm;
-                    if (wi == (pos >> 5)) add |= 1u << (pos & 31u);
-                }
-                f0 |= add;
-            }
-            // (made wave-uniform again: set under the error atomic's lane-0 branch, hipcc would
-            // treat it -- and every window size derived from it -- as divergent)
-            ok = __builtin_amdgcn_readfirstlane((uint32_t)ok) != 0u;
-        }
-        const uint32_t nb0 = ok ? min(SEG, len) : 0u;
-        const uint32_t nfull0 = nb0 >> 4;
-        // The initial state: read by the first block from ini's registers where a
-        // window starts with one (no per-window copy), written here otherwise.
-        TidNfa s[W];
-        if (!(nfull0 >= 2u && skip_first)) {
-#pragma unroll
-            for (int w = 0; w < W; ++w)
-                s[w] = TidNfa{~0u, ini.d1, ini.d2, ini.s0, ini.s1, ini.s2, ~0u, ini.d1, ini.d2};
-        }
-        auto block32 = [&](uint32_t f, uint32_t ch) __attribute__((always_inline)) {
-            const uint32_t code = __builtin_amdgcn_readlane(f, ch);
-            const uint32_t code2 = __builtin_amdgcn_readlane(f, ch + 1u);
-            const uint32_t nm = __builtin_amdgcn_readlane(f, 16u + (ch >> 1));
-            AC_NFA(32, s, code, code2, nm, eb);
-        };
-        // step 1 (after block 0): the claim's result -> the next item's descriptor,
-        // or the next window's first words
-        if (nfull0 >= 2u) {
-            if (skip_first) {  // bases 0-31, no hit accumulation over bases 0-11 (k >= 15)
-                const uint32_t code = __builtin_amdgcn_readlane(f0, 0u);
-                const uint32_t code2 = __builtin_amdgcn_readlane(f0, 1u);
-                const uint32_t nm = __builtin_amdgcn_readlane(f0, 16u);
-                AC_NFA_FIRST(s, ini, code, code2, nm, eb);
-            } else {
-                block32(f0, 0u);
-            }
-        }
-        if (last) {
-            nitem = __builtin_amdgcn_readfirstlane(item_of(jc_waves + __builtin_amdgcn_readfirstlane(pending)));
-            if (nitem < n_items) {
-                desc(nitem * chunk, nbase, nlen);
-            }
-        } else if (fetchable(nbase, nlen)) {
-            if (gate(nbase, nlen)) fetch_next(nbase);
-            else stage_ok = false;
-        }
-        // step 2 (after block 1): the next item's first words
-        if (nfull0 >= 4u) block32(f0, 2u);
-        if (last && nitem < n_items && fetchable(nbase, nlen)) {
-            if (gate(nbase, nlen)) fetch_next(nbase);
-            else stage_ok = false;
-        }
-        if (ok) {
-            auto segment = [&](uint32_t f, uint32_t sb, uint32_t ch) __attribute__((always_inline)) {
-                const uint32_t nb = min(SEG, len - sb);
-                const uint32_t nfull = nb >> 4;
-                for (; ch + 2u <= nfull; ch += 2u) block32(f, ch);
-                if (ch < nfull) {
-                    const uint32_t code = __builtin_amdgcn_readlane(f, ch);
-                    const uint32_t nm = (__builtin_amdgcn_readlane(f, 16u + (ch >> 1)) >> ((ch & 1u) * 16u)) & 0xffffu;
-                    AC_NFA(16, s, code, nm, eb);
-                }
-                if (nb & 15u) {
-                    const uint32_t code = __builtin_amdgcn_readlane(f, nfull);
-                    const uint32_t nm = (__builtin_amdgcn_readlane(f, 16u + (nfull >> 1)) >> ((nfull & 1u) * 16u)) & 0xffffu;
-                    tid_tail<P, W>(s, code, nm, nb & 15u, eb);
-                }
-            };
-            segment(f0, 0u, nfull0 >= 4u ? 4u : (nfull0 >= 2u ? 2u : 0u));
-            for (uint32_t sb = SEG; sb < len; sb += SEG) {  // windows longer than one segment
-                Fetch ff;
-                tid_fetch(ff, im, base + sb, lane, lane_off);
-                uint32_t f = tid_word(ff, lane);
-                asm volatile("" : "+v"(f));
-                segment(f, sb, 0u);
-            }
-            // P <= 2: counted as misses (cnt = 3 x the windows counted - misses, at the end).  The levels nest
-            // (a row-r match is one of row r+1: a2 <= a1 <= a0 bitwise, by induction over the
-            // recurrence), so a candidate's misses b0 + b1 + b2 = 2 * b1 + (b0 ^ b1 ^ b2): one XOR3
-            // per lane word, then two bit extractions, a shift and an ADD3 per candidate (was 3 + 3).
-#pragma unroll
-            for (int w = 0; w < W; ++w) {
-                const uint32_t px = P <= 2 ? __builtin_amdgcn_bitop3_b32(s[w].a0, s[w].a1, s[w].a2, 0x96) : 0u;
-#pragma unroll
-                for (int p = 0; p < P; ++p) {
-                    const uint32_t lb = 31u - ((m - 1u) * P + (uint32_t)p);
-                    if constexpr (P <= 2) {
-                        const uint32_t b1 = __builtin_amdgcn_ubfe(s[w].a1, lb, 1u), bp = __builtin_amdgcn_ubfe(px, lb, 1u);
-                        cnt[w * P + p] += (b1 << 1) + bp;
-                    } else {  // (P = 3, 4, 64 VGPRs at 8 waves per SIMD: hits, the round-4 form, spills least)
-                        cnt[w * P + p] += 3u - ((s[w].a0 >> lb) & 1u) - ((s[w].a1 >> lb) & 1u) - ((s[w].a2 >> lb) & 1u);
-                    }
-                }
-            }
-            if (P <= 2) ++n_counted;
-        }
-        stamp_win(wave, n_win++);
-        // advance the cursor; at an item boundary move to the claimed item
-        // (descriptor and first words already requested) or steal one
-        if (++w >= item_end) {
-            item = nitem;
-            if (item >= n_items && S > 1) {
-                item = __builtin_amdgcn_readfirstlane(steal());
-                if (item < n_items) {
-                    desc(item * chunk, nbase, nlen);
-                    if (fetchable(nbase, nlen)) {
-                        if (gate(nbase, nlen)) fetch_next(nbase);
-                        else stage_ok = false;
-                    }
-                }
-            }
-            if (item < n_items) {
-                w = item * chunk;
-                item_end = min(seg_nw, w + chunk);
-            }
-        }
-        if (STAGED && !stage_ok) break;  // the segment is skipped (the error word says so)
+    // The window loop in two copies (staged kernel; GATED a constant in each): while the segment is not known complete (`partial`), a window's fetch first goes
+    // through the gate; once it is, the loop without any staging state, so none of it stays live -- in
+    // SGPRs or spilled to VGPR lanes -- through the rest of the launch.  The plain kernel runs only the
+    // second.
+    if constexpr (STAGED) {
+#define AC_GATED 1
+#include "wm_window_loop.inc"
+#undef AC_GATED
     }
+#define AC_GATED 0
+#include "wm_window_loop.inc"
+#undef AC_GATED
 
     stamp(wave, 2);
     stamp_val(wave, 6, ((uint64_t)si << 32) | ((uint64_t)g << 16) | j);

@@ -238,6 +238,16 @@ pin)  # staged kernel's loop-read segment fields pinned in SGPRs (main) vs HEAD 
       || { echo "trace $v failed"; tail -5 "$OUT/trs_cfg3_$v.log"; exit 5; }
     echo "== trs cfg3 $v ok" | tee -a "$OUT/summary.log"
   done ;;
+icache)  # instruction-cache counters of the staged instantiation on resident input against the plain kernel, cfg3 / cfg4
+  for c in cfg3 cfg4; do
+    for m in plain staged; do
+      F=""; [ $m = staged ] && F="--staged"
+      ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 150 rocprofv3 --pmc SQC_ICACHE_MISSES SQC_ICACHE_REQ SQ_IFETCH SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_BUSY_CYCLES \
+        -d "$OUT/ic_${c}_$m" -o run -- python3 "$GRAFT_REPO_ROOT/tools/kernel_run.py" --config $c --launches 6 --warmup 4 $F ) > "$OUT/ic_${c}_$m.log" 2>&1 \
+        || { echo "icache $c $m failed"; tail -5 "$OUT/ic_${c}_$m.log"; exit 3; }
+      echo "== ic $c $m ok" | tee -a "$OUT/summary.log"
+    done
+  done ;;
 fetch)  # split tail (main; split2: two rounds) over cur (whole-register fetch + init registers + nested-level count + no round-3 staging) over fetch (the fetch alone) over HEAD (prev)
   run tests_fetch 900 $PYT -m gpu tests/test_gpu_parity.py tests/test_gpu_bench_path.py tests/test_gpu_jobs.py
   for rep in 1 2; do
