@@ -248,6 +248,15 @@ icache)  # instruction-cache counters of the staged instantiation on resident in
       echo "== ic $c $m ok" | tee -a "$OUT/summary.log"
     done
   done ;;
+copiers)  # copier workgroups per staged launch (AC_COPIER_WGS) at cfg3 / cfg4 / cfg5 and cfg2, x2
+  for rep in 1 2; do
+    for w in 16 32 64; do
+      for c in cfg3 cfg4 cfg5; do
+        run ${c}_cw${w}_$rep 300 env AC_COPIER_WGS=$w python3 bench.py --config $c --steps 20 --warmup 5 $BQ --no-kernel-leg
+      done
+      run stage_cw${w}_$rep 200 env AC_COPIER_WGS=$w $B
+    done
+  done ;;
 fetch)  # split tail (main; split2: two rounds) over cur (whole-register fetch + init registers + nested-level count + no round-3 staging) over fetch (the fetch alone) over HEAD (prev)
   run tests_fetch 900 $PYT -m gpu tests/test_gpu_parity.py tests/test_gpu_bench_path.py tests/test_gpu_jobs.py
   for rep in 1 2; do
