@@ -257,6 +257,25 @@ copiers)  # copier workgroups per staged launch (AC_COPIER_WGS) at cfg3 / cfg4 /
       run stage_cw${w}_$rep 200 env AC_COPIER_WGS=$w $B
     done
   done ;;
+wake)  # host pool woken at call entry (main) vs HEAD (prev): jobs tests, stage cfg2-cfg5 with stage traces, x2
+  run tests_wake 600 $PYT -m gpu tests/test_gpu_jobs.py tests/test_gpu_bench_path.py
+  for rep in 1 2; do
+    for v in main prev; do
+      L=$([ $v = main ] && echo "" || echo "APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so")
+      run stage_${v}_$rep 200 env $L AC_STAGE_TRACE=1 $B
+      for c in cfg3 cfg5 cfg4; do
+        run ${c}_${v}_$rep 300 env $L AC_STAGE_TRACE=1 python3 bench.py --config $c --steps 20 --warmup 5 $BQ --no-kernel-leg
+      done
+    done
+  done ;;
+wake2)  # pool pre-wake: cfg2 stage x3 and cfg5 x2 interleaved, main vs prev
+  for rep in 1 2 3; do
+    for v in main prev; do
+      L=$([ $v = main ] && echo "" || echo "APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so")
+      run stage_${v}_$rep 200 env $L AC_STAGE_TRACE=1 $B
+      [ $rep = 3 ] || run cfg5_${v}_$rep 300 env $L AC_STAGE_TRACE=1 python3 bench.py --config cfg5 --steps 20 --warmup 5 $BQ --no-kernel-leg
+    done
+  done ;;
 fetch)  # split tail (main; split2: two rounds) over cur (whole-register fetch + init registers + nested-level count + no round-3 staging) over fetch (the fetch alone) over HEAD (prev)
   run tests_fetch 900 $PYT -m gpu tests/test_gpu_parity.py tests/test_gpu_bench_path.py tests/test_gpu_jobs.py
   for rep in 1 2; do
