@@ -276,6 +276,16 @@ wake2)  # pool pre-wake: cfg2 stage x3 and cfg5 x2 interleaved, main vs prev
       [ $rep = 3 ] || run cfg5_${v}_$rep 300 env $L AC_STAGE_TRACE=1 python3 bench.py --config cfg5 --steps 20 --warmup 5 $BQ --no-kernel-leg
     done
   done ;;
+pub)  # progress records published by a pool worker while the caller is inside the launch (main) vs HEAD (prev)
+  run tests_pub 600 $PYT -m gpu tests/test_gpu_jobs.py tests/test_gpu_bench_path.py
+  for rep in 1 2 3; do
+    for v in main prev; do
+      L=$([ $v = main ] && echo "" || echo "APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so")
+      run stage_${v}_$rep 200 env $L $B
+      [ $rep = 3 ] || run cfg3_${v}_$rep 300 env $L python3 bench.py --config cfg3 --steps 20 --warmup 5 $BQ --no-kernel-leg
+    done
+  done
+  run stamps_staged 120 env APPROX_COUNTER_AMD_LIB=build/var/stamps/libapprox_counter_amd.so python3 tools/stage_stamps.py --calls 40 ;;
 fetch)  # split tail (main; split2: two rounds) over cur (whole-register fetch + init registers + nested-level count + no round-3 staging) over fetch (the fetch alone) over HEAD (prev)
   run tests_fetch 900 $PYT -m gpu tests/test_gpu_parity.py tests/test_gpu_bench_path.py tests/test_gpu_jobs.py
   for rep in 1 2; do
