@@ -286,6 +286,15 @@ pub)  # progress records published by a pool worker while the caller is inside t
     done
   done
   run stamps_staged 120 env APPROX_COUNTER_AMD_LIB=build/var/stamps/libapprox_counter_amd.so python3 tools/stage_stamps.py --calls 40 ;;
+ahead)  # LDS reads 5 / 6 bases ahead (ah5, ah6) vs 4 (main): kernel cfg2 / cfg3 / cfg5 x2
+  for rep in 1 2; do
+    for v in main ah5 ah6; do
+      L=$([ $v = main ] && echo "" || echo "APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so")
+      run ksweep_${v}_$rep 300 env $L python3 tools/kernel_sweep.py --sn 10000 --launches 300
+      run kcfg3_${v}_$rep 300 env $L python3 tools/kernel_sweep.py --sn 100000 --lim 2000 --launches 30 --warmup 10
+      run kcfg5_${v}_$rep 300 env $L python3 tools/kernel_sweep.py --sn 100000 --lim 1000 --k 22 --sl 150 --launches 30 --warmup 10
+    done
+  done ;;
 fetch)  # split tail (main; split2: two rounds) over cur (whole-register fetch + init registers + nested-level count + no round-3 staging) over fetch (the fetch alone) over HEAD (prev)
   run tests_fetch 900 $PYT -m gpu tests/test_gpu_parity.py tests/test_gpu_bench_path.py tests/test_gpu_jobs.py
   for rep in 1 2; do
