@@ -371,7 +371,11 @@ ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hi
             groups_live += (segs[i].n_kmers + cpw - 1) / cpw;
             max_nw = std::max<uint32_t>(max_nw, segs[i].sample.n_windows);
         }
-    const uint64_t s_base = std::max<uint64_t>(1, std::min<uint64_t>(32, resident / (64ull * std::max(1u, groups_live))));
+#ifndef AC_SUBQ_WAVES
+#define AC_SUBQ_WAVES 64  // waves per sub-queue (16 / 32 / 128 measured equal or slower, profiles/r05_m36)
+#endif
+    const uint64_t s_base = std::max<uint64_t>(
+        1, std::min<uint64_t>(32, resident / ((uint64_t)AC_SUBQ_WAVES * std::max(1u, groups_live))));
     uint64_t wave = 0;
     uint32_t groups_total = 0, qbegin = 0, acc_slots = 0;
     for (uint32_t i = 0; i < n; ++i) {

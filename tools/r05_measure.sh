@@ -295,6 +295,15 @@ ahead)  # LDS reads 5 / 6 bases ahead (ah5, ah6) vs 4 (main): kernel cfg2 / cfg3
       run kcfg5_${v}_$rep 300 env $L python3 tools/kernel_sweep.py --sn 100000 --lim 1000 --k 22 --sl 150 --launches 30 --warmup 10
     done
   done ;;
+subq)  # waves per sub-queue 64 (main) / 16 / 32 / 128: kernel cfg2 x2, cfg3, stage cfg2 x2
+  for rep in 1 2; do
+    for v in main sq16 sq32 sq128; do
+      L=$([ $v = main ] && echo "" || echo "APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so")
+      run ksweep_${v}_$rep 300 env $L python3 tools/kernel_sweep.py --sn 10000 --launches 300
+      [ $rep = 1 ] && run kcfg3_${v}_$rep 300 env $L python3 tools/kernel_sweep.py --sn 100000 --lim 2000 --launches 30 --warmup 10
+      run stage_${v}_$rep 200 env $L $B
+    done
+  done ;;
 fetch)  # split tail (main; split2: two rounds) over cur (whole-register fetch + init registers + nested-level count + no round-3 staging) over fetch (the fetch alone) over HEAD (prev)
   run tests_fetch 900 $PYT -m gpu tests/test_gpu_parity.py tests/test_gpu_bench_path.py tests/test_gpu_jobs.py
   for rep in 1 2; do
