@@ -25,6 +25,9 @@ def main():
     ap.add_argument("--sl", type=int, default=100)
     ap.add_argument("--launches", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=150)
+    ap.add_argument("--every", type=int, default=1,
+                    help="events around every n-th launch only (the bench's kernel leg: 5); the launches between "
+                         "run back to back")
     a = ap.parse_args()
     import torch
 
@@ -47,11 +50,13 @@ def main():
             for _ in range(a.warmup):
                 c.count_device(a.k, arr, stream=stream.cuda_stream, window_len=wlen)
             evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                   for _ in range(a.launches)]
-            for b, e in evs:
-                b.record(stream)
+                   for _ in range(0, a.launches, a.every)]
+            for i in range(a.launches):
+                if i % a.every == 0:
+                    evs[i // a.every][0].record(stream)
                 c.count_device(a.k, arr, stream=stream.cuda_stream, window_len=wlen)
-                e.record(stream)
+                if i % a.every == 0:
+                    evs[i // a.every][1].record(stream)
             torch.cuda.synchronize()
             c.check(stream=stream.cuda_stream)
             t = np.array([b.elapsed_time(e) for b, e in evs]) * 1e3

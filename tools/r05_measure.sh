@@ -304,6 +304,16 @@ subq)  # waves per sub-queue 64 (main) / 16 / 32 / 128: kernel cfg2 x2, cfg3, st
       run stage_${v}_$rep 200 env $L $B
     done
   done ;;
+spacing)  # the cfg2 kernel timed with events around every launch vs every 5th (back-to-back launches between), x3
+  for rep in 1 2 3; do
+    run every1_$rep 300 python3 tools/kernel_sweep.py --sn 10000 --launches 300 --every 1
+    run every5_$rep 300 python3 tools/kernel_sweep.py --sn 10000 --launches 300 --every 5
+  done ;;
+legs)  # the cfg2 kernel: bench.py's kernel leg vs tools/kernel_sweep.py (every 5th launch timed), same box, x2
+  for rep in 1 2; do
+    run bench_$rep 300 python3 bench.py $BQ
+    run sweep_$rep 300 python3 tools/kernel_sweep.py --sn 10000 --launches 100 --every 5
+  done ;;
 fetch)  # split tail (main; split2: two rounds) over cur (whole-register fetch + init registers + nested-level count + no round-3 staging) over fetch (the fetch alone) over HEAD (prev)
   run tests_fetch 900 $PYT -m gpu tests/test_gpu_parity.py tests/test_gpu_bench_path.py tests/test_gpu_jobs.py
   for rep in 1 2; do
