@@ -314,6 +314,12 @@ legs)  # the cfg2 kernel: bench.py's kernel leg vs tools/kernel_sweep.py (every 
     run bench_$rep 300 python3 bench.py $BQ
     run sweep_$rep 300 python3 tools/kernel_sweep.py --sn 10000 --launches 100 --every 5
   done ;;
+poll)  # shorter staging poll intervals (copier avail poll, gate) vs HEAD: cfg2 stage x4 interleaved
+  for rep in 1 2 3 4; do
+    for v in poll prev; do
+      run stage_${v}_$rep 200 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so $B
+    done
+  done ;;
 fetch)  # split tail (main; split2: two rounds) over cur (whole-register fetch + init registers + nested-level count + no round-3 staging) over fetch (the fetch alone) over HEAD (prev)
   run tests_fetch 900 $PYT -m gpu tests/test_gpu_parity.py tests/test_gpu_bench_path.py tests/test_gpu_jobs.py
   for rep in 1 2; do
