@@ -320,6 +320,11 @@ poll)  # shorter staging poll intervals (copier avail poll, gate) vs HEAD: cfg2 
       run stage_${v}_$rep 200 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so $B
     done
   done ;;
+cli)  # the drop-in CLI end to end (default vs --host-exact, identical files), 10^4 and 10^5 reads, x2
+  for rep in 1 2; do
+    run cli_10000_$rep 300 python3 tools/cli_e2e.py --reads 10000 --lim 500
+    run cli_100000_$rep 400 python3 tools/cli_e2e.py --reads 100000 --lim 2000
+  done ;;
 fetch)  # split tail (main; split2: two rounds) over cur (whole-register fetch + init registers + nested-level count + no round-3 staging) over fetch (the fetch alone) over HEAD (prev)
   run tests_fetch 900 $PYT -m gpu tests/test_gpu_parity.py tests/test_gpu_bench_path.py tests/test_gpu_jobs.py
   for rep in 1 2; do
