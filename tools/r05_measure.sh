@@ -325,6 +325,28 @@ cli)  # the drop-in CLI end to end (default vs --host-exact, identical files), 1
     run cli_10000_$rep 300 python3 tools/cli_e2e.py --reads 10000 --lim 500
     run cli_100000_$rep 400 python3 tools/cli_e2e.py --reads 100000 --lim 2000
   done ;;
+exact)  # exact count + selection on the GPU (row f1): cfg3 / cfg4 / cfg5 times and a cfg4 kernel trace
+  run exact_cfg3 300 python3 tools/bench_exact.py --reads 100000 --lim 2000 --no-host
+  run exact_cfg5 300 python3 tools/bench_exact.py --reads 100000 --sl 150 --k 22 --lim 1000 --no-host
+  run exact_cfg4 600 python3 tools/bench_exact.py --reads 1000000 --lim 500 --no-host
+  ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/exact_trace_cfg4" -o run -- \
+    python3 "$GRAFT_REPO_ROOT/tools/bench_exact.py" --reads 1000000 --lim 500 --no-host --steps 8 ) > "$OUT/exact_trace_cfg4.log" 2>&1 \
+    || { echo "exact trace failed"; exit 6; }
+  echo "== exact trace ok" | tee -a "$OUT/summary.log" ;;
+exact2)  # keys staged in LDS for coalesced stores (main) vs HEAD (prev): exact tests, cfg3 / cfg5 / cfg4 x2, cfg4 trace
+  run tests_exact 900 $PYT -m gpu tests/test_gpu_exact.py tests/test_gpu_cli.py
+  for rep in 1 2; do
+    for v in main prev; do
+      L=$([ $v = main ] && echo "" || echo "APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so")
+      run ex3_${v}_$rep 300 env $L python3 tools/bench_exact.py --reads 100000 --lim 2000 --no-host
+      run ex5_${v}_$rep 300 env $L python3 tools/bench_exact.py --reads 100000 --sl 150 --k 22 --lim 1000 --no-host
+      run ex4_${v}_$rep 600 env $L python3 tools/bench_exact.py --reads 1000000 --lim 500 --no-host
+    done
+  done
+  ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/exact_trace_cfg4" -o run -- \
+    python3 "$GRAFT_REPO_ROOT/tools/bench_exact.py" --reads 1000000 --lim 500 --no-host --steps 8 ) > "$OUT/exact_trace_cfg4.log" 2>&1 \
+    || { echo "exact trace failed"; exit 6; }
+  echo "== exact trace ok" | tee -a "$OUT/summary.log" ;;
 fetch)  # split tail (main; split2: two rounds) over cur (whole-register fetch + init registers + nested-level count + no round-3 staging) over fetch (the fetch alone) over HEAD (prev)
   run tests_fetch 900 $PYT -m gpu tests/test_gpu_parity.py tests/test_gpu_bench_path.py tests/test_gpu_jobs.py
   for rep in 1 2; do
