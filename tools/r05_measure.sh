@@ -347,6 +347,17 @@ exact2)  # keys staged in LDS for coalesced stores (main) vs HEAD (prev): exact 
     python3 "$GRAFT_REPO_ROOT/tools/bench_exact.py" --reads 1000000 --lim 500 --no-host --steps 8 ) > "$OUT/exact_trace_cfg4.log" 2>&1 \
     || { echo "exact trace failed"; exit 6; }
   echo "== exact trace ok" | tee -a "$OUT/summary.log" ;;
+ahead2)  # copy-ahead window 16 / 64 chunks vs 32 (prev = HEAD): cfg2 stage x3, cfg3 / cfg4 once
+  for rep in 1 2 3; do
+    for v in prev ca16 ca64; do
+      run stage_${v}_$rep 200 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so $B
+    done
+  done
+  for v in prev ca16 ca64; do
+    for c in cfg3 cfg4; do
+      run ${c}_${v} 300 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so python3 bench.py --config $c --steps 20 --warmup 5 $BQ --no-kernel-leg
+    done
+  done ;;
 fetch)  # split tail (main; split2: two rounds) over cur (whole-register fetch + init registers + nested-level count + no round-3 staging) over fetch (the fetch alone) over HEAD (prev)
   run tests_fetch 900 $PYT -m gpu tests/test_gpu_parity.py tests/test_gpu_bench_path.py tests/test_gpu_jobs.py
   for rep in 1 2; do
