@@ -317,7 +317,7 @@ struct BlockAppender {
         if (threadIdx.x == 0) *lbase = atomicAdd(n, (unsigned long long)m);
         __syncthreads();
         const uint64_t b = *lbase;
-        for (uint32_t i = threadIdx.x; i < m; i += EXACT_THREADS)
+        for (uint32_t i = threadIdx.x; i < m; i += blockDim.x)
             if (b + i < cap) {
                 keys[b + i] = lk[i];
                 cnts[b + i] = lc[i];
@@ -949,20 +949,27 @@ __device__ __forceinline__ float key_complexity(uint64_t key, uint32_t k) { retu
 // One workgroup per bucket: count its keys in LDS, then filter, histogram and
 // list them like exact_scan_kernel (the all-T k-mer whose key + 1 wraps to 0 --
 // the 16-mer of 32-bit keys, the 32-mer of 64-bit keys -- is tallied in
-// special[0] and handled by part_special_kernel).  LDS is kept at ~46 KB
-// (32-bit keys: three workgroups per CU) / ~62 KB (64-bit keys: two): the
+// special[0] and handled by part_special_kernel).  LDS is kept at ~52 KB
+// (32-bit keys: three workgroups per CU) / ~68 KB (64-bit keys: two): the
 // table, a 32-bin histogram of the counts 1..32 written out per bucket (phist,
 // summed by part_hist_reduce_kernel: thousands of buckets adding into the same
 // few global bins would serialise), larger counts straight to the global
 // histogram, and a small appender.  An adapter k-mer fills most of its bucket
 // with one key: a wave first merges the lanes holding its first lane's key, so
 // the LDS add on that slot is one per wave instead of one per lane.
-constexpr uint32_t COUNT_APPEND = 512;
+#ifndef AC_COUNT_THREADS
+#define AC_COUNT_THREADS 512
+#endif
+// threads per counting workgroup: 512 (24 / 16 waves per CU) against 256 and 1024 measured
+// 12 % faster at cfg4 / cfg5, 7 % at cfg3 (profiles/r05_m52): the inserts' dependent LDS
+// read -> CAS -> add chains want more waves, the table's size caps the workgroups per CU.
+constexpr uint32_t COUNT_THREADS = AC_COUNT_THREADS;
+constexpr uint32_t COUNT_APPEND = 2 * COUNT_THREADS;
 
 constexpr uint32_t COUNT_BATCH = 8;  // keys per thread loaded together (one memory latency per batch)
 
 template <class K>
-__global__ __launch_bounds__(EXACT_THREADS) void part_count_kernel(ExactArgs a) {
+__global__ __launch_bounds__(COUNT_THREADS) void part_count_kernel(ExactArgs a) {
     constexpr uint32_t SLOTS = EXACT_BUCKET_SLOTS;
     __shared__ K tk[SLOTS];  // key + 1; 0 = empty
     __shared__ uint32_t tc[SLOTS];
@@ -977,7 +984,7 @@ __global__ __launch_bounds__(EXACT_THREADS) void part_count_kernel(ExactArgs a) 
     const K* parts = (const K*)a.parts;
     const uint32_t t = threadIdx.x;
     const uint32_t NB = 1u << a.nb_log2;
-    for (uint32_t i = t; i < SLOTS; i += EXACT_THREADS) {
+    for (uint32_t i = t; i < SLOTS; i += COUNT_THREADS) {
         tk[i] = 0;
         tc[i] = 0;
     }
@@ -995,17 +1002,17 @@ __global__ __launch_bounds__(EXACT_THREADS) void part_count_kernel(ExactArgs a) 
     auto load_batch = [&](K* dst, uint32_t i0, uint32_t hi) __attribute__((always_inline)) {
 #pragma unroll
         for (uint32_t r = 0; r < COUNT_BATCH; ++r) {
-            const uint32_t i = i0 + r * EXACT_THREADS + t;
+            const uint32_t i = i0 + r * COUNT_THREADS + t;
             dst[r] = i < hi ? parts[i] : (K)0;
         }
     };
     if (blockIdx.x < NB) load_batch(nxt, a.bstart[blockIdx.x], a.bstart[blockIdx.x + 1]);
     for (uint32_t b = blockIdx.x; b < NB; b += gridDim.x) {
-        for (uint32_t i = t; i < EXACT_PHIST; i += EXACT_THREADS) hist[i] = 0;
+        for (uint32_t i = t; i < EXACT_PHIST; i += COUNT_THREADS) hist[i] = 0;
         __syncthreads();
         const uint32_t lo = a.bstart[b], hi = a.bstart[b + 1];
         uint32_t allt = 0;
-        for (uint32_t i0 = lo; i0 < hi; i0 += EXACT_THREADS * COUNT_BATCH) {  // block-uniform batches
+        for (uint32_t i0 = lo; i0 < hi; i0 += COUNT_THREADS * COUNT_BATCH) {  // block-uniform batches
             K kb[COUNT_BATCH];
             if (i0 == lo) {
 #pragma unroll
@@ -1015,7 +1022,7 @@ __global__ __launch_bounds__(EXACT_THREADS) void part_count_kernel(ExactArgs a) 
             }
 #pragma unroll
             for (uint32_t r = 0; r < COUNT_BATCH; ++r) {
-                const uint32_t i = i0 + r * EXACT_THREADS + t;
+                const uint32_t i = i0 + r * COUNT_THREADS + t;
                 const bool have = i < hi;
                 const K key = kb[r], stored = (K)(key + 1u);
                 // lanes holding the wave's first key: one add of their number
@@ -1061,7 +1068,7 @@ __global__ __launch_bounds__(EXACT_THREADS) void part_count_kernel(ExactArgs a) 
         __syncthreads();
         uint32_t ones = 0;
         const uint32_t m = n_occ;
-        for (uint32_t s0 = 0; s0 < m; s0 += EXACT_THREADS) {  // block-uniform trips over the claimed slots
+        for (uint32_t s0 = 0; s0 < m; s0 += COUNT_THREADS) {  // block-uniform trips over the claimed slots
             uint32_t c = 0;
             uint64_t key = 0;
             if (s0 + t < m) {
@@ -1082,13 +1089,13 @@ __global__ __launch_bounds__(EXACT_THREADS) void part_count_kernel(ExactArgs a) 
             app.push(c && c >= a.list_min, key, c);
             // flush when the next trip's pushes might not fit (block-uniform test after a barrier)
             __syncthreads();
-            if (app_n + EXACT_THREADS > COUNT_APPEND) app.sync_flush(true);
+            if (app_n + COUNT_THREADS > COUNT_APPEND) app.sync_flush(true);
         }
         for (int off = 32; off; off >>= 1) ones += __shfl_xor(ones, off);
         if (__lane_id() == 0 && ones) atomicAdd(&hist[0], ones);
         __syncthreads();
         if (!a.emit_only)
-            for (uint32_t i = t; i < EXACT_PHIST; i += EXACT_THREADS) a.phist[(uint64_t)b * EXACT_PHIST + i] = hist[i];
+            for (uint32_t i = t; i < EXACT_PHIST; i += COUNT_THREADS) a.phist[(uint64_t)b * EXACT_PHIST + i] = hist[i];
         if (t == 0) n_occ = 0;
         // (the next bucket's first barrier orders these against its inserts)
     }
@@ -1096,20 +1103,29 @@ __global__ __launch_bounds__(EXACT_THREADS) void part_count_kernel(ExactArgs a) 
     if (t == 0 && n_allt && !a.emit_only) atomicAdd(&a.special[0], n_allt);
 }
 
-// hist[c] += sum over buckets of phist[bucket][c - 1], c = 1..EXACT_PHIST: one
-// workgroup per bin.
+// hist[c] += sum over buckets of phist[bucket][c - 1], c = 1..EXACT_PHIST.  A
+// workgroup reads whole rows (HRED_ROWS buckets = 1 KB per pass, coalesced),
+// every HRED_PASSES-th slab of them; thread t keeps bin t % EXACT_PHIST, the
+// rows are summed in LDS and each bin adds once per workgroup.  (One
+// workgroup per bin, reading 4 B of every 128, took 98 us at cfg4: r05_m53.)
+constexpr uint32_t HRED_ROWS = EXACT_THREADS / EXACT_PHIST;
+constexpr uint32_t HRED_PASSES = 16;
+static_assert(EXACT_THREADS % EXACT_PHIST == 0, "a pass covers whole rows");
+
 __global__ __launch_bounds__(EXACT_THREADS) void part_hist_reduce_kernel(ExactArgs a) {
-    __shared__ uint32_t red[EXACT_THREADS / 64];
-    const uint32_t NB = 1u << a.nb_log2, bin = blockIdx.x, t = threadIdx.x;
+    __shared__ uint32_t red[EXACT_THREADS];
+    const uint32_t t = threadIdx.x;
+    const uint64_t n = (uint64_t)EXACT_PHIST << a.nb_log2;
+    const uint64_t step = (uint64_t)gridDim.x * EXACT_THREADS;  // a multiple of EXACT_PHIST: the bin stays t's
     uint32_t sum = 0;
-    for (uint32_t b = t; b < NB; b += EXACT_THREADS) sum += a.phist[(uint64_t)b * EXACT_PHIST + bin];
-    for (int off = 32; off; off >>= 1) sum += __shfl_xor(sum, off);
-    if ((t & 63u) == 0) red[t >> 6] = sum;
+#pragma unroll 4
+    for (uint64_t i = (uint64_t)blockIdx.x * EXACT_THREADS + t; i < n; i += step) sum += a.phist[i];
+    red[t] = sum;
     __syncthreads();
-    if (t == 0) {
+    if (t < EXACT_PHIST) {
         uint32_t tot = 0;
-        for (uint32_t w = 0; w < EXACT_THREADS / 64; ++w) tot += red[w];
-        if (tot) atomicAdd(&a.hist[bin + 1u], tot);
+        for (uint32_t r = 0; r < HRED_ROWS; ++r) tot += red[r * EXACT_PHIST + t];
+        if (tot) atomicAdd(&a.hist[t + 1u], tot);
     }
 }
 
@@ -1131,12 +1147,14 @@ __global__ void part_special_kernel(ExactArgs a, uint64_t key) {
 
 template <class K>
 hipError_t part_count(const ExactArgs& a, hipStream_t stream) {
-    // persistent workgroups: three per CU for 32-bit keys (LDS ~46 KB each), two for 64-bit (~62 KB)
+    // persistent workgroups: three per CU for 32-bit keys (LDS ~52 KB each), two for 64-bit (~68 KB)
     const uint32_t per_cu = sizeof(K) == 4 ? 3u : 2u;
     const uint32_t grid = std::min<uint32_t>(1u << a.nb_log2, 256u * per_cu);
-    hipLaunchKernelGGL(part_count_kernel<K>, dim3(grid), dim3(EXACT_THREADS), 0, stream, a);
+    hipLaunchKernelGGL(part_count_kernel<K>, dim3(grid), dim3(COUNT_THREADS), 0, stream, a);
     if (!a.emit_only)
-        hipLaunchKernelGGL(part_hist_reduce_kernel, dim3(EXACT_PHIST), dim3(EXACT_THREADS), 0, stream, a);
+        hipLaunchKernelGGL(part_hist_reduce_kernel,
+                           dim3(std::max<uint32_t>(1u, (1u << a.nb_log2) / (HRED_ROWS * HRED_PASSES))),
+                           dim3(EXACT_THREADS), 0, stream, a);
     hipLaunchKernelGGL(part_special_kernel, dim3(1), dim3(1), 0, stream, a, (uint64_t)(K)~(K)0);
     return hipGetLastError();
 }

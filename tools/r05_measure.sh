@@ -347,6 +347,23 @@ exact2)  # keys staged in LDS for coalesced stores (main) vs HEAD (prev): exact 
     python3 "$GRAFT_REPO_ROOT/tools/bench_exact.py" --reads 1000000 --lim 500 --no-host --steps 8 ) > "$OUT/exact_trace_cfg4.log" 2>&1 \
     || { echo "exact trace failed"; exit 6; }
   echo "== exact trace ok" | tee -a "$OUT/summary.log" ;;
+exact3)  # 512-thread count kernel on main: exact + CLI GPU tests, then the exact part's times and cfg4 trace
+  run tests_exact 900 $PYT -m gpu tests/test_gpu_exact.py tests/test_gpu_cli.py
+  ;;
+count_threads)  # exact count kernel at 256 (prev = HEAD) / 512 / 1024 threads per workgroup: parity cfg3 / cfg5, times x2
+  for v in prev ct512 ct1024; do
+    L="APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so"
+    run par3_$v 300 env $L python3 tools/bench_exact.py --reads 100000 --lim 2000 --steps 3 --warmup 1
+    run par5_$v 300 env $L python3 tools/bench_exact.py --reads 100000 --sl 150 --k 22 --lim 1000 --steps 3 --warmup 1
+  done
+  for rep in 1 2; do
+    for v in prev ct512 ct1024; do
+      L="APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so"
+      run ex3_${v}_$rep 300 env $L python3 tools/bench_exact.py --reads 100000 --lim 2000 --no-host
+      run ex5_${v}_$rep 300 env $L python3 tools/bench_exact.py --reads 100000 --sl 150 --k 22 --lim 1000 --no-host
+      run ex4_${v}_$rep 600 env $L python3 tools/bench_exact.py --reads 1000000 --lim 500 --no-host
+    done
+  done ;;
 ahead2)  # copy-ahead window 16 / 64 chunks vs 32 (prev = HEAD): cfg2 stage x3, cfg3 / cfg4 once
   for rep in 1 2 3; do
     for v in prev ca16 ca64; do
