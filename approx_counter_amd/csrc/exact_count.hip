@@ -491,7 +491,8 @@ __device__ __forceinline__ uint32_t bucket_of(K key, uint32_t nb_log2) {
     return part_hash(key) >> (32u - nb_log2);
 }
 
-// Exclusive prefix of a block's values (thread t holds x); returns the total.
+// Exclusive prefix of a block's values (thread t of NT holds x); returns the total.
+template <uint32_t NT = EXACT_THREADS>
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t& excl, uint32_t* wsum) {
     const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
     uint32_t incl = x;
@@ -504,7 +505,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t& excl, 
     __syncthreads();
     uint32_t before = 0, total = 0;
 #pragma unroll
-    for (uint32_t w = 0; w < EXACT_THREADS / 64; ++w) {
+    for (uint32_t w = 0; w < NT / 64; ++w) {
         before += w < wv ? wsum[w] : 0u;
         total += wsum[w];
     }
@@ -555,20 +556,30 @@ __device__ __forceinline__ uint32_t wave_bin_add(uint32_t* cnt, uint32_t b) {
 // N flags once and rolls the rest (one 2-bit code and one N flag per step),
 // instead of gathering every position's words anew.
 constexpr uint32_t SEG_POS = 16;
-// Windows per keys workgroup: ~100-bp windows make 6 segments each, so 42 of
-// them fill the 256 threads once (16 windows left 62 % of the threads idle).
-constexpr uint32_t KEYS_WINDOWS = 42;
+// Threads and windows per keys workgroup: ~100-bp windows make 6 segments each,
+// so 42 windows per 256 threads fill them once (16 windows left 62 % of the
+// threads idle).  Every round takes its output range with one atomic on the
+// shared key counter, and those atomics serialise: at 256 threads the kernel
+// took 574 us at cfg4, 300 with block-private ranges (r05_m55); 1,024 threads
+// (a quarter of the atomics) 209 us, 512 307 (r05_m56).  64-bit keys stay at
+// 512: their LDS stage is twice as large (64 KB).
+template <class K>
+struct KeysShape {
+    static constexpr uint32_t THREADS = sizeof(K) == 4 ? 1024u : 512u;
+    static constexpr uint32_t WINDOWS = 42u * THREADS / 256u;
+};
 
 template <class K>
-__global__ __launch_bounds__(EXACT_THREADS) void part_keys_kernel(ExactArgs a) {
+__global__ __launch_bounds__(KeysShape<K>::THREADS) void part_keys_kernel(ExactArgs a) {
+    constexpr uint32_t KEYS_THREADS = KeysShape<K>::THREADS, KEYS_WINDOWS = KeysShape<K>::WINDOWS;
     __shared__ uint32_t wseg[KEYS_WINDOWS + 1];  // prefix sums of segments per window
-    __shared__ uint32_t wsum[EXACT_THREADS / 64];
+    __shared__ uint32_t wsum[KEYS_THREADS / 64];
     __shared__ unsigned long long base_sh;
     __shared__ uint32_t n_had, tot_sh;
     // A round's keys, staged at their block-local offsets, then stored with consecutive lanes on
     // consecutive keys: stored straight from the threads' 16-position runs, each store instruction
     // wrote 64 keys 64 B apart (603 us at cfg4 for 340 MB of keys, profiles/r05_m45).
-    __shared__ K stage[EXACT_THREADS * SEG_POS];
+    __shared__ K stage[KEYS_THREADS * SEG_POS];
     K* keys_out = (K*)a.keys;
     const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
     const uint32_t w0 = blockIdx.x * KEYS_WINDOWS;
@@ -584,7 +595,7 @@ __global__ __launch_bounds__(EXACT_THREADS) void part_keys_kernel(ExactArgs a) {
             nseg = (npos + SEG_POS - 1u) / SEG_POS;
         }
         uint32_t excl;
-        const uint32_t tot = block_excl_scan(nseg, excl, wsum);
+        const uint32_t tot = block_excl_scan<KEYS_THREADS>(nseg, excl, wsum);
         if (t < nw) wseg[t] = excl;
         if (t == 0) {
             wseg[nw] = tot;
@@ -597,7 +608,7 @@ __global__ __launch_bounds__(EXACT_THREADS) void part_keys_kernel(ExactArgs a) {
     const uint64_t kmask = (1ull << k) - 1ull;
     const K keymask = 2u * k >= 8u * sizeof(K) ? (K)~(K)0 : (K)(((K)1 << (2u * k)) - 1u);
     uint32_t had = 0;
-    for (uint32_t s0 = 0; s0 < total; s0 += EXACT_THREADS) {  // block-uniform rounds
+    for (uint32_t s0 = 0; s0 < total; s0 += KEYS_THREADS) {  // block-uniform rounds
         const uint32_t sg = s0 + t;
         K key[SEG_POS];
         uint32_t valid = 0, c = 0;
@@ -641,7 +652,7 @@ __global__ __launch_bounds__(EXACT_THREADS) void part_keys_kernel(ExactArgs a) {
         __syncthreads();
         if (t == 0) {
             uint32_t tot = 0;
-            for (uint32_t w = 0; w < EXACT_THREADS / 64; ++w) {
+            for (uint32_t w = 0; w < KEYS_THREADS / 64; ++w) {
                 const uint32_t x = wsum[w];
                 wsum[w] = tot;
                 tot += x;
@@ -657,7 +668,7 @@ __global__ __launch_bounds__(EXACT_THREADS) void part_keys_kernel(ExactArgs a) {
         __syncthreads();
         const uint64_t base = base_sh;
         const uint32_t tot = tot_sh;
-        for (uint32_t i = t; i < tot; i += EXACT_THREADS)
+        for (uint32_t i = t; i < tot; i += KEYS_THREADS)
             if (base + i < a.key_cap) keys_out[base + i] = stage[i];
         __syncthreads();  // wsum / base_sh / stage are reused by the next round
     }
@@ -1168,8 +1179,8 @@ hipError_t partitioned(const ExactArgs& a, hipStream_t stream) {
     if (a.s_log2 > a.nb_log2 || S > EXACT_MAX_SUPER || S < 32 || (NB >> a.s_log2) > EXACT_MAX_SUB || !a.n_chunks ||
         (uint64_t)a.n_chunks * CHUNK < a.key_cap || a.n_chunks2 < a.n_chunks + S)
         return hipErrorInvalidValue;
-    const uint32_t wblocks = (a.n_windows + KEYS_WINDOWS - 1) / KEYS_WINDOWS;
-    if (wblocks) hipLaunchKernelGGL(part_keys_kernel<K>, dim3(wblocks), dim3(EXACT_THREADS), 0, stream, a);
+    const uint32_t wblocks = (a.n_windows + KeysShape<K>::WINDOWS - 1) / KeysShape<K>::WINDOWS;
+    if (wblocks) hipLaunchKernelGGL(part_keys_kernel<K>, dim3(wblocks), dim3(KeysShape<K>::THREADS), 0, stream, a);
     hipLaunchKernelGGL(part_hist1_kernel<K>, dim3(a.n_chunks), dim3(EXACT_THREADS), 0, stream, a);
     const uint32_t slabs = (a.n_chunks + EXACT_SCAN_SLAB - 1) / EXACT_SCAN_SLAB;
     hipLaunchKernelGGL(part_scan1a_kernel, dim3(S / 32, slabs), dim3(EXACT_THREADS), 0, stream, a);

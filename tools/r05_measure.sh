@@ -347,6 +347,23 @@ exact2)  # keys staged in LDS for coalesced stores (main) vs HEAD (prev): exact 
     python3 "$GRAFT_REPO_ROOT/tools/bench_exact.py" --reads 1000000 --lim 500 --no-host --steps 8 ) > "$OUT/exact_trace_cfg4.log" 2>&1 \
     || { echo "exact trace failed"; exit 6; }
   echo "== exact trace ok" | tee -a "$OUT/summary.log" ;;
+keys_threads)  # keys kernel at 256 (prev = HEAD) / 512 / 1024 threads: parity cfg3 / cfg5, cfg4 traces
+  for v in prev kt512 kt1024; do
+    L="APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so"
+    run par3_$v 300 env $L python3 tools/bench_exact.py --reads 100000 --lim 2000 --steps 3 --warmup 1
+    run par5_$v 300 env $L python3 tools/bench_exact.py --reads 100000 --sl 150 --k 22 --lim 1000 --steps 3 --warmup 1
+    run ex5_$v 300 env $L python3 tools/bench_exact.py --reads 100000 --sl 150 --k 22 --lim 1000 --no-host
+    ( cd /tmp && export TMPDIR=/tmp APPROX_COUNTER_AMD_LIB="$GRAFT_REPO_ROOT/build/var/$v/libapprox_counter_amd.so" && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/keys_$v" -o run -- \
+      python3 "$GRAFT_REPO_ROOT/tools/bench_exact.py" --reads 1000000 --lim 500 --no-host --steps 8 ) > "$OUT/keys_$v.log" 2>&1 \
+      || { echo "keys trace $v failed"; exit 6; }
+  done ;;
+keysdiag)  # keys kernel with block-private output ranges (timing diagnostic, wrong downstream) vs main: cfg4 traces
+  for v in main kdiag; do
+    L=$([ $v = main ] && echo "approx_counter_amd/lib/libapprox_counter_amd.so" || echo "build/var/$v/libapprox_counter_amd.so")
+    ( cd /tmp && export TMPDIR=/tmp APPROX_COUNTER_AMD_LIB="$GRAFT_REPO_ROOT/$L" && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/keys_$v" -o run -- \
+      python3 "$GRAFT_REPO_ROOT/tools/bench_exact.py" --reads 1000000 --lim 500 --no-host --steps 8 ) > "$OUT/keys_$v.log" 2>&1 \
+      || { echo "keys trace $v failed"; exit 6; }
+  done ;;
 exact3)  # 512-thread count kernel on main: exact + CLI GPU tests, then the exact part's times and cfg4 trace
   run tests_exact 900 $PYT -m gpu tests/test_gpu_exact.py tests/test_gpu_cli.py
   ;;
