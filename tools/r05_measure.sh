@@ -347,6 +347,18 @@ exact2)  # keys staged in LDS for coalesced stores (main) vs HEAD (prev): exact 
     python3 "$GRAFT_REPO_ROOT/tools/bench_exact.py" --reads 1000000 --lim 500 --no-host --steps 8 ) > "$OUT/exact_trace_cfg4.log" 2>&1 \
     || { echo "exact trace failed"; exit 6; }
   echo "== exact trace ok" | tee -a "$OUT/summary.log" ;;
+chunk64)  # 64-KB partition chunks (ch64) vs 32 KB (prev = HEAD): exact tests on ch64, parity cfg3 / cfg5, cfg4 x2 + traces
+  run tests_ch64 900 env APPROX_COUNTER_AMD_LIB=build/var/ch64/libapprox_counter_amd.so $PYT -m gpu tests/test_gpu_exact.py
+  for v in prev ch64; do
+    L="APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so"
+    run par3_$v 300 env $L python3 tools/bench_exact.py --reads 100000 --lim 2000 --steps 3 --warmup 1
+    run par5_$v 300 env $L python3 tools/bench_exact.py --reads 100000 --sl 150 --k 22 --lim 1000 --steps 3 --warmup 1
+    run ex4_${v}_1 300 env $L python3 tools/bench_exact.py --reads 1000000 --lim 500 --no-host
+    run ex4_${v}_2 300 env $L python3 tools/bench_exact.py --reads 1000000 --lim 500 --no-host
+    ( cd /tmp && export TMPDIR=/tmp APPROX_COUNTER_AMD_LIB="$GRAFT_REPO_ROOT/build/var/$v/libapprox_counter_amd.so" && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/tr_$v" -o run -- \
+      python3 "$GRAFT_REPO_ROOT/tools/bench_exact.py" --reads 1000000 --lim 500 --no-host --steps 8 ) > "$OUT/tr_$v.log" 2>&1 \
+      || { echo "trace $v failed"; exit 6; }
+  done ;;
 sub_log2)  # 64 (prev = HEAD) / 128 / 256 buckets per super-bucket: parity cfg3 / cfg5, exact tests on sub8, cfg4 traces
   run tests_sub8 900 env APPROX_COUNTER_AMD_LIB=build/var/sub8/libapprox_counter_amd.so $PYT -m gpu tests/test_gpu_exact.py
   for v in prev sub7 sub8; do
