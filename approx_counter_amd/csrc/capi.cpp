@@ -342,6 +342,11 @@ ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hi
             return fail(ctx, AC_ERR_INVALID, "equal windows reach past n_bases");
         if (s.sample.n_bases % 32 || s.sample.n_bases >= AC_MAX_IMAGE_BASES)
             return fail(ctx, AC_ERR_INVALID, "sample n_bases must be a multiple of 32 below 2^34");
+        // The count hand-off adds (1 << 32) + sum into 64-bit slots (wm_count.hip): a candidate's sum,
+        // at most 3 per window, must stay below 2^32 or its carry would count as an arrival and the
+        // slot would never see its last workgroup.
+        if (s.n_kmers && 3ull * s.sample.n_windows >= (1ull << 32))
+            return fail(ctx, AC_ERR_INVALID, "a segment of 2^32 / 3 windows or more: its counts would overflow");
         const uint32_t groups = (s.n_kmers + cpw - 1) / cpw;
         items += (uint64_t)groups * s.sample.n_windows;
     }

@@ -142,6 +142,18 @@ def cpu_share():
     return n, quota
 
 
+def cgroup_cpu_stat():
+    """cgroup v2 cpu.stat (nr_periods, nr_throttled, throttled_usec, usage_usec ...) as ints, {} if unreadable."""
+    out = {}
+    try:
+        for ln in open("/sys/fs/cgroup/cpu.stat"):
+            key, v = ln.split()
+            out[key] = int(v)
+    except (OSError, ValueError):
+        pass
+    return out
+
+
 def cpu_baseline(wl, k, seconds):
     """The oracle's OpenMP Myers restatement (kind "port": the reference's SeqAn
     FM-index path cannot be built here) on this host's cores: the
@@ -398,7 +410,8 @@ def main():
             allreduce_by = "library (ac_allreduce_counts, RCCL)"
         except Exception as exc:  # noqa: BLE001 -- reported on the line, the run continues on torch's RCCL
             print(f"[bench] library RCCL communicator unavailable ({exc}); using torch.distributed", file=sys.stderr)
-            allreduce_by = f"torch.distributed RCCL (library communicator failed: {exc})"
+            allreduce_by = (f"torch.distributed RCCL (library communicator failed: {exc})" if world > 1 else
+                            f"none: one rank and no library communicator ({exc}); the step skips the all-reduce")
     elif world > 1:
         allreduce_by = f"torch.distributed {backend} on host copies (rehearsal)"
 
@@ -412,14 +425,17 @@ def main():
             if backend == "nccl":
                 if allreduce_by.startswith("library"):
                     counter.allreduce_counts(d_counts, stream=stream.cuda_stream)  # RCCL over xGMI
-                else:
+                elif world > 1:
                     dist.all_reduce(d_counts)  # torch's RCCL, on the current stream
+                # (world 1 without the library communicator: no process group, so no all-reduce;
+                # the line's `allreduce` field says so)
                 h_counts.copy_(d_counts, non_blocking=True)
                 stream.synchronize()
             else:
                 stream.synchronize()
                 host = d_counts.cpu()
-                dist.all_reduce(host)
+                if world > 1:
+                    dist.all_reduce(host)
                 h_counts.copy_(host)
 
     for _ in range(args.warmup):
@@ -434,6 +450,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    cg0 = cgroup_cpu_stat()  # CPU-quota throttling over the timed steps
     t0 = time.perf_counter()
     marks = []
     for _ in range(args.steps):
@@ -443,6 +460,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    cg1 = cgroup_cpu_stat()
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -493,6 +511,13 @@ def main():
             out["step_ms"] = {"min": float(d.min()), "p50": float(np.median(d)), "p99": float(np.percentile(d, 99)),
                               "p99.9": float(np.percentile(d, 99.9)), "max": float(d.max())}
         out["stage_cold_call_ms"] = cold_ms
+        if cg1:
+            dl = {key: cg1[key] - cg0.get(key, 0) for key in ("nr_periods", "nr_throttled", "throttled_usec", "usage_usec")
+                  if key in cg1}
+            out["cgroup_cpu"] = {**dl, "cpus_used_per_wall_s": dl.get("usage_usec", 0) / 1e6 / elapsed,
+                                 "quota_cpus": cpu_share()[1],
+                                 "note": "rank 0's cgroup cpu.stat deltas over the timed steps: a throttled period "
+                                         "stalls every thread of the cgroup until the next 100 ms period"}
         out["host_pool"] = {"participants": pool_participants, "cpus": _ranges(pool_cpus),
                             "note": "rank 0's pack pool as it ran the timed steps (read after the first stage call "
                                     "made it): GPU-local CPUs split among the local ranks, at most its share of the "

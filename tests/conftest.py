@@ -10,6 +10,7 @@ if ROOT not in sys.path:
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device)")
+    config.addinivalue_line("markers", "slow: CPU tests at BASELINE sizes (quick suite: -m 'not gpu and not slow')")
 
 
 @pytest.fixture(scope="session")

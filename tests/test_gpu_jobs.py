@@ -419,6 +419,29 @@ def test_image_size_limit_rejected(counter):
     assert np.array_equal(seg.counts_numpy(), oracle.count_myers(16, kmers, wins, 16))
 
 
+def test_window_count_limit_rejected(counter):
+    """The count hand-off keeps a candidate's sum (<= 3 per window) in 32 bits beside the arrival
+    count: a segment of 2^32 / 3 windows or more is refused before any launch (AC_ERR_INVALID);
+    one window fewer passes the check (here: empty equal windows, so nothing reaches the kernel's
+    image).  ADVICE r5."""
+    import ctypes
+
+    kmers, wins = cases.planted_case(23, 16, 64, 8, win_len=(100, 100))
+    seg = ac.DeviceSegment.upload(kmers, ac.pack_windows(wins))
+    limit = (1 << 32) // 3 + 1  # 3 * limit >= 2^32 > 3 * (limit - 1)
+    seg.n_windows = limit
+    arr = ac.ApproxCounter.segment_array([seg])
+    wl = np.zeros(1, np.uint32)  # length-0 windows: every one at base 0, inside any image
+    L = counter._L
+    st = L.ac_error_count_device_equal(counter.handle, 16, arr, wl.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+                                       1, None)
+    assert st == 1 and "2^32 / 3" in L.ac_last_error(counter.handle).decode()
+    seg.n_windows = len(wins)  # the context still counts afterwards
+    counter.count_device(16, [seg])
+    counter.check()
+    assert np.array_equal(seg.counts_numpy(), oracle.count_myers(16, kmers, wins, 16))
+
+
 def test_large_call_early_launch_copier_workgroups():
     """A large call (700k windows: 22 MB of staging region, ~5,500 chunks, far more than
     half the workgroups) takes the early launch in one part since round 4: a few copier

@@ -36,6 +36,7 @@ def test_dense_restatement_is_the_loop_one(k):
     assert host_ref.rank_dense(uk, c, 0, 2, k) == host_ref.get_solid_kmers(exp, 2, k)
 
 
+@pytest.mark.slow  # (~40 s and a few GB for cfg4: out of the quick suite, in the full CPU suite)
 @pytest.mark.parametrize("cfg", [dict(k=16, n=1_000_000, L=100, lim=500), dict(k=22, n=100_000, L=151, lim=1000)],
                          ids=["cfg4", "cfg5"])
 def test_host_stages_full_scale_vs_oracle(cfg):
@@ -52,6 +53,7 @@ def test_host_stages_full_scale_vs_oracle(cfg):
     assert got[0][1] > cfg["n"] // 4  # the planted adapter's k-mers lead
 
 
+@pytest.mark.slow
 def test_host_stages_full_scale_solid_and_forbidden():
     """cfg5's sample in solid mode (-sk) with a forbidden set (-fk) taken from its own top list."""
     from tools.synth import make_windows_fast

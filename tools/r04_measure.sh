@@ -1,4 +1,6 @@
 #!/bin/bash
+# HISTORICAL: the round-4 batch as it ran.  Parts naming AC_ARM_US (armed launches) or AC_SLOT_STREAMS
+# measure options removed in round 5 (ABI 6): on today's library both arms run the same code.
 # Round-4 measurement batch on the GPU box (one box acquisition per call).  Every step has its
 # own time limit; a test failure (rc 1) lets the next step run, anything else stops the batch.
 # usage: tools/r04_measure.sh OUTDIR part...

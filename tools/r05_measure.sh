@@ -2,8 +2,9 @@
 # Round-5 measurement batch on the GPU box (one box acquisition per call).  Every step has its
 # own time limit; a test failure (rc 1) lets the next step run, anything else stops the batch.
 # usage: tools/r05_measure.sh OUTDIR part...
-#   slots     AC_SLOT_STREAMS=1 vs default: cfg2 stage x3 interleaved, cfg3 / cfg5 / cfg4 once each,
-#             and the jobs tests on two slot streams
+#   slots     HISTORICAL (round 5, profiles/r05_m1): AC_SLOT_STREAMS=1 vs default.  The slot streams were
+#             removed after that run, so the variable is no longer read and both arms now run the same
+#             code; the part refuses to run rather than log a meaningless A/B.
 #   long      2,000 cfg2 steps with the host pool at 16 / 15 / 14 participants (step-time tail)
 #   stamps    per-wave timelines of the resident cfg2 launch (-DAC_STAMPS build in build/var/stamps)
 #   suite     the whole -m gpu suite
@@ -31,15 +32,7 @@ B="python3 bench.py --steps 400 --warmup 20 --no-cpu-baseline --no-pipelined --n
 for part in "$@"; do
 case $part in
 slots)
-  for rep in 1 2 3; do
-    run ab_one_$rep 120 $B
-    run ab_slots_$rep 120 env AC_SLOT_STREAMS=1 $B
-  done
-  for c in cfg3 cfg5 cfg4; do
-    run ab_one_$c 200 python3 bench.py --config $c --steps 20 --warmup 5 $BQ --no-kernel-leg
-    run ab_slots_$c 200 env AC_SLOT_STREAMS=1 python3 bench.py --config $c --steps 20 --warmup 5 $BQ --no-kernel-leg
-  done
-  run tests_jobs_slots 400 env AC_SLOT_STREAMS=1 $PYT -m gpu tests/test_gpu_jobs.py tests/test_gpu_bench_path.py ;;
+  echo "slots: historical A/B of the removed AC_SLOT_STREAMS (profiles/r05_m1); nothing to compare now" | tee -a "$OUT/summary.log" ;;
 long)
   for t in 16 15 14; do
     run long_t$t 200 env AC_HOST_THREADS=$t python3 bench.py --steps 2000 --warmup 20 $BQ --no-kernel-leg

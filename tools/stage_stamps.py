@@ -26,8 +26,8 @@ def main():
     ap.add_argument("--lim", type=int, default=500)
     ap.add_argument("--calls", type=int, default=60)
     ap.add_argument("--t0", choices=("entry", "progress"), default="entry",
-                    help="progress: time from segment 0's poller first seeing the call (armed launches: the next "
-                         "call's kernel overwrites the entry stamps while it waits, so read with a long AC_ARM_US)")
+                    help="progress: time from segment 0's poller first seeing the call's first progress record "
+                         "(round 4's armed launches and their AC_ARM_US were removed in round 5)")
     a = ap.parse_args()
     import approx_counter_amd as ac
     from approx_counter_amd import _lib
