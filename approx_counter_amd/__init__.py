@@ -6,8 +6,8 @@ include/approx_counter_amd.h; this package is the host-side mirror of the
 reference interface for that path (see counter.error_count).
 """
 from .counter import (ApproxCounter, DeviceSegment, Dna5Sample, Jobs, PackedSample, error_count,
-                      pack_windows, to_dna5)
+                      pack_windows, pinned_copy, pinned_empty, to_dna5)
 from ._lib import ApproxCounterError
 
 __all__ = ["ApproxCounter", "ApproxCounterError", "DeviceSegment", "Dna5Sample", "Jobs", "PackedSample",
-           "error_count", "pack_windows", "to_dna5"]
+           "error_count", "pack_windows", "pinned_copy", "pinned_empty", "to_dna5"]

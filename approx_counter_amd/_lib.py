@@ -138,6 +138,11 @@ def load():
     if hasattr(L, "ac_idle"):  # (ABI >= 5; A/B builds of older ABIs lack it)
         L.ac_idle.argtypes = [vp]
         L.ac_idle.restype = ctypes.c_int
+    if hasattr(L, "ac_host_alloc"):  # (ABI >= 7; A/B builds of older ABIs lack it)
+        L.ac_host_alloc.argtypes = [ctypes.c_size_t, ctypes.POINTER(vp)]
+        L.ac_host_alloc.restype = ctypes.c_int
+        L.ac_host_free.argtypes = [vp]
+        L.ac_host_free.restype = ctypes.c_int
     L.ac_exact_path.argtypes = [vp]
     L.ac_exact_path.restype = ctypes.c_int
     pint = ctypes.POINTER(ctypes.c_int)

@@ -108,6 +108,38 @@ def pack_windows(windows) -> PackedSample:
     return PackedSample(codes, nmask, out_start[: len(arrs)], out_len[: len(arrs)], n_bases)
 
 
+class _PinnedBlock:
+    """One ac_host_alloc block, released when the last array viewing it goes (numpy keeps this
+    object as the arrays' base)."""
+
+    def __init__(self, nbytes: int):
+        L = _lib.load()
+        p = ctypes.c_void_p()
+        check(L.ac_host_alloc(max(int(nbytes), 1), ctypes.byref(p)))
+        self._L, self.ptr, self.nbytes = L, p.value, max(int(nbytes), 1)
+        self.__array_interface__ = {"shape": (self.nbytes,), "typestr": "|u1", "data": (self.ptr, False),
+                                    "version": 3}
+
+    def __del__(self):
+        if getattr(self, "ptr", None):
+            self._L.ac_host_free(ctypes.c_void_p(self.ptr))
+            self.ptr = None
+
+
+def pinned_empty(n: int, dtype) -> np.ndarray:
+    """An uninitialised array of n elements in pinned, device-mapped host memory (ac_host_alloc)."""
+    dt = np.dtype(dtype)
+    return np.asarray(_PinnedBlock(n * dt.itemsize)).view(dt)[:n]
+
+
+def pinned_copy(a) -> np.ndarray:
+    """A copy of `a` in ac_host_alloc memory."""
+    a = np.ascontiguousarray(a)
+    out = pinned_empty(max(a.size, 1), a.dtype)[: a.size]
+    out[...] = a.reshape(-1)
+    return out.reshape(a.shape)
+
+
 class Dna5Sample:
     """A sample as errorCount receives it: a StringSet<Dna5String>
     (approx_counter.cpp:38), i.e. Dna5 ordinal bytes concatenated, with each
@@ -140,6 +172,11 @@ class Dna5Sample:
             offset[1:] = np.cumsum(length[:-1], dtype=np.uint64)
         bases = np.concatenate(arrs) if arrs and length.sum() else np.zeros(1, np.uint8)
         return cls(bases, offset, length)
+
+    def pinned(self) -> "Dna5Sample":
+        """The same sample with its bytes and offsets in ac_host_alloc memory: ac_error_count_jobs
+        then packs it on the device when its windows have one length of 1..256 bases."""
+        return Dna5Sample(pinned_copy(self.bases), pinned_copy(self.offset), pinned_copy(self.length))
 
     def subset(self, lo: int, hi: int) -> "Dna5Sample":
         """Windows [lo, hi) (a shard), sharing the bases."""

@@ -19,6 +19,7 @@
 #include <string>
 #include <thread>
 #include <memory>
+#include <mutex>
 #include <vector>
 
 #include "approx_counter_amd.h"
@@ -292,6 +293,11 @@ struct StageLaunch {
     uint32_t tag = 0;              // tagged completion (wm_count.h LaunchArgs::tag)
     uint64_t* grp_err = nullptr;   // its per-group error words (device-visible pinned address)
     uint32_t copiers = 0;          // copier workgroups (wm_count.h LaunchArgs::copier_wgs; 0: nothing to stage)
+    // device packing (wm_count.h SegDev::dp_*): the segment's Dna5 bytes and window offsets in
+    // pinned host memory, device-visible addresses; dp_src = NULL: the host packed the segment
+    const uint8_t* dp_src[AC_MAX_SEGS] = {};
+    const uint64_t* dp_off[AC_MAX_SEGS] = {};
+    uint32_t dp_bytes[AC_MAX_SEGS] = {};
 };
 
 // Who stages a staged launch (wm_count.h LaunchArgs::copier_wgs): a few copier workgroups stage
@@ -401,6 +407,9 @@ ac_status launch(ac_ctx* ctx, uint32_t k, const ac_segment* segs, uint32_t n, hi
             d.stage_dst = stage->dst[i];
             d.stage_chunks = stage->chunks[i];
             d.stage_codes_off = stage->codes_off[i];
+            d.dp_src = stage->dp_src[i];
+            d.dp_off = stage->dp_off[i];
+            d.dp_src_bytes = stage->dp_bytes[i];
         }
         d.n_kmers = s.n_kmers;
         d.n_windows = s.sample.n_windows;
@@ -1424,8 +1433,77 @@ int ac_plan_host_cpus(const char* const* rank_cpulists, int n_ranks, int rank, c
 }  // extern "C"
 
 // ---------------------------------------------------------------------------
+// Pinned host blocks (ac_host_alloc): a sample whose Dna5 bytes and window offsets lie
+// in them is read by the count kernel itself (device packing), so a jobs call does no per-window host
+// work beyond the length scan.  Process-wide: one registry for every context and device.
+namespace {
+struct HostBlock {
+    char* h = nullptr;
+    size_t n = 0;
+    char* d = nullptr;  // device-visible address of h
+};
+std::mutex g_blocks_m;
+std::vector<HostBlock> g_blocks;
+
+// The block holding [p, p + bytes) (bytes >= 1), if any.
+bool find_block(const void* p, size_t bytes, HostBlock* out) {
+    const char* c = (const char*)p;
+    std::lock_guard<std::mutex> lk(g_blocks_m);
+    for (const HostBlock& b : g_blocks)
+        if (c >= b.h && c < b.h + b.n && bytes <= (size_t)(b.h + b.n - c)) {
+            *out = b;
+            return true;
+        }
+    return false;
+}
+}  // namespace
+
+extern "C" {
+ac_status ac_host_alloc(size_t bytes, void** out) {
+    if (!out) return fail(nullptr, AC_ERR_INVALID, "out is NULL");
+    *out = nullptr;
+    HostBlock b;
+    b.n = bytes ? bytes : 16;
+    hipError_t e = hipHostMalloc((void**)&b.h, b.n, hipHostMallocDefault);
+    if (e != hipSuccess) return hip_fail(nullptr, e, "hipHostMalloc");
+    e = hipHostGetDevicePointer((void**)&b.d, b.h, 0);
+    if (e != hipSuccess) {
+        (void)hipHostFree(b.h);
+        return hip_fail(nullptr, e, "hipHostGetDevicePointer");
+    }
+    {
+        std::lock_guard<std::mutex> lk(g_blocks_m);
+        g_blocks.push_back(b);
+    }
+    *out = b.h;
+    return AC_OK;
+}
+
+ac_status ac_host_free(void* p) {
+    if (!p) return AC_OK;
+    HostBlock b;
+    {
+        std::lock_guard<std::mutex> lk(g_blocks_m);
+        auto it = std::find_if(g_blocks.begin(), g_blocks.end(), [&](const HostBlock& x) { return x.h == p; });
+        if (it == g_blocks.end()) return fail(nullptr, AC_ERR_INVALID, "ac_host_free: not a block of ac_host_alloc");
+        b = *it;
+        g_blocks.erase(it);
+    }
+    const hipError_t e = hipHostFree(b.h);
+    return e == hipSuccess ? AC_OK : hip_fail(nullptr, e, "hipHostFree");
+}
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
 // ac_error_count_jobs: the whole errorCount stage from Dna5 host buffers.
 namespace {
+
+// Device packing of jobs whose samples lie in ac_host_alloc blocks (default on; AC_DEVICE_PACK=0 packs
+// every job on the host, for A/B runs).
+bool device_pack_enabled() {
+    static const bool v = env_int("AC_DEVICE_PACK", 1) != 0;
+    return v;
+}
 
 // AC_STAGE_TRACE=1: per-phase host timings of the jobs stage, summed over the
 // calls and printed to stderr at exit (a measurement aid; no effect otherwise).
@@ -1489,6 +1567,9 @@ struct JobPlan {
     uint32_t ulen[AC_MAX_JOBS] = {}, chunks[AC_MAX_JOBS] = {}, codes_off[AC_MAX_JOBS] = {};
     bool nrec[AC_MAX_JOBS] = {};
     uint32_t pre = 0, copiers = 0;
+    // device packing: job j's Dna5 bytes / offsets read by the kernel from pinned memory
+    bool dp[AC_MAX_JOBS] = {};
+    bool dp_any = false;
 };
 
 // Calls whose pack and DMA take hundreds of
@@ -1766,6 +1847,32 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
         for (uint32_t j = 0; j < p.n; ++j) tickets += p.chunks[j] ? p.chunks[j] + 1u : 0u;
         p.copiers = stage_copiers(tickets);
     }
+    // Device packing: a job of equal windows (1..256 bases) whose Dna5 bytes and window
+    // offsets lie in ac_host_alloc blocks is packed by the kernel's copier workgroups straight from them;
+    // the host packs nothing of it (its region in the staging block stays unwritten).  Not with jobs sent
+    // ahead of the launch (p.pre: those are host-packed and copied by the copy kernel).
+    const uint8_t* dp_src[AC_MAX_JOBS] = {};
+    const uint64_t* dp_off[AC_MAX_JOBS] = {};
+    uint32_t dp_bytes[AC_MAX_JOBS] = {};
+    p.dp_any = false;
+    if (p.early && p.pre == 0 && device_pack_enabled())
+        for (uint32_t j = 0; j < p.n; ++j) {
+            p.dp[j] = false;
+            const ac_dna5_windows& w = jobs[j].sample;
+            const uint32_t nw = p.hi[j] - p.lo[j];
+            if (!jobs[j].n_kmers || !nw || ulen[j] == AC_NO_ULEN || ulen[j] == 0 || ulen[j] > 256 || !p.chunks[j]) continue;
+            HostBlock bb, bo;
+            if (!find_block(w.bases, 1, &bb) || !find_block(w.offset + p.lo[j], sizeof(uint64_t) * nw, &bo)) continue;
+            const size_t extent = (size_t)(bb.h + bb.n - (const char*)w.bases);  // bytes readable from `bases`
+            if (extent < ulen[j] || extent >= (size_t(1) << 31)) continue;
+            p.dp[j] = p.dp_any = true;
+            dp_src[j] = (const uint8_t*)(bb.d + ((const char*)w.bases - bb.h));
+            dp_off[j] = (const uint64_t*)(bo.d + ((const char*)(w.offset + p.lo[j]) - bo.h));
+            dp_bytes[j] = (uint32_t)extent;
+        }
+    if (p.dp_any) {  // the host packs only the other jobs' windows
+        tasks.erase(std::remove_if(tasks.begin(), tasks.end(), [&](const Task& x) { return p.dp[x.job]; }), tasks.end());
+    }
     // The slot: wait until the launch that last read it has finished, grow it.
     ac_ctx::Slot& sl = ctx->slot[p.slot];
     if (sl.pending) {
@@ -1872,6 +1979,11 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
             stg.codes_off[j] = p.codes_off[j];
         }
         stg.copiers = p.copiers;
+        for (uint32_t j = 0; j < p.n; ++j) {
+            stg.dp_src[j] = dp_src[j];
+            stg.dp_off[j] = dp_off[j];
+            stg.dp_bytes[j] = dp_bytes[j];
+        }
         // A large call (copier workgroups) packs its jobs' tasks interleaved, so every segment's
         // windows arrive from the start and no segment's waves sit idle while the jobs before it are
         // packed (each copier workgroup starts on its own segment, wm_count.hip).  Small calls keep
@@ -1952,6 +2064,11 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
             nt[j] = 0;
         }
         uint32_t helped = 0, left_jobs = p.n;
+        for (uint32_t j = 0; j < p.n; ++j)
+            if (p.dp[j]) {  // the kernel publishes a device-packed job's words itself: nothing to flag
+                flagged[j] = true;
+                --left_jobs;
+            }
         bool first_flag = true;
         // Job j is finished: its final byte count and N verdict, then its flag (or, jobs below
         // `pre`, the copy kernel sends it ahead of the launch; those finish in job order).
@@ -2273,7 +2390,7 @@ ac_status count_jobs_sync(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint32_t 
             for (uint32_t i = 0; i < jobs[j].n_kmers; ++i) jobs[j].counts[i] += hc[i];
         }
     }
-    if (first_err == AC_OK) units[0].c->last_mode = units[0].plan.early ? 2 : 0;
+    if (first_err == AC_OK) units[0].c->last_mode = units[0].plan.dp_any ? 3 : units[0].plan.early ? 2 : 0;
     if (g_trace.on) {
         g_trace.sum[7] += now_us() - t_sync;
         g_trace.cur[7] += now_us() - t_sync;
@@ -2366,7 +2483,7 @@ ac_status ac_error_count_jobs_submit(ac_ctx* ctx, uint32_t k, const ac_job* jobs
                                             parts == 1))
             return rc;
         if (q > 0) AC_HIP(ctx, hipEventRecord(ctx->sub_ev[q], st));
-        if (q == 0) ctx->last_mode = p.early ? 2 : 0;
+        if (q == 0) ctx->last_mode = p.dp_any ? 3 : p.early ? 2 : 0;
     }
     for (int q = 1; q < parts; ++q) AC_HIP(ctx, hipStreamWaitEvent(caller, ctx->sub_ev[q], 0));
     if (g_trace.on) {

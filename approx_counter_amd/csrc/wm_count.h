@@ -107,6 +107,13 @@ struct SegDev {
     uint32_t stage_chunks;
     uint32_t stage_codes_off;  // bytes of the region before the codes (k-mers)
     uint32_t* stage_gen;       // per chunk, one line each: = the launch's generation once copied (early counting)
+    // Device packing (staged launches, equal windows of 1..256 bases): the segment's
+    // sample is read as Dna5 bytes straight from pinned host memory (ac_host_alloc) by the copier
+    // workgroups, which pack each codes chunk themselves (stage_pack_chunk) instead of copying one the
+    // host packed.  dp_src = NULL: the host packed the codes into the staging block.
+    const uint8_t* dp_src;     // device-visible address the windows' offsets are relative to
+    const uint64_t* dp_off;    // device-visible address of the segment's n_windows offsets
+    uint32_t dp_src_bytes;     // bytes readable from dp_src (< 2^31); a window outside them is an error
 };
 
 struct LaunchArgs {

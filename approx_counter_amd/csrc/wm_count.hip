@@ -330,6 +330,112 @@ struct StageClock {
     }
 };
 
+#ifndef AC_PACK_BLOCKS
+#define AC_PACK_BLOCKS 2  // 32-base blocks whose host loads a packing lane keeps in flight at once
+#endif
+// 4 Dna5 bytes (one per base, ordinal 0-3 = A C G T, anything else N) -> the byte of their four
+// 2-bit codes (base i at bits 2i..2i+1) and, in `n`, bit i set iff base i is N.
+__device__ __forceinline__ uint32_t dna5_codes4(uint32_t x) {
+    uint32_t c = x & 0x03030303u;
+    c = (c | (c >> 6)) & 0x000f000fu;  // bases 0-1 at bits 0-3, bases 2-3 at bits 16-19
+    return (c | (c >> 12)) & 0xffu;
+}
+__device__ __forceinline__ uint32_t dna5_n4(uint32_t x) {
+    const uint32_t t = x & 0xfcfcfcfcu;                                  // nonzero byte <=> ordinal >= 4
+    const uint32_t nz = (((t & 0x7f7f7f7fu) + 0x7f7f7f7fu) | t) & 0x80808080u;  // bit 7 of each such byte
+    return (((nz >> 7) * 0x00204081u) >> 21) & 0xfu;                    // bits 7, 15, 23, 31 -> 0..3
+}
+
+// Device packing of codes chunk `lo_b` (byte offset in the codes section) of an
+// equal-window segment: the windows whose slots overlap the chunk are read as Dna5 bytes from
+// pinned host memory (offset of window w at offs[w], relative to src; src_bytes readable), one
+// window per lane, and packed exactly as the host packer does (host_pack.cpp pack_dna5_range with
+// records): 2-bit codes, padding bases code 0, the window's inline N record (nrec.h) in the top bits
+// of its slot's last code word when the segment has records (rec), and its N-bitmap words.  Only
+// the code words inside the chunk are stored (a slot that straddles two chunks is packed by both
+// owners, each storing its own words), with write-through stores like the copy; the N-bitmap words
+// of the chunk's blocks go to the bitmap section (read only by a window whose record overflowed, or
+// by every window of a segment without records, and then only once the whole segment is in).
+// A window outside src_bytes is stored as zeros and reported (AC_DEVERR_WINDOW).
+__device__ __forceinline__ void stage_pack_chunk(const uint8_t* src, const uint64_t* offs, uint32_t src_bytes,
+                                                           uint32_t n_windows, uint32_t ulen, uint32_t rec,
+                                                           uint32_t code_bytes, uint8_t* codes_dst, uint8_t* nmask_dst,
+                                                           uint32_t lo_b, uint32_t* err) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t SW = ((ulen + 31u) & ~31u) / 16u;  // code words per slot (2..16)
+    const uint32_t nblk = SW / 2u;                    // 32-base blocks per slot, each holding real bases
+    const uint32_t hi_b = min(lo_b + AC_STAGE_CHUNK, code_bytes);
+    const uint32_t cw_lo = lo_b / 4u, cw_hi = hi_b / 4u;  // the chunk's code words
+    const uint32_t w0 = cw_lo / SW, w1 = min(n_windows, (cw_hi + SW - 1u) / SW);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)src, 0, (int)src_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void*)offs, 0, (int)(n_windows * 8u), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc((void*)codes_dst, 0, (int)code_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rn = __builtin_amdgcn_make_buffer_rsrc((void*)nmask_dst, 0, (int)(code_bytes / 2u), 0x00020000);
+    const uint32_t cap = nrec_cap(ulen), pb = nrec_pos_bits(ulen);
+    typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    constexpr uint32_t PB = AC_PACK_BLOCKS;
+    uint32_t bad = 0;
+    for (uint32_t w = w0 + lane; w < w1; w += 64u) {
+        const v2u ov = __builtin_amdgcn_raw_buffer_load_b64(ro, w * 8u, 0, 0);
+        const bool ok = ov.y == 0u && ov.x <= src_bytes - ulen;  // (the host checked src_bytes >= ulen)
+        bad |= ok ? 0u : 1u;
+        const uint32_t off = ok ? ov.x : 0u, a = off & ~3u, sh = off & 3u;
+        uint32_t cnt = 0, pos = 0, last_lo = 0, last_hi = 0;
+        const uint32_t cw_w = w * SW;  // the slot's first code word
+        // PB blocks (32 bases each) per pass: their loads in flight together
+#pragma unroll 1
+        for (uint32_t b0 = 0; b0 < nblk; b0 += PB) {
+            v4u d[PB][2];
+            uint32_t e[PB];
+#pragma unroll
+            for (uint32_t i = 0; i < PB; ++i)
+                if (b0 + i < nblk) {
+                    const uint32_t o = a + 32u * (b0 + i);
+                    d[i][0] = __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0);
+                    d[i][1] = __builtin_amdgcn_raw_buffer_load_b128(rs, o + 16u, 0, 0);
+                    e[i] = __builtin_amdgcn_raw_buffer_load_b32(rs, o + 32u, 0, 0);
+                }
+#pragma unroll
+            for (uint32_t i = 0; i < PB; ++i) {
+                const uint32_t b = b0 + i;
+                if (b >= nblk) continue;
+                const uint32_t raw[9] = {d[i][0].x, d[i][0].y, d[i][0].z, d[i][0].w,
+                                         d[i][1].x, d[i][1].y, d[i][1].z, d[i][1].w, e[i]};
+                const uint32_t nv = ok ? min(32u, ulen - 32u * b) : 0u;  // real bases of the block
+                uint32_t code0 = 0, code1 = 0, nmw = 0;
+#pragma unroll
+                for (uint32_t q = 0; q < 8; ++q) {
+                    uint32_t x = (uint32_t)((((uint64_t)raw[q + 1] << 32) | raw[q]) >> (8u * sh));
+                    const uint32_t have = nv > 4u * q ? nv - 4u * q : 0u;  // bytes of this dword that are bases
+                    x = have >= 4u ? x : (have ? x & ((1u << (8u * have)) - 1u) : 0u);
+                    if (q < 4) code0 |= dna5_codes4(x) << (8u * q);
+                    else code1 |= dna5_codes4(x) << (8u * (q - 4u));
+                    nmw |= dna5_n4(x) << (4u * q);
+                }
+                // the record's N positions, in window order (a window holds <= 256 bases)
+                for (uint32_t m = nmw; m; m &= m - 1u) {
+                    if (cnt < cap) pos |= (32u * b + (uint32_t)__builtin_ctz(m)) << nrec_pos_shift(pb, cnt);
+                    ++cnt;
+                }
+                const uint32_t cw = cw_w + 2u * b;
+                const bool mine = cw >= cw_lo && cw < cw_hi;  // (a block never straddles a chunk)
+                if (b + 1u == nblk) {  // the slot's last block: its second word takes the record
+                    last_lo = code0;
+                    last_hi = code1;
+                } else if (mine) {
+                    __builtin_amdgcn_raw_buffer_store_b64(v2u{code0, code1}, rc, cw * 4u, 0, 16);  // sc1
+                }
+                if (mine) __builtin_amdgcn_raw_buffer_store_b32(nmw, rn, cw * 2u, 0, 16);
+            }
+        }
+        if (rec && cnt) last_hi |= cnt <= cap ? (pos | cnt << 29) : (NREC_OVERFLOW << 29);
+        const uint32_t cw = cw_w + SW - 2u;
+        if (cw >= cw_lo && cw < cw_hi) __builtin_amdgcn_raw_buffer_store_b64(v2u{last_lo, last_hi}, rc, cw * 4u, 0, 16);
+    }
+    if (__ballot(bad != 0u) && lane == 0) atomicOr(err, AC_DEVERR_WINDOW);
+}
+
 // Claims and serves tickets until none is left; false on timeout.  Chunks below `pre_chunks` (the
 // k-mer section, in place in the pinned block before the launch) are copied without waiting.
 __device__ __attribute__((noinline)) bool stage_copy(const uint8_t* src, uint8_t* dst, uint32_t chunks,
@@ -365,6 +471,12 @@ __device__ __attribute__((noinline)) bool stage_copy(const uint8_t* src, uint8_t
                                   ? ~0u
                                   : (info & AC_HDR_INFO_HAS_N ? 1u : 0u);
                     if (verdict == 0u) ready = bytes;  // no N anywhere: the whole region is N-free
+                    // the final words before the prefix they complete: a copier released by the prefix can
+                    // finish the segment's last chunk, and a reader that then sees the done count complete
+                    // reads the verdict (so it must be there first)
+                    wave_store(sw.verdict, verdict);
+                    wave_store(sw.bytes, verdict == ~0u ? 0u : bytes);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 }
                 if (verdict != ~0u && ready > published && ready <= chunks * AC_STAGE_CHUNK) {
                     if (published == 0) stage_stamp(si, 1);
@@ -377,8 +489,6 @@ __device__ __attribute__((noinline)) bool stage_copy(const uint8_t* src, uint8_t
                 }
                 if (fin) {
                     stage_stamp(si, 0);
-                    wave_store(sw.verdict, verdict);
-                    wave_store(sw.bytes, verdict == ~0u ? 0u : bytes);
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     wave_store(sw.fin, 1u);
                     break;
@@ -456,6 +566,86 @@ __device__ __attribute__((noinline)) bool stage_copy(const uint8_t* src, uint8_t
             prev = __hip_atomic_fetch_add(sw.done + lane * AC_QUEUE_LINE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (__builtin_amdgcn_readfirstlane(prev) + 1u == chunks) stage_stamp(si, 2);  // (diagnostic builds) last chunk in
         if (x == pre_chunks) stage_stamp(si, 4);  // (diagnostic builds) first codes chunk in
+    }
+}
+
+// The copier loop of a device-packed segment: the host published nothing and packs
+// nothing -- its Dna5 bytes sit in pinned memory from before the launch -- so ticket 0 publishes the
+// segment's final words at once (no header read over PCIe): the verdict (1: the N bitmap is there for
+// the windows that need it), the byte count, the whole region as available (with inline N records;
+// without them only the k-mers, so readers wait for the whole segment and its bitmap) and `fin`.
+// Tickets c >= 1: k-mer chunks are copied from the staging block, codes chunks packed from the Dna5
+// bytes (stage_pack_chunk), N-bitmap chunks have no work of their own (their words are stored by the
+// codes chunks' owners); then, as in stage_copy, the chunk's flag and the done replicas -- only once
+// `fin` is out, so a reader that sees the segment complete reads its verdict.  Inlined into the
+// kernel (its registers then come from the kernel's budget: as a called function it spilled).
+__device__ __forceinline__ bool stage_copy_dp(const SegDev& sg, uint32_t* words, uint32_t gen, uint32_t* err) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const StageWords sw = stage_words(words);
+    const uint32_t chunks = sg.stage_chunks, pre_chunks = sg.stage_codes_off / AC_STAGE_CHUNK;
+    const uint32_t code_bytes = (uint32_t)(sg.n_bases >> 2);
+    const uint32_t nmask_off = pre_chunks * AC_STAGE_CHUNK + ((code_bytes + 255u) & ~255u);  // (256-B aligned sections)
+    StageClock clk;
+    bool fin_seen = false;
+    for (;;) {
+        uint32_t c = 0;
+        if (lane == 0) c = __hip_atomic_fetch_add(sw.claim, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        c = __builtin_amdgcn_readfirstlane(c);
+        if (c > chunks) return true;
+        clk.progress();
+        if (c == 0) {
+            const uint32_t bytes = chunks * AC_STAGE_CHUNK;  // (the host sized the region: codes + bitmap)
+            wave_store(sw.verdict, 1u);
+            wave_store(sw.bytes, bytes);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane < AC_STAGE_REPL)
+                __hip_atomic_store(sw.avail + lane * AC_QUEUE_LINE, sg.nrec ? bytes : sg.stage_codes_off,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            wave_store(sw.fin, 1u);
+            continue;
+        }
+        const uint32_t x = c - 1u, lo = x * AC_STAGE_CHUNK;
+#if AC_COPY_AHEAD
+        if (x >= AC_COPY_AHEAD) {  // in chunk order, as stage_copy
+            uint32_t* my_done = sw.done + (x % AC_STAGE_REPL) * AC_QUEUE_LINE;
+            uint32_t dn = 0, dseen = 0;
+            while ((dn = wave_load(my_done)) < x - AC_COPY_AHEAD) {
+                if (dn > dseen) {
+                    dseen = dn;
+                    clk.progress();
+                } else if (clk.late()) {
+                    return false;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+#endif
+        if (x < pre_chunks) {  // k-mers: in the pinned staging block since before the launch
+            typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)sg.stage_src, 0, (int)(pre_chunks * AC_STAGE_CHUNK), 0x00020000);
+            const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)sg.stage_dst, 0, (int)(pre_chunks * AC_STAGE_CHUNK), 0x00020000);
+            v4u v[4];
+            const uint32_t o = lo + lane * 16u;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, o + u * 1024u, 0, AC_STAGE_LOAD_AUX);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) __builtin_amdgcn_raw_buffer_store_b128(v[u], rd, o + u * 1024u, 0, 16);  // sc1
+        } else if (lo - pre_chunks * AC_STAGE_CHUNK < code_bytes) {
+            stage_pack_chunk(sg.dp_src, sg.dp_off, sg.dp_src_bytes, sg.n_windows, sg.ulen, sg.nrec, code_bytes,
+                             sg.stage_dst + pre_chunks * AC_STAGE_CHUNK, sg.stage_dst + nmask_off,
+                             lo - pre_chunks * AC_STAGE_CHUNK, err);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        while (!fin_seen) {  // (ticket 0's words out before the first chunk counts as done)
+            fin_seen = wave_load(sw.fin) != 0u;
+            if (!fin_seen) {
+                if (clk.late()) return false;
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+        wave_store(chunk_flag(sg.stage_gen, x), gen);
+        if (lane < AC_STAGE_REPL)
+            __hip_atomic_fetch_add(sw.done + lane * AC_QUEUE_LINE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -650,10 +840,12 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
                 const uint32_t s2 = (blockIdx.x + i2) % a.n_segs;
                 const SegDev& c2 = a.seg[s2];
                 if (!c2.stage_chunks) continue;
-                if (!__builtin_amdgcn_readfirstlane((uint32_t)stage_copy(
-                        c2.stage_src, c2.stage_dst, c2.stage_chunks, c2.stage_codes_off / AC_STAGE_CHUNK,
-                        a.host_hdr + s2 * AC_QUEUE_LINE, a.stage + AC_STAGE_L_SEG(s2) * AC_QUEUE_LINE, c2.stage_gen,
-                        a.gen, s2)))
+                const bool ok = c2.dp_src
+                                    ? stage_copy_dp(c2, a.stage + AC_STAGE_L_SEG(s2) * AC_QUEUE_LINE, a.gen, a.err)
+                                    : stage_copy(c2.stage_src, c2.stage_dst, c2.stage_chunks,
+                                                 c2.stage_codes_off / AC_STAGE_CHUNK, a.host_hdr + s2 * AC_QUEUE_LINE,
+                                                 a.stage + AC_STAGE_L_SEG(s2) * AC_QUEUE_LINE, c2.stage_gen, a.gen, s2);
+                if (!__builtin_amdgcn_readfirstlane((uint32_t)ok))
                     if (lane == 0) atomicOr(a.err, AC_DEVERR_STAGE);
             }
         }

@@ -97,6 +97,10 @@ def parse():
                     help="submit: at N = 1 run the N > 1 step form (ac_error_count_jobs_submit, the library's RCCL "
                          "all-reduce on a one-rank communicator, counts copied back, stream synchronised) -- a "
                          "rehearsal of the multi-GPU step's own costs, never the default line")
+    ap.add_argument("--sample", choices=("pinned", "heap"), default="pinned",
+                    help="where the Dna5 sample lives: pinned = ac_host_alloc memory, packed on the device by the "
+                         "count kernel's copier workgroups (DESIGN.md 4d); heap = ordinary memory, packed by the host "
+                         "pool (4c)")
     ap.add_argument("--kernel-launches", type=int, default=100,
                     help="launches of the kernel-only leg (at least --steps); it runs before the stage, so the "
                          "device is at its sustained clock when the stage's warmup starts (DESIGN.md 4c)")
@@ -226,7 +230,12 @@ def load_pmc(workload: str):
 
 def stage_text(stage_path: str, world: int) -> str:
     """config.stage: what one timed step runs, from host Dna5 buffers to counts."""
-    if stage_path == "early-launch":
+    if stage_path == "early-launch-device-pack":
+        body = ("1 fused count launch; the Dna5 sample sits in pinned host memory (ac_host_alloc) and 16 copier "
+                "workgroups of the kernel read it over PCIe and pack each 4 KB chunk of 2-bit codes (N positions "
+                "inline) into HBM while the others count a window as soon as its chunk is in; the host packs "
+                "nothing")
+    elif stage_path == "early-launch":
         body = ("1 fused count launch issued first in the call, then both read ends packed (host pool, pinned; "
                 "N positions inline in each window's slot) with progress records; 16 copier workgroups of the "
                 "kernel pull each 4 KB chunk into HBM as it is packed while the others count a window as soon "
@@ -236,7 +245,7 @@ def stage_text(stage_path: str, world: int) -> str:
                 "HBM while the previous part counts")
     if world > 1:
         tail = " -> RCCL all-reduce -> counts D2H"
-    elif stage_path == "early-launch":
+    elif stage_path.startswith("early-launch"):
         tail = (" -> counts tagged with the call's generation stored to pinned host memory by each candidate "
                 "group, polled")
     else:
@@ -313,7 +322,10 @@ def main():
     n_c = [int(wl[e]["kmers"].size) for e in ends]
     bases = [sum(int(w.size) for w in wl[e]["windows"]) for e in ends]
     units_rank = sum(n * b for n, b in zip(n_c, bases))
-    jobs = ac.Jobs([(wl[e]["kmers"], ac.Dna5Sample.from_windows(wl[e]["windows"])) for e in ends])
+    samples = [ac.Dna5Sample.from_windows(wl[e]["windows"]) for e in ends]
+    if args.sample == "pinned":  # the sample built in ac_host_alloc memory (outside the timed steps, like sampling)
+        samples = [smp.pinned() for smp in samples]
+    jobs = ac.Jobs([(wl[e]["kmers"], smp) for e, smp in zip(ends, samples)])
     counter = ac.ApproxCounter(local)
     stream = torch.cuda.current_stream(dev)
     d_counts = torch.zeros(max(1, jobs.n_counts), dtype=torch.int32, device=dev)
@@ -367,7 +379,7 @@ def main():
     while counter.stage_mode() < 0 and tune_calls < 4:
         counter.count_jobs(args.k, jobs)
         tune_calls += 1
-    stage_path = {2: "early-launch", 0: "dma"}.get(counter.stage_mode(), "undecided")
+    stage_path = {3: "early-launch-device-pack", 2: "early-launch", 0: "dma"}.get(counter.stage_mode(), "undecided")
 
     # ---- pipelined leg (informational, 1 GPU): host-buffer steps back to back, max(steps, 100)
     # of them.  Run before the stage, so the stage is timed in steady state; one stage call on

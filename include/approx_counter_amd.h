@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define AC_ABI_VERSION 6
+#define AC_ABI_VERSION 7
 
 typedef int32_t ac_status;
 #define AC_OK 0
@@ -264,6 +264,23 @@ typedef struct ac_dna5_windows {
     uint32_t n_windows;
 } ac_dna5_windows;
 
+/*
+ * Pinned host memory for the sample (ABI 7; no reference counterpart: the reference's
+ * sampleSequences, approx_counter.cpp:415-476, fills an ordinary StringSet<Dna5String>).
+ * A job of ac_error_count_jobs / _submit whose windows all have one length of 1..256 bases (a read
+ * end: sl or sl + 1) and whose `bases` and `offset` arrays lie inside blocks of ac_host_alloc is
+ * packed on the device: the count kernel's copier workgroups read its Dna5 bytes over PCIe and
+ * pack them into HBM themselves, so the host does no per-window work for it beyond scanning the
+ * lengths (ac_stage_mode then reports 3).  The bytes readable from `bases` are those up to the end
+ * of its block; a window reaching past them is an error (AC_ERR_INVALID, its counts short).
+ * Blocks are process-wide (any context, any device).  A submit's device-packed jobs are read by
+ * the device until its stream work completes: do not change or free them before that.
+ *   ac_host_alloc  a pinned, device-mapped block of `bytes` (AC_ERR_DEVICE without a HIP device)
+ *   ac_host_free   releases a block of ac_host_alloc (NULL: no-op; another pointer: AC_ERR_INVALID)
+ */
+ac_status ac_host_alloc(size_t bytes, void** out);
+ac_status ac_host_free(void* p);
+
 /* One errorCount call (approx_counter.cpp:922) over a Dna5 sample. */
 typedef struct ac_job {
     const uint64_t* kmers; /* dna2int layout (approx_counter.cpp:55-62)         */
@@ -377,6 +394,7 @@ int ac_plan_host_cpus(const char* const* rank_cpulists, int n_ranks, int rank, c
  * inputs (no reference counterpart).  ABI note: the values changed in ABI 3 --
  * 1 (zero-copy, round 2) is no longer returned -- and in ABI 4 large calls moved
  * from 0 to 2; callers should compare against 2 / 0 only.
+ * 3 = the early launch with at least one job packed on the device (ac_host_alloc samples, ABI 7).
  * 2 = the early launch, for every single-device call
  * (default; AC_STAGE_EARLY=0 turns it off): the count kernel is
  * launched before the host packs, the host flags each job in a pinned header as

@@ -27,7 +27,7 @@ def test_library_targets_gfx950():
 
 
 def test_abi_version():
-    assert _lib.load().ac_abi_version() == 6
+    assert _lib.load().ac_abi_version() == 7  # ABI 7: ac_host_alloc / ac_host_free (device packing)
 
 
 def test_pack_layout():

@@ -2,8 +2,9 @@
 
 bench.py's `value` is `ac_error_count_jobs` on cfg2 (k=16, 2 x 10k windows of
 100 / 101 bases, 0.1 % N, 500 candidates per end, seed 1): the early launch
-(`ac_stage_mode() == 2`), i.e. `wm2_count_kernel<2, STAGED, EQ>` staging its own
-inputs while the host pool packs them.  Its N > 1 steps go through
+(`ac_stage_mode() == 3` on the sample in ac_host_alloc memory, the bench's default since round 6:
+the kernel's copier workgroups pack the Dna5 bytes themselves; `== 2` on ordinary memory, the host
+pool packing), i.e. `wm2_count_kernel<2, STAGED, EQ>` staging its own inputs.  Its N > 1 steps go through
 `ac_error_count_jobs_submit` on one rank's shard.  Both are checked here over
 EVERY candidate and window against `oracle.count_myers` (errorCount,
 approx_counter.cpp:531-601), on the very workload objects bench.py builds
@@ -32,9 +33,17 @@ def _expected(k, wl):
     return [oracle.count_myers(k, wl[e]["kmers"], wl[e]["windows"], THREADS) for e in ENDS]
 
 
-def test_bench_cfg2_stage_bit_exact():
+def _samples(wl, where):
+    smp = [ac.Dna5Sample.from_windows(wl[e]["windows"]) for e in ENDS]
+    return [x.pinned() for x in smp] if where == "pinned" else smp
+
+
+@pytest.mark.parametrize("where", ["pinned", "heap"])
+def test_bench_cfg2_stage_bit_exact(where):
     """cfg2 as bench.py times it: the synchronous early launch, 6 calls on one context (both
-    staging slots, three times each), then the submit form the N > 1 steps use."""
+    staging slots, three times each), then the submit form the N > 1 steps use; on the sample in
+    pinned memory (device packing, bench --sample pinned, the default) and in ordinary memory."""
+    mode = 3 if where == "pinned" else 2
     import torch
 
     args = _bench_args("cfg2")
@@ -43,11 +52,11 @@ def test_bench_cfg2_stage_bit_exact():
     assert [len(wl[e]["windows"]) for e in ENDS] == [10_000, 10_000]
     assert units == sum(500 * sum(int(w.size) for w in wl[e]["windows"]) for e in ENDS)
     exp = _expected(16, wl)
-    jobs = ac.Jobs([(wl[e]["kmers"], ac.Dna5Sample.from_windows(wl[e]["windows"])) for e in ENDS])
+    jobs = ac.Jobs([(wl[e]["kmers"], smp) for e, smp in zip(ENDS, _samples(wl, where))])
     with ac.ApproxCounter(0) as c:
         for i in range(6):
             got = c.count_jobs(16, jobs)
-            assert c.stage_mode() == 2, c.stage_mode()  # the early launch, as timed
+            assert c.stage_mode() == mode, c.stage_mode()  # the early launch, as timed
             for e, g, x in zip(ENDS, got, exp):
                 assert np.array_equal(g, x), (i, e)
         out = torch.full((jobs.n_counts,), -1, dtype=torch.int32, device="cuda")
@@ -55,13 +64,14 @@ def test_bench_cfg2_stage_bit_exact():
         for _ in range(3):
             c.submit_jobs(16, jobs, out, stream=st.cuda_stream)
         c.check(stream=st.cuda_stream)
-        assert c.stage_mode() == 2
+        assert c.stage_mode() == mode
         got = out.cpu().numpy().view(np.uint32).astype(np.uint64)
         assert np.array_equal(got, np.concatenate(exp))
 
 
+@pytest.mark.parametrize("where", ["pinned", "heap"])
 @pytest.mark.parametrize("rank", [0, 7])
-def test_bench_cfg4_rank_shard_submit_bit_exact(rank):
+def test_bench_cfg4_rank_shard_submit_bit_exact(rank, where):
     """One rank's 1/8 shard of cfg4 (strong scaling, 2 x 125k windows) through
     ac_error_count_jobs_submit, as bench.py's N = 8 step issues it, over every
     candidate of both ends against the oracle on the shard's own windows."""
@@ -71,13 +81,14 @@ def test_bench_cfg4_rank_shard_submit_bit_exact(rank):
     wl, _ = bench.build_workload(args, rank, 8)
     assert all(abs(len(wl[e]["windows"]) - 125_000) < 100 for e in ENDS)
     exp = _expected(16, wl)
-    jobs = ac.Jobs([(wl[e]["kmers"], ac.Dna5Sample.from_windows(wl[e]["windows"])) for e in ENDS])
+    jobs = ac.Jobs([(wl[e]["kmers"], smp) for e, smp in zip(ENDS, _samples(wl, where))])
     with ac.ApproxCounter(0) as c:
         out = torch.full((jobs.n_counts,), -1, dtype=torch.int32, device="cuda")
         st = torch.cuda.current_stream()
         for _ in range(2):
             c.submit_jobs(16, jobs, out, stream=st.cuda_stream)
         c.check(stream=st.cuda_stream)
+        assert c.stage_mode() == (3 if where == "pinned" else 2)
         got = out.cpu().numpy().view(np.uint32).astype(np.uint64)
         assert np.array_equal(got, np.concatenate(exp))
         sync = c.count_jobs(16, jobs)
@@ -96,11 +107,13 @@ def test_bench_line_reports_the_pool_that_ran():
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, AC_HOST_THREADS="3")
-    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "3", "--warmup", "1",
-                        "--no-cpu-baseline", "--no-pipelined", "--no-kernel-leg"],
-                       env=env, capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stderr[-2000:]
-    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
-    assert line["host_pool"]["participants"] == 3
-    assert "issued first in the call" in line["config"]["stage"]
-    assert "armed_launch" not in line
+    for sample, path, text in (("heap", "early-launch", "issued first in the call"),
+                               ("pinned", "early-launch-device-pack", "the host packs nothing")):
+        r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "3", "--warmup", "1",
+                            "--no-cpu-baseline", "--no-pipelined", "--no-kernel-leg", "--sample", sample],
+                           env=env, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+        assert line["host_pool"]["participants"] == 3
+        assert line["config"]["stage_path"] == path and text in line["config"]["stage"]
+        assert "armed_launch" not in line and "cgroup_cpu" in line

@@ -5,7 +5,7 @@
 #   stall      CPU-quota throttling vs the step-time tail: cfg2 for 10 s and
 #              cfg5 for 200 steps at the default pool, at 14 participants and with a 100-us worker spin
 #   stallpin   the same on pinned samples (device packing)
-#   tests      the jobs / bench-path GPU tests
+#   tests      the device-pack / jobs / bench-path GPU tests
 #   suite      the whole -m gpu suite
 #   bench      the default bench line (cfg2) and cfg3 / cfg4 / cfg5 lines
 #   ab         cfg2 stage, host packing vs device packing (AC_DEVICE_PACK=0 / 1), x3 interleaved
@@ -41,6 +41,7 @@ stallpin)
   run stallpin_cfg5 300 $S --config cfg5 --steps 200 --pinned
   run stallpin_cfg4 400 $S --config cfg4 --steps 100 --pinned ;;
 tests)
+  run tests_dp 600 $PYT -m gpu tests/test_gpu_device_pack.py
   run tests_jobs 600 $PYT -m gpu tests/test_gpu_jobs.py tests/test_gpu_bench_path.py ;;
 suite)
   run suite 1100 $PYT -m gpu tests ;;
@@ -49,11 +50,19 @@ bench)
   for c in cfg3 cfg5 cfg4; do
     run bench_$c 400 python3 bench.py --config $c --steps 20 --warmup 5 $BQ
   done ;;
-ab)
+ab)  # cfg2 stage: device packing (pinned sample) vs host packing of the same pinned sample vs a heap sample
   for rep in 1 2 3; do
-    run ab_host_$rep 120 env AC_DEVICE_PACK=0 $B
-    run ab_dev_$rep 120 env AC_DEVICE_PACK=1 $B
+    run ab_dev_$rep 120 $B --sample pinned
+    run ab_hostpin_$rep 120 env AC_DEVICE_PACK=0 $B --sample pinned
+    run ab_heap_$rep 120 $B --sample heap
   done ;;
+abbig)  # cfg3 / cfg5 / cfg4 and one rank's cfg4 shard: device vs host packing
+  for c in cfg3 cfg5 cfg4; do
+    run abbig_dev_$c 300 python3 bench.py --config $c --steps 20 --warmup 5 $BQ --no-kernel-leg --sample pinned
+    run abbig_heap_$c 300 python3 bench.py --config $c --steps 20 --warmup 5 $BQ --no-kernel-leg --sample heap
+  done
+  run shard_dev 300 python3 bench.py --config cfg4 --shard 0/8 --steps 50 --warmup 5 $BQ --no-kernel-leg --sample pinned
+  run shard_heap_t2 300 env AC_HOST_THREADS=2 python3 bench.py --config cfg4 --shard 0/8 --steps 50 --warmup 5 $BQ --no-kernel-leg --sample heap ;;
 *) echo "unknown part $part" ;;
 esac
 done

@@ -90,7 +90,9 @@ def main():
             thr.append((ta, tb, sb["throttled_usec"] - sa.get("throttled_usec", 0)))
     slow = [(t, ms) for t, ms in durs if ms > 2 * p50]
     slow_in_thr = sum(1 for t, _ in slow if any(ta <= t <= tb for ta, tb, _ in thr))
-    pool = ac.host_pool_cpus()
+    from approx_counter_amd.counter import host_pool_cpus
+
+    pool = host_pool_cpus()
     out = {
         "config": a.config, "pinned": a.pinned, "steps": len(durs), "seconds": el,
         "stage_mode": counter.stage_mode(),
