@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <cctype>
+#include <cmath>
 #include <chrono>
 #include <cstdlib>
 #include <cstdio>
@@ -596,9 +597,9 @@ int env_int(const char* name, int dflt) {
 // One process per GPU (torchrun: LOCAL_RANK / LOCAL_WORLD_SIZE, local rank r
 // on device r mod the visible devices): the local ranks whose GPUs share a
 // CPU list split it into disjoint runs of physical cores, and each rank's pool
-// takes at most its share of the cgroup CPU quota (16 participants at most), so
-// 8 ranks on one node never pin their workers onto the same CPUs nor spin
-// more threads than the quota runs.  (The reference sizes its one OpenMP team
+// takes at most its share of the cgroup CPU quota minus headroom (below; 16
+// participants at most), so 8 ranks on one node never pin their workers onto the
+// same CPUs nor spin more threads than the quota runs.  (The reference sizes its one OpenMP team
 // with omp_set_num_threads(nb_thread), approx_counter.cpp:547.)
 void plan_host_pool(int device, int n_dev) {
     if (acamd::host_plan().participants) return;  // set already (ac_set_host_cpus or an earlier context)
@@ -611,8 +612,16 @@ void plan_host_pool(int device, int n_dev) {
     acamd::HostPlan plan;
     plan.cpus = acamd::plan_host_cpus(lists, lr, allowed, acamd::sysfs_core_of, &shared);
     size_t n = plan.cpus.empty() ? allowed.size() : plan.cpus.size();
+    // Headroom under the quota: a pool of all of it (16 participants spinning on a 16-CPU quota, with
+    // Python's and the HIP runtime's threads beside them) was throttled in 91 of 100 CFS periods of a
+    // 10-s cfg2 run (191 ms throttled, 59 of its 60 steps over 2x p50 inside throttled periods; 14
+    // participants: none, p50 equal; profiles/r06_m3/stall_*.log): 2 CPUs of headroom above a share
+    // of 4, 1 below.
     const double quota = acamd::cgroup_cpu_quota();
-    if (quota > 0.0) n = std::min<size_t>(n, (size_t)std::max(1.0, quota / lws));
+    if (quota > 0.0) {
+        const double share = quota / lws;
+        n = std::min<size_t>(n, (size_t)std::max(1.0, std::floor(share) - (share > 4.0 ? 2.0 : 1.0)));
+    }
     plan.participants = shared ? 1u : (unsigned)std::max<size_t>(1, std::min<size_t>(16, n));
     (void)acamd::set_host_plan(plan);
 }

@@ -331,7 +331,7 @@ struct StageClock {
 };
 
 #ifndef AC_PACK_BLOCKS
-#define AC_PACK_BLOCKS 2  // 32-base blocks whose host loads a packing lane keeps in flight at once
+#define AC_PACK_BLOCKS 4  // 32-base blocks whose host loads a packing lane keeps in flight at once
 #endif
 // 4 Dna5 bytes (one per base, ordinal 0-3 = A C G T, anything else N) -> the byte of their four
 // 2-bit codes (base i at bits 2i..2i+1) and, in `n`, bit i set iff base i is N.
@@ -357,81 +357,103 @@ __device__ __forceinline__ uint32_t dna5_n4(uint32_t x) {
 // of the chunk's blocks go to the bitmap section (read only by a window whose record overflowed, or
 // by every window of a segment without records, and then only once the whole segment is in).
 // A window outside src_bytes is stored as zeros and reported (AC_DEVERR_WINDOW).
+// Each PCIe round trip costs ~2 us: a lane has its next windows' offsets in flight while it packs,
+// and all of a window's loads (AC_PACK_BLOCKS blocks of 32 bases) in flight together.
+struct PackOut {
+    uint32_t cnt = 0, pos = 0, last_lo = 0, last_hi = 0;
+};
+struct PackCtx {
+    __amdgpu_buffer_rsrc_t rc, rn;
+    uint32_t ulen, nblk, SW, cw_lo, cw_hi, cap, pb;
+};
+typedef uint32_t pk_v2u __attribute__((ext_vector_type(2)));
+typedef uint32_t pk_v4u __attribute__((ext_vector_type(4)));
+// One 32-base block b of a window from its 9 loaded dwords (the 32 bytes from byte `sh` of the first).
+__device__ __forceinline__ void pack_block(const PackCtx& pc, const pk_v4u& d0, const pk_v4u& d1, uint32_t e, uint32_t b,
+                                           bool ok, uint32_t sh, uint32_t cw_w, PackOut& o) {
+    const uint32_t raw[9] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w, e};
+    const uint32_t nv = ok ? min(32u, pc.ulen - 32u * b) : 0u;  // real bases of the block
+    uint32_t code0 = 0, code1 = 0, nmw = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < 8; ++q) {
+        uint32_t x = (uint32_t)((((uint64_t)raw[q + 1] << 32) | raw[q]) >> (8u * sh));
+        const uint32_t have = nv > 4u * q ? nv - 4u * q : 0u;  // bytes of this dword that are bases
+        x = have >= 4u ? x : (have ? x & ((1u << (8u * have)) - 1u) : 0u);
+        if (q < 4) code0 |= dna5_codes4(x) << (8u * q);
+        else code1 |= dna5_codes4(x) << (8u * (q - 4u));
+        nmw |= dna5_n4(x) << (4u * q);
+    }
+    for (uint32_t m = nmw; m; m &= m - 1u) {  // the record's N positions, in window order
+        if (o.cnt < pc.cap) o.pos |= (32u * b + (uint32_t)__builtin_ctz(m)) << nrec_pos_shift(pc.pb, o.cnt);
+        ++o.cnt;
+    }
+    const uint32_t cw = cw_w + 2u * b;
+    const bool mine = cw >= pc.cw_lo && cw < pc.cw_hi;  // (a block never straddles a chunk)
+    if (b + 1u == pc.nblk) {  // the slot's last block: its second word takes the record
+        o.last_lo = code0;
+        o.last_hi = code1;
+    } else if (mine) {
+        __builtin_amdgcn_raw_buffer_store_b64(pk_v2u{code0, code1}, pc.rc, cw * 4u, 0, 16);  // sc1
+    }
+    if (mine) __builtin_amdgcn_raw_buffer_store_b32(nmw, pc.rn, cw * 2u, 0, 16);
+}
+__device__ __forceinline__ void pack_finish(const PackCtx& pc, uint32_t rec, uint32_t cw_w, PackOut& o) {
+    if (rec && o.cnt) o.last_hi |= o.cnt <= pc.cap ? (o.pos | o.cnt << 29) : (NREC_OVERFLOW << 29);
+    const uint32_t cw = cw_w + pc.SW - 2u;
+    if (cw >= pc.cw_lo && cw < pc.cw_hi)
+        __builtin_amdgcn_raw_buffer_store_b64(pk_v2u{o.last_lo, o.last_hi}, pc.rc, cw * 4u, 0, 16);
+}
+
 __device__ __forceinline__ void stage_pack_chunk(const uint8_t* src, const uint64_t* offs, uint32_t src_bytes,
-                                                           uint32_t n_windows, uint32_t ulen, uint32_t rec,
-                                                           uint32_t code_bytes, uint8_t* codes_dst, uint8_t* nmask_dst,
-                                                           uint32_t lo_b, uint32_t* err) {
+                                                 uint32_t n_windows, uint32_t ulen, uint32_t rec, uint32_t code_bytes,
+                                                 uint8_t* codes_dst, uint8_t* nmask_dst, uint32_t lo_b, uint32_t* err) {
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t SW = ((ulen + 31u) & ~31u) / 16u;  // code words per slot (2..16)
-    const uint32_t nblk = SW / 2u;                    // 32-base blocks per slot, each holding real bases
+    PackCtx pc;
+    pc.ulen = ulen;
+    pc.SW = ((ulen + 31u) & ~31u) / 16u;  // code words per slot (2..16)
+    pc.nblk = pc.SW / 2u;                 // 32-base blocks per slot, each holding real bases
     const uint32_t hi_b = min(lo_b + AC_STAGE_CHUNK, code_bytes);
-    const uint32_t cw_lo = lo_b / 4u, cw_hi = hi_b / 4u;  // the chunk's code words
-    const uint32_t w0 = cw_lo / SW, w1 = min(n_windows, (cw_hi + SW - 1u) / SW);
+    pc.cw_lo = lo_b / 4u;
+    pc.cw_hi = hi_b / 4u;  // the chunk's code words
+    pc.cap = nrec_cap(ulen);
+    pc.pb = nrec_pos_bits(ulen);
+    const uint32_t w0 = pc.cw_lo / pc.SW, w1 = min(n_windows, (pc.cw_hi + pc.SW - 1u) / pc.SW);
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)src, 0, (int)src_bytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void*)offs, 0, (int)(n_windows * 8u), 0x00020000);
-    const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc((void*)codes_dst, 0, (int)code_bytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rn = __builtin_amdgcn_make_buffer_rsrc((void*)nmask_dst, 0, (int)(code_bytes / 2u), 0x00020000);
-    const uint32_t cap = nrec_cap(ulen), pb = nrec_pos_bits(ulen);
-    typedef uint32_t v2u __attribute__((ext_vector_type(2)));
-    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-    constexpr uint32_t PB = AC_PACK_BLOCKS;
+    pc.rc = __builtin_amdgcn_make_buffer_rsrc((void*)codes_dst, 0, (int)code_bytes, 0x00020000);
+    pc.rn = __builtin_amdgcn_make_buffer_rsrc((void*)nmask_dst, 0, (int)(code_bytes / 2u), 0x00020000);
     uint32_t bad = 0;
+    // The offsets of the lane's first two windows in one round trip (a chunk holds <= 128 slots of
+    // >= 128 bases, 2 rounds of 64; shorter slots take more rounds, their offsets loaded per round).
+    pk_v2u onext = w0 + lane < w1 ? __builtin_amdgcn_raw_buffer_load_b64(ro, (w0 + lane) * 8u, 0, 0) : pk_v2u{0u, 0u};
+    pk_v2u onext2 = w0 + lane + 64u < w1 ? __builtin_amdgcn_raw_buffer_load_b64(ro, (w0 + lane + 64u) * 8u, 0, 0)
+                                          : pk_v2u{0u, 0u};
+    constexpr uint32_t PB = AC_PACK_BLOCKS;  // blocks per pass: their loads in flight together
     for (uint32_t w = w0 + lane; w < w1; w += 64u) {
-        const v2u ov = __builtin_amdgcn_raw_buffer_load_b64(ro, w * 8u, 0, 0);
+        const pk_v2u ov = onext;
+        onext = onext2;
+        if (w + 128u < w1) onext2 = __builtin_amdgcn_raw_buffer_load_b64(ro, (w + 128u) * 8u, 0, 0);
         const bool ok = ov.y == 0u && ov.x <= src_bytes - ulen;  // (the host checked src_bytes >= ulen)
         bad |= ok ? 0u : 1u;
-        const uint32_t off = ok ? ov.x : 0u, a = off & ~3u, sh = off & 3u;
-        uint32_t cnt = 0, pos = 0, last_lo = 0, last_hi = 0;
-        const uint32_t cw_w = w * SW;  // the slot's first code word
-        // PB blocks (32 bases each) per pass: their loads in flight together
+        const uint32_t off = ok ? ov.x : 0u, a = off & ~3u, sh = off & 3u;  // out of range: read as zeros
+        PackOut o;
 #pragma unroll 1
-        for (uint32_t b0 = 0; b0 < nblk; b0 += PB) {
-            v4u d[PB][2];
+        for (uint32_t b0 = 0; b0 < pc.nblk; b0 += PB) {
+            pk_v4u d[PB][2];
             uint32_t e[PB];
 #pragma unroll
             for (uint32_t i = 0; i < PB; ++i)
-                if (b0 + i < nblk) {
-                    const uint32_t o = a + 32u * (b0 + i);
-                    d[i][0] = __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0);
-                    d[i][1] = __builtin_amdgcn_raw_buffer_load_b128(rs, o + 16u, 0, 0);
-                    e[i] = __builtin_amdgcn_raw_buffer_load_b32(rs, o + 32u, 0, 0);
+                if (b0 + i < pc.nblk) {
+                    const uint32_t x = a + 32u * (b0 + i);
+                    d[i][0] = __builtin_amdgcn_raw_buffer_load_b128(rs, x, 0, 0);
+                    d[i][1] = __builtin_amdgcn_raw_buffer_load_b128(rs, x + 16u, 0, 0);
+                    e[i] = __builtin_amdgcn_raw_buffer_load_b32(rs, x + 32u, 0, 0);
                 }
 #pragma unroll
-            for (uint32_t i = 0; i < PB; ++i) {
-                const uint32_t b = b0 + i;
-                if (b >= nblk) continue;
-                const uint32_t raw[9] = {d[i][0].x, d[i][0].y, d[i][0].z, d[i][0].w,
-                                         d[i][1].x, d[i][1].y, d[i][1].z, d[i][1].w, e[i]};
-                const uint32_t nv = ok ? min(32u, ulen - 32u * b) : 0u;  // real bases of the block
-                uint32_t code0 = 0, code1 = 0, nmw = 0;
-#pragma unroll
-                for (uint32_t q = 0; q < 8; ++q) {
-                    uint32_t x = (uint32_t)((((uint64_t)raw[q + 1] << 32) | raw[q]) >> (8u * sh));
-                    const uint32_t have = nv > 4u * q ? nv - 4u * q : 0u;  // bytes of this dword that are bases
-                    x = have >= 4u ? x : (have ? x & ((1u << (8u * have)) - 1u) : 0u);
-                    if (q < 4) code0 |= dna5_codes4(x) << (8u * q);
-                    else code1 |= dna5_codes4(x) << (8u * (q - 4u));
-                    nmw |= dna5_n4(x) << (4u * q);
-                }
-                // the record's N positions, in window order (a window holds <= 256 bases)
-                for (uint32_t m = nmw; m; m &= m - 1u) {
-                    if (cnt < cap) pos |= (32u * b + (uint32_t)__builtin_ctz(m)) << nrec_pos_shift(pb, cnt);
-                    ++cnt;
-                }
-                const uint32_t cw = cw_w + 2u * b;
-                const bool mine = cw >= cw_lo && cw < cw_hi;  // (a block never straddles a chunk)
-                if (b + 1u == nblk) {  // the slot's last block: its second word takes the record
-                    last_lo = code0;
-                    last_hi = code1;
-                } else if (mine) {
-                    __builtin_amdgcn_raw_buffer_store_b64(v2u{code0, code1}, rc, cw * 4u, 0, 16);  // sc1
-                }
-                if (mine) __builtin_amdgcn_raw_buffer_store_b32(nmw, rn, cw * 2u, 0, 16);
-            }
+            for (uint32_t i = 0; i < PB; ++i)
+                if (b0 + i < pc.nblk) pack_block(pc, d[i][0], d[i][1], e[i], b0 + i, ok, sh, w * pc.SW, o);
         }
-        if (rec && cnt) last_hi |= cnt <= cap ? (pos | cnt << 29) : (NREC_OVERFLOW << 29);
-        const uint32_t cw = cw_w + SW - 2u;
-        if (cw >= cw_lo && cw < cw_hi) __builtin_amdgcn_raw_buffer_store_b64(v2u{last_lo, last_hi}, rc, cw * 4u, 0, 16);
+        pack_finish(pc, rec, w * pc.SW, o);
     }
     if (__ballot(bad != 0u) && lane == 0) atomicOr(err, AC_DEVERR_WINDOW);
 }
@@ -578,7 +600,8 @@ __device__ __attribute__((noinline)) bool stage_copy(const uint8_t* src, uint8_t
 // bytes (stage_pack_chunk), N-bitmap chunks have no work of their own (their words are stored by the
 // codes chunks' owners); then, as in stage_copy, the chunk's flag and the done replicas -- only once
 // `fin` is out, so a reader that sees the segment complete reads its verdict.  Inlined into the
-// kernel (its registers then come from the kernel's budget: as a called function it spilled).
+// kernel: as a called function its registers came from the budget of the 8-wave kernels (64 VGPRs)
+// and it spilled inside the packing loop.
 __device__ __forceinline__ bool stage_copy_dp(const SegDev& sg, uint32_t* words, uint32_t gen, uint32_t* err) {
     const uint32_t lane = threadIdx.x & 63u;
     const StageWords sw = stage_words(words);

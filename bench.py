@@ -89,6 +89,7 @@ def parse():
     ap.add_argument("--no-kernel-leg", action="store_true",
                     help="skip the device-resident kernel timing (and with it the roofline)")
     ap.add_argument("--no-pipelined", action="store_true", help="skip the informational pipelined leg")
+    ap.add_argument("--no-exact", action="store_true", help="skip the exact-count block (SURVEY.md 8(f) rank 1)")
     ap.add_argument("--verify", action="store_true", help="check the stage's counts against the oracle (slow)")
     ap.add_argument("--shard", metavar="R/N",
                     help="rehearsal on one GPU: time rank R's shard of an N-rank strong-scaling run alone "
@@ -211,6 +212,86 @@ def cpu_baseline(wl, k, seconds):
     out["one_thread"] = {"value": v1, "threads": 1,
                          "sample": f"a prefix (<= 5%) of the candidates of both ends over all windows ({units:.4g} kmer*bp) x {reps} "
                                    f"= {dt:.1f} s"}
+    return out
+
+
+EXACT_CONFIGS = {  # the exact count (count_kmers + get_most_frequent) at BASELINE's sample sizes, start windows
+    "cfg3": dict(n=100_000, L=100, k=16, lim=2000),
+    "cfg4": dict(n=1_000_000, L=100, k=16, lim=500),
+    "cfg5": dict(n=100_000, L=150, k=22, lim=1000),
+}
+
+
+def exact_block(dev_index: int, calls: int = 10):
+    """Row f1: ac_exact_count_device -- count_kmers (approx_counter.cpp:487-519) with
+    the low-complexity / N / forbidden filters and get_most_frequent's top-lim (396-405) -- on a sample
+    resident in HBM, at cfg3 / cfg4 / cfg5's sizes, against the HBM roofline of its partitioned passes
+    (DESIGN.md 4b): the image read once (0.375 B/base), then per k-mer position a B-byte key (4 B for
+    k <= 16, 8 B above) written by the keys pass and moved through 7 more streaming touches (level-1
+    histogram read, scatter read + write, level-2 histogram read, scatter read + write, count read).
+    `pmc` = the committed rocprof FETCH_SIZE (x2, MI355X_MICROARCH.md's gfx950 correction) and WRITE_SIZE
+    per call, summed over the call's kernels (profiles/*_exact_pmc.json), when present."""
+    import ctypes
+
+    import approx_counter_amd as ac
+    from approx_counter_amd import _lib
+    from approx_counter_amd.counter import _ptr
+    from tools.synth import make_windows_fast
+    from tools.workload import adjust_threshold
+
+    L = _lib.load()
+    pmc = {}
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_exact_pmc.json"))):
+        try:
+            pmc.update(json.load(open(path)))
+        except (OSError, ValueError):
+            pass
+    out = {}
+    with ac.ApproxCounter(dev_index) as c:
+        for name, cfg in EXACT_CONFIGS.items():
+            k, lim = cfg["k"], cfg["lim"]
+            w2d, _ = make_windows_fast(cfg["n"], cfg["L"], seed=1)
+            sample = ac.pack_windows(w2d)
+            del w2d
+            hw, dw = sample.as_struct(), _lib.ACWindows()
+            ac.counter.check(L.ac_sample_upload(c.handle, ctypes.byref(hw), ctypes.byref(dw)), c.handle)
+            thr = float(adjust_threshold(1.0, 16, k))
+            km, ct = np.zeros(lim, np.uint64), np.zeros(lim, np.uint64)
+            fb = np.zeros(1, np.uint64)
+            n_out, n_dist, had_n = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+
+            def once():
+                ac.counter.check(L.ac_exact_count_device(
+                    c.handle, k, ctypes.byref(dw), thr, _ptr(fb, ctypes.c_uint64), 0, lim, 0, _ptr(km, ctypes.c_uint64),
+                    _ptr(ct, ctypes.c_uint64), lim, ctypes.byref(n_out), ctypes.byref(n_dist), ctypes.byref(had_n)),
+                    c.handle)
+
+            for _ in range(3):
+                once()
+            times = []
+            for _ in range(calls):
+                t0 = time.perf_counter()
+                once()
+                times.append(time.perf_counter() - t0)
+            ms = float(np.median(times)) * 1e3
+            n_pos = cfg["n"] * max(0, cfg["L"] - k + 1)
+            key_b = 4 if k <= 16 else 8
+            alg = SAMPLE_BYTES_PER_BASE * sample.n_bases + 8 * key_b * n_pos
+            row = {"ms": ms, "ms_min": float(min(times)) * 1e3, "path": {1: "partitioned", 0: "hash table"}.get(
+                       c.exact_path(), "?"), "windows": cfg["n"], "L": cfg["L"], "k": k, "lim": lim,
+                   "kmer_positions": n_pos, "distinct": int(n_dist.value),
+                   "algorithmic_bytes": alg, "achieved_GBps": alg / (ms * 1e-3) / 1e9,
+                   "frac_hbm": alg / (ms * 1e-3) / HBM_PEAK}
+            if name in pmc:
+                row["pmc"] = pmc[name]
+                tb = pmc[name].get("traffic_bytes_per_call")
+                if tb:
+                    row["traffic_GBps"] = tb / (ms * 1e-3) / 1e9
+            out[name] = row
+    out["note"] = ("ac_exact_count_device, sample resident in HBM (synthetic start windows, tools/synth."
+                   "make_windows_fast seed 1), median of %d synchronous calls incl. the host's CompareCount "
+                   "ranking of the short list; algorithmic bytes = 0.375 B/base + 8 streaming touches x key "
+                   "bytes per k-mer position (DESIGN.md 4b); peak 8 TB/s" % calls)
     return out
 
 
@@ -568,6 +649,8 @@ def main():
                                    "algorithmic_bytes_per_launch": sample_bytes}
         if pipelined:
             out["pipelined"] = pipelined
+        if not args.no_exact and world == 1 and not args.shard:
+            out["exact"] = exact_block(local)
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(wl, args.k, args.cpu_seconds)
         print(json.dumps(out), flush=True)

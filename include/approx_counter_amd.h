@@ -370,8 +370,9 @@ ac_status ac_allreduce_counts(ac_ctx* ctx, uint32_t* d_counts, uint64_t n, void*
  * the first ac_create: the CPUs local to the GPU's PCIe root, split among the
  * local ranks (LOCAL_RANK / LOCAL_WORLD_SIZE, local rank r on device r mod the
  * visible devices) whose GPUs share them -- disjoint runs of physical cores per
- * rank -- with at most min(16, this rank's share of the cgroup CPU quota)
- * participants (the calling thread included).
+ * rank -- with at most min(16, this rank's share of the cgroup CPU quota less
+ * 2 CPUs of headroom, 1 for a share of 4 or less) participants (the calling
+ * thread included): a pool spinning on the whole quota was throttled by the CFS.
  *   ac_set_host_cpus   the pool's CPUs and participants (0 = min(16, n_cpus))
  *                      instead; only before the first ac_create
  *                      (AC_ERR_INVALID afterwards)

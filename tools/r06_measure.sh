@@ -23,8 +23,8 @@ run() {  # name timeout cmd...
   grep -h 'passed\|failed\|"ms_per_step"\|"step_ms"' "$OUT/$name.log" | cut -c1-600 | tee -a "$OUT/summary.log"
 }
 PYT="python3 -u -m pytest -x -v --timeout 300 --timeout-method thread -p no:cacheprovider"
-BQ="--no-cpu-baseline --no-pipelined"
-B="python3 bench.py --steps 400 --warmup 20 --no-cpu-baseline --no-pipelined --no-kernel-leg"
+BQ="--no-cpu-baseline --no-pipelined --no-exact"
+B="python3 bench.py --steps 400 --warmup 20 --no-cpu-baseline --no-pipelined --no-kernel-leg --no-exact"
 S="python3 tools/stall_check.py"
 cat /sys/fs/cgroup/cpu.max /sys/fs/cgroup/cpu.stat > "$OUT/cgroup.txt" 2>&1
 for part in "$@"; do
@@ -42,7 +42,8 @@ stallpin)
   run stallpin_cfg4 400 $S --config cfg4 --steps 100 --pinned ;;
 tests)
   run tests_dp 600 $PYT -m gpu tests/test_gpu_device_pack.py
-  run tests_jobs 600 $PYT -m gpu tests/test_gpu_jobs.py tests/test_gpu_bench_path.py ;;
+  run tests_jobs 600 $PYT -m gpu tests/test_gpu_jobs.py tests/test_gpu_bench_path.py
+  run tests_exact 600 $PYT -m gpu tests/test_gpu_exact.py ;;
 suite)
   run suite 1100 $PYT -m gpu tests ;;
 bench)
@@ -63,6 +64,32 @@ abbig)  # cfg3 / cfg5 / cfg4 and one rank's cfg4 shard: device vs host packing
   done
   run shard_dev 300 python3 bench.py --config cfg4 --shard 0/8 --steps 50 --warmup 5 $BQ --no-kernel-leg --sample pinned
   run shard_heap_t2 300 env AC_HOST_THREADS=2 python3 bench.py --config cfg4 --shard 0/8 --steps 50 --warmup 5 $BQ --no-kernel-leg --sample heap ;;
+exactpmc)  # rocprof FETCH_SIZE / WRITE_SIZE passes and a kernel trace of the exact count at cfg3 / cfg4 / cfg5
+  export TMPDIR=/tmp
+  for spec in "cfg3 100000 100 16 2000" "cfg4 1000000 100 16 500" "cfg5 100000 150 22 1000"; do
+    set -- $spec
+    EX="python3 tools/bench_exact.py --fast --reads $2 --sl $3 --k $4 --lim $5 --steps 5 --warmup 2 --no-host"
+    run exact_$1_fetch 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/exact_$1_fetch" -o run -- $EX
+    run exact_$1_write 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/exact_$1_write" -o run -- $EX
+    run exact_$1_trace 120 rocprofv3 --kernel-trace --stats -d "$OUT/exact_$1_trace" -o run -- $EX
+    run exact_$1_json 60 python3 tools/exact_pmc.py --config $1 --fetch "$OUT/exact_$1_fetch" --write "$OUT/exact_$1_write" --out "$OUT/$1_exact_pmc.json"
+  done ;;
+xab)  # exact-count count-kernel variants (tools/variants.sh xpack*agg*), cfg4 and cfg5, x2 interleaved
+  for rep in 1 2; do for v in xpack0agg0 xpack0agg1 xpack1agg0 xpack1agg1; do
+    run xab_${v}_cfg4_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so python3 tools/bench_exact.py --fast --reads 1000000 --lim 500 --steps 10 --no-host
+    run xab_${v}_cfg5_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so python3 tools/bench_exact.py --fast --reads 100000 --sl 150 --k 22 --lim 1000 --steps 10 --no-host
+  done; done ;;
+abdev)  # cfg2 stage: device packing (16 / 32 / 64 copier workgroups) vs host packing of a heap sample
+  for rep in 1 2 3; do
+    run abdev_dev16_$rep 120 $B --sample pinned
+    run abdev_heap_$rep 120 $B --sample heap
+    run abdev_dev32_$rep 120 env AC_COPIER_WGS=32 $B --sample pinned
+    run abdev_dev64_$rep 120 env AC_COPIER_WGS=64 $B --sample pinned
+  done ;;
+stall2)  # the default pool (quota - 2 since r06_m3) at cfg2 for 10 s and cfg5 for 200 steps
+  run stall2_cfg2 120 $S --config cfg2 --seconds 10
+  run stall2_cfg5 300 $S --config cfg5 --steps 200
+  run stall2_cfg3 300 $S --config cfg3 --steps 300 ;;
 *) echo "unknown part $part" ;;
 esac
 done
