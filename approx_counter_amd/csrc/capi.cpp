@@ -1507,10 +1507,23 @@ ac_status ac_host_free(void* p) {
 // ac_error_count_jobs: the whole errorCount stage from Dna5 host buffers.
 namespace {
 
-// Device packing of jobs whose samples lie in ac_host_alloc blocks (default on; AC_DEVICE_PACK=0 packs
-// every job on the host, for A/B runs).
-bool device_pack_enabled() {
-    static const bool v = env_int("AC_DEVICE_PACK", 1) != 0;
+// Device packing of jobs whose samples lie in ac_host_alloc blocks: 2 = auto (default),
+// 1 = every eligible job (AC_DEVICE_PACK=1), 0 = never (AC_DEVICE_PACK=0: the host pool packs).
+int device_pack_mode() {
+    static const int v = [] {
+        const char* e = std::getenv("AC_DEVICE_PACK");
+        return (e && *e) ? (std::atoi(e) ? 1 : 0) : 2;
+    }();
+    return v;
+}
+// Auto: the kernel packs a call of at least this many windows, or any call when the host pool has at
+// most 2 participants (a rank's share of the node).  Below it the host pool, which packs a cfg2 call in
+// a few microseconds, is ahead: cfg2 stage 0.1145-0.1149 ms host-packed against 0.1262-0.1292 device-
+// packed (the image crosses PCIe as 1 B/base instead of 0.25, 2 MB per call; profiles/r06_m4/abdev_*);
+// at cfg3-cfg5 the two are within 1-3 % and the device-packed steps have no host-side tail
+// (profiles/r06_m3/stall*, abbig_*).
+uint64_t device_pack_min_windows() {
+    static const uint64_t v = (uint64_t)std::max(0, env_int("AC_DEVICE_PACK_MIN_WINDOWS", 1 << 16));
     return v;
 }
 
@@ -1864,7 +1877,8 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
     const uint64_t* dp_off[AC_MAX_JOBS] = {};
     uint32_t dp_bytes[AC_MAX_JOBS] = {};
     p.dp_any = false;
-    if (p.early && p.pre == 0 && device_pack_enabled())
+    const int dpm = (g_test_hooks.load(std::memory_order_relaxed) & AC_TESTING_DEVICE_PACK) ? 1 : device_pack_mode();
+    if (p.early && p.pre == 0 && (dpm == 1 || (dpm == 2 && (total_w >= device_pack_min_windows() || pool.size() <= 2))))
         for (uint32_t j = 0; j < p.n; ++j) {
             p.dp[j] = false;
             const ac_dna5_windows& w = jobs[j].sample;

@@ -30,6 +30,9 @@ extern "C" {
  * records: a host slower in total than the kernel's 0.5 s timeout, whose every
  * gap is not (the waits restart their clock on progress). */
 #define AC_TESTING_SLOW_HOST 4u
+/* Device packing (ABI 7) for every eligible job, whatever the call's size: the
+ * default policy leaves small calls to the host pool. */
+#define AC_TESTING_DEVICE_PACK 8u
 
 /* Sets the hooks (an OR of the flags above); returns the previous value. */
 uint32_t ac_testing_stage_hooks(uint32_t flags);

@@ -2,9 +2,9 @@
 
 bench.py's `value` is `ac_error_count_jobs` on cfg2 (k=16, 2 x 10k windows of
 100 / 101 bases, 0.1 % N, 500 candidates per end, seed 1): the early launch
-(`ac_stage_mode() == 3` on the sample in ac_host_alloc memory, the bench's default since round 6:
-the kernel's copier workgroups pack the Dna5 bytes themselves; `== 2` on ordinary memory, the host
-pool packing), i.e. `wm2_count_kernel<2, STAGED, EQ>` staging its own inputs.  Its N > 1 steps go through
+(`ac_stage_mode() == 2`: the host pool packs a cfg2 call, on ordinary or pinned memory; a pinned
+call of >= 2^16 windows, such as one rank's cfg4 shard, is packed by the kernel's copier workgroups
+themselves, `== 3`), i.e. `wm2_count_kernel<2, STAGED, EQ>` staging its own inputs.  Its N > 1 steps go through
 `ac_error_count_jobs_submit` on one rank's shard.  Both are checked here over
 EVERY candidate and window against `oracle.count_myers` (errorCount,
 approx_counter.cpp:531-601), on the very workload objects bench.py builds
@@ -43,7 +43,7 @@ def test_bench_cfg2_stage_bit_exact(where):
     """cfg2 as bench.py times it: the synchronous early launch, 6 calls on one context (both
     staging slots, three times each), then the submit form the N > 1 steps use; on the sample in
     pinned memory (device packing, bench --sample pinned, the default) and in ordinary memory."""
-    mode = 3 if where == "pinned" else 2
+    mode = 2  # (cfg2's 20k windows are host-packed on pinned memory too: the default policy, DESIGN.md 4d)
     import torch
 
     args = _bench_args("cfg2")
@@ -88,7 +88,7 @@ def test_bench_cfg4_rank_shard_submit_bit_exact(rank, where):
         for _ in range(2):
             c.submit_jobs(16, jobs, out, stream=st.cuda_stream)
         c.check(stream=st.cuda_stream)
-        assert c.stage_mode() == (3 if where == "pinned" else 2)
+        assert c.stage_mode() == (3 if where == "pinned" else 2)  # (250k windows: device-packed when pinned)
         got = out.cpu().numpy().view(np.uint32).astype(np.uint64)
         assert np.array_equal(got, np.concatenate(exp))
         sync = c.count_jobs(16, jobs)
@@ -107,11 +107,12 @@ def test_bench_line_reports_the_pool_that_ran():
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, AC_HOST_THREADS="3")
-    for sample, path, text in (("heap", "early-launch", "issued first in the call"),
-                               ("pinned", "early-launch-device-pack", "the host packs nothing")):
+    for sample, dp, path, text in (("heap", "", "early-launch", "issued first in the call"),
+                                   ("pinned", "", "early-launch", "issued first in the call"),
+                                   ("pinned", "1", "early-launch-device-pack", "the host packs nothing")):
         r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "3", "--warmup", "1",
-                            "--no-cpu-baseline", "--no-pipelined", "--no-kernel-leg", "--sample", sample],
-                           env=env, capture_output=True, text=True, timeout=300)
+                            "--no-cpu-baseline", "--no-pipelined", "--no-kernel-leg", "--no-exact", "--sample", sample],
+                           env=dict(env, AC_DEVICE_PACK=dp), capture_output=True, text=True, timeout=300)
         assert r.returncode == 0, r.stderr[-2000:]
         line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
         assert line["host_pool"]["participants"] == 3

@@ -18,6 +18,19 @@ from tests import cases
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 pytestmark = pytest.mark.gpu
+AC_TESTING_DEVICE_PACK = 8  # include/approx_counter_amd_testing.h: device packing whatever the call's size
+
+
+@pytest.fixture(autouse=True)
+def _device_pack_every_call():
+    """These calls are small (the default policy packs calls under 2^16 windows on the host):
+    force device packing for every eligible job while a test runs."""
+    from approx_counter_amd import _lib
+
+    L = _lib.load()
+    prev = L.ac_testing_stage_hooks(AC_TESTING_DEVICE_PACK)
+    yield
+    L.ac_testing_stage_hooks(prev)
 
 
 def _equal(wins, L):
@@ -180,6 +193,9 @@ def pinned_rotation(calls=24):
     """Rotates pinned (device-packed) and ordinary (host-packed) workloads of different sizes,
     N patterns and lengths through one context, alternating staging slots: a stale line, an early
     completion or a wrong N decision shows up as a wrong count."""
+    from approx_counter_amd import _lib
+
+    _lib.load().ac_testing_stage_hooks(AC_TESTING_DEVICE_PACK)
     work = []
     for seed, (nw, L, p_n, pin) in enumerate([(900, 100, 0.0, True), (2500, 101, 0.02, True), (400, 100, 0.01, False),
                                               (6000, 100, 0.07, True), (3000, 150, 0.0, True),
@@ -203,6 +219,29 @@ def test_device_pack_rotating_inputs_bit_exact():
     code = "from tests.test_gpu_device_pack import pinned_rotation; pinned_rotation(28); print('OK')"
     r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, PYTHONPATH=ROOT), capture_output=True,
                        text=True, timeout=200, cwd=ROOT)
+    assert r.returncode == 0 and "OK" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])
+
+
+def test_device_pack_policy_small_call_host_large_call_device():
+    """The default policy (no hook): a pinned call under 2^16 windows is packed by the host pool (stage
+    mode 2, faster there: DESIGN.md 4d), one of 2^16 windows or more by the kernel (mode 3)."""
+    code = ("import numpy as np, approx_counter_amd as ac, oracle\n"
+            "from tests import cases\n"
+            "km, w = cases.planted_case(9600, 16, 200, 3000, win_len=(100, 100), p_n=0.01)\n"
+            "w = [(x + 'A' * 100)[:100] for x in w]\n"
+            "big = w * 23\n"  # 69,000 windows
+            "c = ac.ApproxCounter(0)\n"
+            "g = c.count_jobs(16, ac.Jobs([(km, ac.Dna5Sample.from_windows(w).pinned())]))\n"
+            "assert c.stage_mode() == 2, c.stage_mode()\n"
+            "e = oracle.count_myers(16, km, w)\n"
+            "assert np.array_equal(g[0], e)\n"
+            "g = c.count_jobs(16, ac.Jobs([(km, ac.Dna5Sample.from_windows(big).pinned())]))\n"
+            "assert c.stage_mode() == 3, c.stage_mode()\n"
+            "assert np.array_equal(g[0], 23 * e)\n"
+            "c.close(); print('OK')\n")
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    env.pop("AC_DEVICE_PACK", None)
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=200, cwd=ROOT)
     assert r.returncode == 0 and "OK" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])
 
 

@@ -41,8 +41,8 @@ stallpin)
   run stallpin_cfg5 300 $S --config cfg5 --steps 200 --pinned
   run stallpin_cfg4 400 $S --config cfg4 --steps 100 --pinned ;;
 tests)
-  run tests_dp 600 $PYT -m gpu tests/test_gpu_device_pack.py
-  run tests_jobs 600 $PYT -m gpu tests/test_gpu_jobs.py tests/test_gpu_bench_path.py
+  run tests_dp 600 $PYT -m gpu tests/test_gpu_device_pack.py tests/test_gpu_bench_path.py
+  run tests_jobs 600 $PYT -m gpu tests/test_gpu_jobs.py
   run tests_exact 600 $PYT -m gpu tests/test_gpu_exact.py ;;
 suite)
   run suite 1100 $PYT -m gpu tests ;;
@@ -90,6 +90,26 @@ stall2)  # the default pool (quota - 2 since r06_m3) at cfg2 for 10 s and cfg5 f
   run stall2_cfg2 120 $S --config cfg2 --seconds 10
   run stall2_cfg5 300 $S --config cfg5 --steps 200
   run stall2_cfg3 300 $S --config cfg3 --steps 300 ;;
+host8)  # 8 processes at once, each one rank's host-side work per step (submit of its 1/8 cfg4 shard), x2
+  for rep in 1 2; do
+    run host8_pinned_$rep 400 python3 tools/host8.py --sample pinned
+    run host8_heap_$rep 400 python3 tools/host8.py --sample heap
+  done ;;
+shardload)  # rank 0's 1/8 cfg4 shard on the GPU with 7 host-packing load processes beside it
+  run shardload_pinned 500 python3 tools/shard_load.py --sample pinned
+  run shardload_heap 500 python3 tools/shard_load.py --sample heap ;;
+stall3)  # cfg3 tails: device-packed (pinned), and host-packed with workers pinned to the whole CPU set
+  run stall3_cfg3_pinned 300 $S --config cfg3 --steps 300 --pinned
+  run stall3_cfg3_pinset 300 env AC_HOST_PIN=set $S --config cfg3 --steps 300
+  run stall3_cfg3_default 300 $S --config cfg3 --steps 300 ;;
+wpb)  # count kernel on resident input: 4 / 8 / 16 waves per workgroup (tools/variants.sh base wpb8 wpb16)
+  export TMPDIR=/tmp
+  for c in cfg2 cfg5; do
+    run wpb_$c 400 bash tools/kernel_ab.sh "base wpb8 wpb16" $c
+  done ;;
+stamps)  # per-wave timelines of the resident cfg2 launch, 4- and 16-wave workgroups (-DAC_STAMPS builds)
+  run stamps_base 120 env APPROX_COUNTER_AMD_LIB=build/var/stamps/libapprox_counter_amd.so python3 tools/stamps.py
+  run stamps_wpb16 120 env APPROX_COUNTER_AMD_LIB=build/var/stamps16/libapprox_counter_amd.so python3 tools/stamps.py ;;
 *) echo "unknown part $part" ;;
 esac
 done
