@@ -1510,6 +1510,9 @@ namespace {
 // Device packing of jobs whose samples lie in ac_host_alloc blocks: 2 = auto (default),
 // 1 = every eligible job (AC_DEVICE_PACK=1), 0 = never (AC_DEVICE_PACK=0: the host pool packs).
 int device_pack_mode() {
+#ifdef AC_NO_DEVICE_PACK
+    return 0;  // (A/B builds: the kernel has no device packer)
+#endif
     static const int v = [] {
         const char* e = std::getenv("AC_DEVICE_PACK");
         return (e && *e) ? (std::atoi(e) ? 1 : 0) : 2;

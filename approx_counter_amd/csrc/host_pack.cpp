@@ -286,7 +286,11 @@ WorkPool& host_pool() {
         g_plan.cpus = use;
         const char* pin = std::getenv("AC_HOST_PIN");
         if (pin && std::atoi(pin) == 0) use.clear();
-        const bool pin_each = !(pin && std::string(pin) == "set");
+        // Each worker may run on any CPU of the set (AC_HOST_PIN=each: one CPU per worker, the round-5
+        // default): a worker pinned to one CPU waits out another tenant's time slice on it while holding
+        // a claimed task, and the call waits with it -- cfg3, 300 steps: p99 / p50 1.117, max 10.1 ms
+        // pinned each vs 1.016, max 3.15 ms on the set, p50 equal (profiles/r06_m6/stall3_*).
+        const bool pin_each = pin && std::string(pin) == "each";
         return WorkPool(n, use, pin_each);
     }();
     return pool;

@@ -92,8 +92,8 @@ HostPlan host_plan();  // the plan in force (after the pool's creation: what it 
 // AC_HOST_THREADS environment variable, else the plan's participants, else
 // min(16, CPUs this process may run on); AC_HOST_THREADS=1 packs on the
 // calling thread alone.  Workers are pinned to the plan's CPUs (minus those
-// the process may not use): AC_HOST_PIN=0 disables, AC_HOST_PIN=set pins every
-// worker to the whole set instead of one CPU each.
+// the process may not use), each to the whole set: AC_HOST_PIN=0 disables,
+// AC_HOST_PIN=each pins worker i to one CPU of it instead.
 WorkPool& host_pool();
 // CPUs of a sysfs cpulist file / text ("0-63,128-191"), sorted; empty if unreadable.
 std::vector<int> read_cpulist(const char* path);

@@ -863,11 +863,17 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
                 const uint32_t s2 = (blockIdx.x + i2) % a.n_segs;
                 const SegDev& c2 = a.seg[s2];
                 if (!c2.stage_chunks) continue;
+#ifndef AC_NO_DEVICE_PACK
                 const bool ok = c2.dp_src
                                     ? stage_copy_dp(c2, a.stage + AC_STAGE_L_SEG(s2) * AC_QUEUE_LINE, a.gen, a.err)
                                     : stage_copy(c2.stage_src, c2.stage_dst, c2.stage_chunks,
                                                  c2.stage_codes_off / AC_STAGE_CHUNK, a.host_hdr + s2 * AC_QUEUE_LINE,
                                                  a.stage + AC_STAGE_L_SEG(s2) * AC_QUEUE_LINE, c2.stage_gen, a.gen, s2);
+#else  // (A/B builds without the device packer: its code out of the staged kernel, the host never asks for it)
+                const bool ok = stage_copy(c2.stage_src, c2.stage_dst, c2.stage_chunks, c2.stage_codes_off / AC_STAGE_CHUNK,
+                                           a.host_hdr + s2 * AC_QUEUE_LINE, a.stage + AC_STAGE_L_SEG(s2) * AC_QUEUE_LINE,
+                                           c2.stage_gen, a.gen, s2);
+#endif
                 if (!__builtin_amdgcn_readfirstlane((uint32_t)ok))
                     if (lane == 0) atomicOr(a.err, AC_DEVERR_STAGE);
             }

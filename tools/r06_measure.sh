@@ -110,6 +110,28 @@ wpb)  # count kernel on resident input: 4 / 8 / 16 waves per workgroup (tools/va
 stamps)  # per-wave timelines of the resident cfg2 launch, 4- and 16-wave workgroups (-DAC_STAMPS builds)
   run stamps_base 120 env APPROX_COUNTER_AMD_LIB=build/var/stamps/libapprox_counter_amd.so python3 tools/stamps.py
   run stamps_wpb16 120 env APPROX_COUNTER_AMD_LIB=build/var/stamps16/libapprox_counter_amd.so python3 tools/stamps.py ;;
+abnodp)  # host-packed stage with and without the device packer compiled into the staged kernel
+  for rep in 1 2 3; do
+    run abnodp_cur_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/cur/libapprox_counter_amd.so $B --sample heap
+    run abnodp_nodp_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/nodp/libapprox_counter_amd.so $B --sample heap
+  done
+  for c in cfg5 cfg3; do
+    run abnodp_cur_$c 300 env APPROX_COUNTER_AMD_LIB=build/var/cur/libapprox_counter_amd.so python3 bench.py --config $c --steps 20 --warmup 5 $BQ --no-kernel-leg --sample heap
+    run abnodp_nodp_$c 300 env APPROX_COUNTER_AMD_LIB=build/var/nodp/libapprox_counter_amd.so python3 bench.py --config $c --steps 20 --warmup 5 $BQ --no-kernel-leg --sample heap
+  done ;;
+xab2)  # count kernel: CAS as the probe, 4 / 16 keys per thread per batch, vs the current (cur)
+  for rep in 1 2; do for v in cur xcas xb16 xb4; do
+    run xab2_${v}_cfg4_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so python3 tools/bench_exact.py --fast --reads 1000000 --lim 500 --steps 10 --no-host
+  done; done ;;
+pin)  # host pool workers on the whole CPU set (default since r06_m6) vs one CPU each: cfg2 stage and tails
+  for rep in 1 2 3; do
+    run pin_set_$rep 120 $B --sample heap
+    run pin_each_$rep 120 env AC_HOST_PIN=each $B --sample heap
+  done
+  run pinstall_cfg2_set 120 $S --config cfg2 --seconds 10
+  run pinstall_cfg2_each 120 env AC_HOST_PIN=each $S --config cfg2 --seconds 10
+  run pinstall_cfg3_set 300 $S --config cfg3 --steps 300
+  run pinstall_cfg5_set 300 $S --config cfg5 --steps 200 ;;
 *) echo "unknown part $part" ;;
 esac
 done
