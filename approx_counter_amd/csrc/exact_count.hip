@@ -977,13 +977,7 @@ __device__ __forceinline__ float key_complexity(uint64_t key, uint32_t k) { retu
 constexpr uint32_t COUNT_THREADS = AC_COUNT_THREADS;
 constexpr uint32_t COUNT_APPEND = 2 * COUNT_THREADS;
 
-#ifndef AC_COUNT_BATCH
-#define AC_COUNT_BATCH 8
-#endif
-constexpr uint32_t COUNT_BATCH = AC_COUNT_BATCH;  // keys per thread loaded together (one memory latency per batch)
-#ifndef AC_COUNT_CAS_FIRST
-#define AC_COUNT_CAS_FIRST 0
-#endif
+constexpr uint32_t COUNT_BATCH = 8;  // keys per thread loaded together (one memory latency per batch)
 
 template <class K>
 __global__ __launch_bounds__(COUNT_THREADS) void part_count_kernel(ExactArgs a) {
@@ -1062,15 +1056,9 @@ __global__ __launch_bounds__(COUNT_THREADS) void part_count_kernel(ExactArgs a) 
                     uint32_t h = part_hash(key) & (SLOTS - 1u);
                     uint32_t probe = 0;
                     for (; probe < COUNT_PROBES; ++probe) {
-#if AC_COUNT_CAS_FIRST  // (A/B builds: the CAS as the probe, no read first)
-                        K cur = 0u;
-                        {
-                            cur = atomicCAS(&tk[h], (K)0, stored);
-#else
                         K cur = tk[h];
                         if (cur == 0u) {
                             cur = atomicCAS(&tk[h], (K)0, stored);
-#endif
                             if (cur == 0u) {  // claimed: list the slot for scoring and clearing
                                 cur = stored;
                                 occ[atomicAdd(&n_occ, 1u)] = (uint16_t)h;

@@ -132,6 +132,22 @@ pin)  # host pool workers on the whole CPU set (default since r06_m6) vs one CPU
   run pinstall_cfg2_each 120 env AC_HOST_PIN=each $S --config cfg2 --seconds 10
   run pinstall_cfg3_set 300 $S --config cfg3 --steps 300
   run pinstall_cfg5_set 300 $S --config cfg5 --steps 200 ;;
+final1)  # the round's end: whole GPU suite, smoke, the default bench line twice
+  run suite 1200 $PYT -m gpu tests
+  run smoke 300 python3 -c 'import __graft_entry__ as g; g.smoke()'
+  run bench_cfg2_a 400 python3 bench.py
+  run bench_cfg2_b 400 python3 bench.py --no-cpu-baseline ;;
+final2)  # rocprof evidence: the bench's kernel trace, the count kernel's PMC passes, cfg3-cfg5 lines
+  export TMPDIR=/tmp
+  run bench_trace 300 rocprofv3 --kernel-trace --stats -d "$OUT/bench_trace" -o run -- python3 bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-pipelined --no-exact
+  run pmc_fetch 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run -- python3 tools/kernel_run.py --config cfg2 --launches 20
+  run pmc_write 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run -- python3 tools/kernel_run.py --config cfg2 --launches 20
+  run pmc_sq 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_INSTS_SALU SQ_INSTS_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY -d "$OUT/pmc_sq" -o run -- python3 tools/kernel_run.py --config cfg2 --launches 20
+  run pmc_json 60 python3 tools/pmc_traffic.py --fetch "$OUT/pmc_fetch" --write "$OUT/pmc_write" --valu "$OUT/pmc_sq" --workload "cfg2: k=16 sn=10000 sl=100 lim=500, start+end ends fused, 10000 reads/rank" --out "$OUT/r06_cfg2_pmc_traffic.json"
+  run kern_trace 200 rocprofv3 --kernel-trace --stats -d "$OUT/kern_trace" -o run -- python3 tools/kernel_run.py --config cfg2 --launches 50 --warmup 150
+  for c in cfg3 cfg5 cfg4; do
+    run bench_$c 400 python3 bench.py --config $c --steps 20 --warmup 5 --no-cpu-baseline --no-pipelined --no-exact
+  done ;;
 *) echo "unknown part $part" ;;
 esac
 done
