@@ -112,8 +112,6 @@ def load():
     for fn in (L.ac_exact_count, L.ac_exact_count_device):
         fn.argtypes = exact
         fn.restype = ctypes.c_int
-    L.ac_error_count_sample.argtypes = [vp, ctypes.c_uint32, p64, ctypes.c_uint32, ctypes.POINTER(ACWindows), p64]
-    L.ac_error_count_sample.restype = ctypes.c_int
     L.ac_sample_upload_slot.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ACWindows), ctypes.POINTER(ACWindows)]
     L.ac_sample_upload_slot.restype = ctypes.c_int
     for fn in (L.ac_error_count_samples, L.ac_error_count_images):
@@ -135,9 +133,6 @@ def load():
     if hasattr(L, "ac_testing_stage_hooks"):  # (an A/B build of an older ABI may lack it)
         L.ac_testing_stage_hooks.argtypes = [ctypes.c_uint32]
         L.ac_testing_stage_hooks.restype = ctypes.c_uint32
-    if hasattr(L, "ac_idle"):  # (ABI >= 5; A/B builds of older ABIs lack it)
-        L.ac_idle.argtypes = [vp]
-        L.ac_idle.restype = ctypes.c_int
     if hasattr(L, "ac_host_alloc"):  # (ABI >= 7; A/B builds of older ABIs lack it)
         L.ac_host_alloc.argtypes = [ctypes.c_size_t, ctypes.POINTER(vp)]
         L.ac_host_alloc.restype = ctypes.c_int

@@ -325,12 +325,6 @@ class ApproxCounter:
         """ac_exact_path: 1 partitioned, 0 hash table, -1 no exact count yet."""
         return int(self._L.ac_exact_path(self._h))
 
-    def idle(self) -> None:
-        """ac_idle (ABI >= 5): since ABI 6 no call leaves device work behind it, so this only checks
-        the context (kept for callers written against ABI 5's armed launches)."""
-        if hasattr(self._L, "ac_idle"):
-            check(self._L.ac_idle(self._h), self._h)
-
     def stage_mode(self) -> int:
         """ac_stage_mode: the last jobs call's stage -- 2 early launch (the count kernel copies each
         job in as the host flags it), 0 copy kernel / copy engine ahead of the launch, -1 no call yet."""

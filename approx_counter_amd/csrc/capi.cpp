@@ -1313,13 +1313,6 @@ ac_status ac_error_count_samples(ac_ctx* ctx, uint32_t k, const ac_sample_job* j
     return AC_OK;
 }
 
-ac_status ac_error_count_sample(ac_ctx* ctx, uint32_t k, const uint64_t* kmers, uint32_t n_kmers,
-                                const ac_windows* dev, uint64_t* counts) {
-    if (!ctx) return fail(nullptr, AC_ERR_INVALID, "ctx is NULL");
-    if (!dev) return fail(ctx, AC_ERR_INVALID, "NULL argument");
-    const ac_sample_job job{kmers, n_kmers, *dev, counts};
-    return ac_error_count_samples(ctx, k, &job, 1);
-}
 
 ac_status ac_last_launch(const ac_ctx* ctx, uint64_t* waves, uint32_t* windows_per_wave, uint32_t* groups) {
     if (!ctx) return fail(nullptr, AC_ERR_INVALID, "ctx is NULL");
@@ -2450,12 +2443,6 @@ ac_status ac_error_count_jobs(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint3
 
 uint32_t ac_testing_stage_hooks(uint32_t flags) { return g_test_hooks.exchange(flags); }
 
-// (ABI 5's armed launch was removed in ABI 6 -- measured no faster at any configuration,
-// DESIGN.md §4c -- so nothing is ever left waiting for a next call: ac_idle only checks its argument.)
-ac_status ac_idle(ac_ctx* ctx) {
-    if (!ctx) return fail(nullptr, AC_ERR_INVALID, "ctx is NULL");
-    return AC_OK;
-}
 
 ac_status ac_error_count_jobs_submit(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint32_t n_jobs,
                                      uint32_t* d_counts, void* hip_stream) {

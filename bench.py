@@ -7,11 +7,14 @@
 A step is one pass of the stage BASELINE.md defines over one batch: both read
 ends of one run (start + end windows, approx_counter.cpp:858), each against its
 own top-`lim` candidates, from HOST buffers to HOST counts -- the sample as a
-StringSet<Dna5String> (one byte per base, what errorCount receives), packed to
-2-bit codes (N positions inline) by the library's host worker pool into pinned
-memory, pulled into HBM by the count kernel's own copier workgroups while it
-counts -- ONE fused kernel launch over both ends, issued before the packing --
-(N > 1: one RCCL all-reduce of the count vector), counts back.  That is `value`.  Default workload = BASELINE.json
+StringSet<Dna5String> (one byte per base, what errorCount receives; built once,
+outside the timed steps, in pinned memory from ac_host_alloc, `--sample pinned`),
+ONE fused kernel launch over both ends issued first in the call, the windows
+packed to 2-bit codes (N positions inline) either by the library's host pool
+(cfg2-sized calls) or by the count kernel's own copier workgroups straight from
+the pinned Dna5 bytes (calls of >= 2^16 windows, or a rank's small host share:
+DESIGN.md 4d), pulled into HBM while the other workgroups count, (N > 1: one
+RCCL all-reduce of the count vector), counts back.  That is `value`.  Default workload = BASELINE.json
 configs[1] (k=16, sn=10,000, sl=100, lim=500), on seeded synthetic reads
 (SURVEY.md §8(d)).
 

@@ -195,11 +195,6 @@ ac_status ac_exact_count(ac_ctx* ctx, uint32_t k, const ac_windows* host, float 
                          uint64_t* kmers_out, uint64_t* counts_out, uint64_t capacity, uint64_t* n_out,
                          uint64_t* n_distinct, uint64_t* had_n);
 
-/* ac_error_count over a device sample from ac_sample_upload: host k-mers in,
- * host counts out, synchronous (errorCount, approx_counter.cpp:531-601). */
-ac_status ac_error_count_sample(ac_ctx* ctx, uint32_t k, const uint64_t* kmers, uint32_t n_kmers,
-                                const ac_windows* dev, uint64_t* counts);
-
 /*
  * ac_sample_upload into upload slot `slot` (0 .. AC_MAX_JOBS-1; slot 0 is
  * ac_sample_upload's), so both read ends of a run stay on the device at once:
@@ -313,13 +308,9 @@ typedef struct ac_job {
 ac_status ac_error_count_jobs(ac_ctx* ctx, uint32_t k, const ac_job* jobs, uint32_t n_jobs);
 
 /*
- * ABI 5 added armed launches (opt-in: the next synchronous call's kernel
- * enqueued during the current one) and ac_idle to cancel them.  They measured
- * no faster at any configuration and were removed in ABI 6, so
- * no call leaves device work behind it; ac_idle is kept for callers built
- * against ABI 5 and only checks its argument (AC_ERR_INVALID for NULL).
+ * (ABI 7 removed ac_idle -- a no-op since ABI 6 removed the armed launches it cancelled -- and
+ * ac_error_count_sample, which ac_error_count_samples with one job replaces.)
  */
-ac_status ac_idle(ac_ctx* ctx);
 
 /*
  * The same stage without the way back, for callers that combine shards with

@@ -69,15 +69,6 @@ def test_comm_entry_points_without_a_context():
     assert L.ac_allreduce_counts(None, None, 0, None) == _lib.AC_ERR_INVALID
 
 
-def test_idle_without_a_context():
-    """ac_idle (kept from ABI 5; a no-op since the armed launch was removed in ABI 6) rejects a NULL
-    context, and the removed test-only arm statistics are no longer exported."""
-    L = _lib.load()
-    assert L.ac_idle(None) == _lib.AC_ERR_INVALID
-    assert b"ctx" in L.ac_last_error(None)
-    assert not hasattr(L, "ac_testing_arm_stats")
-
-
 def _has_gpu():
     try:
         import torch
@@ -140,3 +131,12 @@ def test_dna5_sample_rejects_windows_past_the_buffer():
         ac.Dna5Sample(np.zeros(10, np.uint8), np.array([0, 6], np.uint64), np.array([5, 5], np.uint32))
     with pytest.raises(ValueError):
         ac.Dna5Sample(np.zeros(10, np.uint8), np.array([0], np.uint64), np.array([5, 5], np.uint32))
+
+
+def test_removed_entry_points_are_gone():
+    """ABI 7 removed ac_idle (a no-op since ABI 6's removal of the armed launch) and
+    ac_error_count_sample (ac_error_count_samples with one job); round 4's test-only arm statistics
+    went with the armed launch (ABI sprawl)."""
+    L = _lib.load()
+    for name in ("ac_idle", "ac_error_count_sample", "ac_testing_arm_stats"):
+        assert not hasattr(L, name), name

@@ -148,6 +148,11 @@ final2)  # rocprof evidence: the bench's kernel trace, the count kernel's PMC pa
   for c in cfg3 cfg5 cfg4; do
     run bench_$c 400 python3 bench.py --config $c --steps 20 --warmup 5 --no-cpu-baseline --no-pipelined --no-exact
   done ;;
+xab3)  # count kernel: claimed slots listed by a table scan (xscan) vs the per-claim append (cur)
+  for rep in 1 2; do for v in cur xscan; do
+    run xab3_${v}_cfg4_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so python3 tools/bench_exact.py --fast --reads 1000000 --lim 500 --steps 10 --no-host
+    run xab3_${v}_cfg3_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so python3 tools/bench_exact.py --fast --reads 100000 --lim 2000 --steps 10
+  done; done ;;
 *) echo "unknown part $part" ;;
 esac
 done
