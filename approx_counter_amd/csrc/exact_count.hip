@@ -978,9 +978,6 @@ constexpr uint32_t COUNT_THREADS = AC_COUNT_THREADS;
 constexpr uint32_t COUNT_APPEND = 2 * COUNT_THREADS;
 
 constexpr uint32_t COUNT_BATCH = 8;  // keys per thread loaded together (one memory latency per batch)
-#ifndef AC_COUNT_SCAN
-#define AC_COUNT_SCAN 0
-#endif
 
 template <class K>
 __global__ __launch_bounds__(COUNT_THREADS) void part_count_kernel(ExactArgs a) {
@@ -989,9 +986,6 @@ __global__ __launch_bounds__(COUNT_THREADS) void part_count_kernel(ExactArgs a) 
     __shared__ uint32_t tc[SLOTS];
     __shared__ uint16_t occ[SLOTS];  // the slots claimed, in claim order: only they are scored and cleared
     __shared__ uint32_t n_occ;
-#if AC_COUNT_SCAN
-    __shared__ uint32_t scan_cnt[COUNT_THREADS / 64];
-#endif
     __shared__ uint32_t hist[EXACT_PHIST];  // counts 1 .. EXACT_PHIST
     __shared__ uint64_t app_k[COUNT_APPEND];
     __shared__ uint32_t app_c[COUNT_APPEND];
@@ -1067,9 +1061,7 @@ __global__ __launch_bounds__(COUNT_THREADS) void part_count_kernel(ExactArgs a) 
                             cur = atomicCAS(&tk[h], (K)0, stored);
                             if (cur == 0u) {  // claimed: list the slot for scoring and clearing
                                 cur = stored;
-#if !AC_COUNT_SCAN
                                 occ[atomicAdd(&n_occ, 1u)] = (uint16_t)h;
-#endif
                             }
                         }
                         if (cur == stored) {
@@ -1085,32 +1077,6 @@ __global__ __launch_bounds__(COUNT_THREADS) void part_count_kernel(ExactArgs a) 
         if (allt) atomicAdd(&n_allt, allt);
         if (b + gridDim.x < NB) load_batch(nxt, a.bstart[b + gridDim.x], a.bstart[b + gridDim.x + 1]);
         __syncthreads();
-#if AC_COUNT_SCAN
-        {  // (A/B builds) the claimed slots listed by scanning the table, wave by wave, instead of a
-           // same-address LDS append per claim during the inserts
-            constexpr uint32_t PER_WAVE = SLOTS / (COUNT_THREADS / 64u);
-            const uint32_t wv = t >> 6, lane = t & 63u;
-            uint32_t mine = 0;
-            for (uint32_t i = 0; i < PER_WAVE; i += 64u) mine += (uint32_t)__popcll(__ballot(tk[wv * PER_WAVE + i + lane] != 0u));
-            if (lane == 0) scan_cnt[wv] = mine;
-            __syncthreads();
-            uint32_t pos = 0, tot = 0;
-            for (uint32_t w = 0; w < COUNT_THREADS / 64u; ++w) {
-                pos += w < wv ? scan_cnt[w] : 0u;
-                tot += scan_cnt[w];
-            }
-            for (uint32_t i = 0; i < PER_WAVE; i += 64u) {
-                const uint32_t sl = wv * PER_WAVE + i + lane;
-                const uint64_t bm = __ballot(tk[sl] != 0u);
-                if (tk[sl] != 0u)
-                    occ[pos + __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u))] =
-                        (uint16_t)sl;
-                pos += (uint32_t)__popcll(bm);
-            }
-            if (t == 0) n_occ = tot;
-            __syncthreads();
-        }
-#endif
         uint32_t ones = 0;
         const uint32_t m = n_occ;
         for (uint32_t s0 = 0; s0 < m; s0 += COUNT_THREADS) {  // block-uniform trips over the claimed slots
