@@ -153,6 +153,16 @@ xab3)  # count kernel: claimed slots listed by a table scan (xscan) vs the per-c
     run xab3_${v}_cfg4_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so python3 tools/bench_exact.py --fast --reads 1000000 --lim 500 --steps 10 --no-host
     run xab3_${v}_cfg3_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so python3 tools/bench_exact.py --fast --reads 100000 --lim 2000 --steps 10
   done; done ;;
+xtime)  # count kernel split (timing-only builds): no scoring (xt1), no inserts (xt2), full (cur)
+  for rep in 1 2; do for v in cur xt1 xt2; do
+    run xtime_${v}_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so python3 tools/bench_exact.py --fast --reads 1000000 --lim 500 --steps 10 --no-host
+  done; done ;;
+rank8)  # cfg2 with one rank's share of an 8-rank node (LOCAL_WORLD_SIZE=8: a 1-participant pool): host vs device packing
+  for rep in 1 2; do
+    run rank8_host_$rep 120 env LOCAL_WORLD_SIZE=8 LOCAL_RANK=0 AC_DEVICE_PACK=0 $B --sample pinned
+    run rank8_dev_$rep 120 env LOCAL_WORLD_SIZE=8 LOCAL_RANK=0 $B --sample pinned
+  done
+  run submit1 200 python3 bench.py --step-form submit --steps 200 --warmup 10 $BQ --no-kernel-leg ;;
 *) echo "unknown part $part" ;;
 esac
 done
