@@ -1512,12 +1512,13 @@ int device_pack_mode() {
     }();
     return v;
 }
-// Auto: the kernel packs a call of at least this many windows, or any call when the host pool has at
-// most 2 participants (a rank's share of the node).  Below it the host pool, which packs a cfg2 call in
-// a few microseconds, is ahead: cfg2 stage 0.1145-0.1149 ms host-packed against 0.1262-0.1292 device-
-// packed (the image crosses PCIe as 1 B/base instead of 0.25, 2 MB per call; profiles/r06_m4/abdev_*);
-// at cfg3-cfg5 the two are within 1-3 % and the device-packed steps have no host-side tail
-// (profiles/r06_m3/stall*, abbig_*).
+// Auto: the kernel packs a call of at least this many windows.  Below it the host pool, which packs a
+// cfg2 call in a few microseconds, is ahead: cfg2 stage 0.1145-0.1149 ms host-packed against
+// 0.1262-0.1292 device-packed (the image crosses PCIe as 1 B/base instead of 0.25, 2 MB per call;
+// profiles/r06_m4/abdev_*), and still with an 8-rank node's 1-participant pool: 0.1150 / 0.1158
+// against 0.1270 / 0.1302 (profiles/r06_m10/rank8_*; round 6 first device-packed every call of a pool
+// of <= 2 participants, which cost a cfg2 rank at N = 8 those 12 us).  At cfg3-cfg5 the two are within
+// 1-3 % and the device-packed steps have no host-side tail (profiles/r06_m3/stall*, abbig_*).
 uint64_t device_pack_min_windows() {
     static const uint64_t v = (uint64_t)std::max(0, env_int("AC_DEVICE_PACK_MIN_WINDOWS", 1 << 16));
     return v;
@@ -1874,7 +1875,7 @@ ac_status stage_and_launch(ac_ctx* ctx, uint32_t k, const ac_job* jobs, JobPlan&
     uint32_t dp_bytes[AC_MAX_JOBS] = {};
     p.dp_any = false;
     const int dpm = (g_test_hooks.load(std::memory_order_relaxed) & AC_TESTING_DEVICE_PACK) ? 1 : device_pack_mode();
-    if (p.early && p.pre == 0 && (dpm == 1 || (dpm == 2 && (total_w >= device_pack_min_windows() || pool.size() <= 2))))
+    if (p.early && p.pre == 0 && (dpm == 1 || (dpm == 2 && total_w >= device_pack_min_windows())))
         for (uint32_t j = 0; j < p.n; ++j) {
             p.dp[j] = false;
             const ac_dna5_windows& w = jobs[j].sample;

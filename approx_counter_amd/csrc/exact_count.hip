@@ -978,6 +978,9 @@ constexpr uint32_t COUNT_THREADS = AC_COUNT_THREADS;
 constexpr uint32_t COUNT_APPEND = 2 * COUNT_THREADS;
 
 constexpr uint32_t COUNT_BATCH = 8;  // keys per thread loaded together (one memory latency per batch)
+#ifndef AC_COUNT_EARLY_NEXT
+#define AC_COUNT_EARLY_NEXT 0  // the next bucket's first batch requested before this bucket's inserts (A/B)
+#endif
 
 template <class K>
 __global__ __launch_bounds__(COUNT_THREADS) void part_count_kernel(ExactArgs a) {
@@ -1028,6 +1031,8 @@ __global__ __launch_bounds__(COUNT_THREADS) void part_count_kernel(ExactArgs a) 
             if (i0 == lo) {
 #pragma unroll
                 for (uint32_t r = 0; r < COUNT_BATCH; ++r) kb[r] = nxt[r];
+                if (AC_COUNT_EARLY_NEXT && b + gridDim.x < NB)
+                    load_batch(nxt, a.bstart[b + gridDim.x], a.bstart[b + gridDim.x + 1]);
             } else {
                 load_batch(kb, i0, hi);
             }
@@ -1075,7 +1080,8 @@ __global__ __launch_bounds__(COUNT_THREADS) void part_count_kernel(ExactArgs a) 
             }
         }
         if (allt) atomicAdd(&n_allt, allt);
-        if (b + gridDim.x < NB) load_batch(nxt, a.bstart[b + gridDim.x], a.bstart[b + gridDim.x + 1]);
+        if ((!AC_COUNT_EARLY_NEXT || lo == hi) && b + gridDim.x < NB)  // (an empty bucket had no first batch)
+            load_batch(nxt, a.bstart[b + gridDim.x], a.bstart[b + gridDim.x + 1]);
         __syncthreads();
         uint32_t ones = 0;
         const uint32_t m = n_occ;

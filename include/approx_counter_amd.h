@@ -264,12 +264,12 @@ typedef struct ac_dna5_windows {
  * sampleSequences, approx_counter.cpp:415-476, fills an ordinary StringSet<Dna5String>).
  * A job of ac_error_count_jobs / _submit whose windows all have one length of 1..256 bases (a read
  * end: sl or sl + 1) and whose `bases` and `offset` arrays lie inside blocks of ac_host_alloc is
- * packed on the device when the call is large (>= 2^16 windows; AC_DEVICE_PACK_MIN_WINDOWS) or the
- * host pool small (<= 2 participants, a rank's share of a node): the count kernel's copier
- * workgroups read its Dna5 bytes over PCIe and pack them into HBM themselves, so the host does no
- * per-window work for it beyond scanning the lengths (ac_stage_mode then reports 3).  Smaller calls
- * are packed by the host pool, which is faster there (AC_DEVICE_PACK=1 / 0: always / never).  The bytes readable from `bases` are those up to the end
- * of its block; a window reaching past them is an error (AC_ERR_INVALID, its counts short).
+ * packed on the device when the call is large (>= 2^16 windows; AC_DEVICE_PACK_MIN_WINDOWS): the
+ * count kernel's copier workgroups read its Dna5 bytes over PCIe and pack them into HBM themselves,
+ * so the host does no per-window work for it beyond scanning the lengths (ac_stage_mode then reports
+ * 3).  Smaller calls are packed by the host pool, which is faster there, a 1-participant pool
+ * included (AC_DEVICE_PACK=1 / 0: always / never).  The bytes readable from `bases` are those up to
+ * the end of its block; a window reaching past them is an error (AC_ERR_INVALID, its counts short).
  * Blocks are process-wide (any context, any device).  A submit's device-packed jobs are read by
  * the device until its stream work completes: do not change or free them before that.
  *   ac_host_alloc  a pinned, device-mapped block of `bytes` (AC_ERR_DEVICE without a HIP device)

@@ -106,15 +106,18 @@ def test_bench_line_reports_the_pool_that_ran():
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, AC_HOST_THREADS="3")
-    for sample, dp, path, text in (("heap", "", "early-launch", "issued first in the call"),
-                                   ("pinned", "", "early-launch", "issued first in the call"),
-                                   ("pinned", "1", "early-launch-device-pack", "the host packs nothing")):
+    # (a 1-participant pool -- an 8-rank node's share -- still host-packs cfg2 on pinned memory: the
+    # device-pack policy is by call size only)
+    for threads, sample, dp, path, text in ((3, "heap", "", "early-launch", "issued first in the call"),
+                                            (3, "pinned", "", "early-launch", "issued first in the call"),
+                                            (1, "pinned", "", "early-launch", "issued first in the call"),
+                                            (3, "pinned", "1", "early-launch-device-pack", "the host packs nothing")):
         r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "3", "--warmup", "1",
                             "--no-cpu-baseline", "--no-pipelined", "--no-kernel-leg", "--no-exact", "--sample", sample],
-                           env=dict(env, AC_DEVICE_PACK=dp), capture_output=True, text=True, timeout=300)
+                           env=dict(os.environ, AC_HOST_THREADS=str(threads), AC_DEVICE_PACK=dp),
+                           capture_output=True, text=True, timeout=300)
         assert r.returncode == 0, r.stderr[-2000:]
         line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
-        assert line["host_pool"]["participants"] == 3
+        assert line["host_pool"]["participants"] == threads
         assert line["config"]["stage_path"] == path and text in line["config"]["stage"]
         assert "armed_launch" not in line and "cgroup_cpu" in line

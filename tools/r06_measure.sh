@@ -163,6 +163,21 @@ rank8)  # cfg2 with one rank's share of an 8-rank node (LOCAL_WORLD_SIZE=8: a 1-
     run rank8_dev_$rep 120 env LOCAL_WORLD_SIZE=8 LOCAL_RANK=0 $B --sample pinned
   done
   run submit1 200 python3 bench.py --step-form submit --steps 200 --warmup 10 $BQ --no-kernel-leg ;;
+tailab)  # count kernel: launch-tail split into one-word halves (tools/variants.sh tail1/tail2/tail4) vs cur
+  for v in tail2; do
+    run tests_$v 900 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so $PYT -m gpu tests/test_gpu_parity.py tests/test_gpu_jobs.py tests/test_gpu_bench_path.py tests/test_gpu_device_pack.py
+  done
+  run kab_cfg2 900 bash tools/kernel_ab.sh "cur tail1 tail2 tail4" cfg2
+  run kab_cfg5 900 bash tools/kernel_ab.sh "cur tail2" cfg5
+  for rep in 1 2; do for v in cur tail1 tail2 tail4; do
+    run stage_${v}_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so $B
+  done; done ;;
+xearly)  # exact count: the next bucket's first batch requested before this bucket's inserts (xearly) vs cur
+  run tests_xearly 600 env APPROX_COUNTER_AMD_LIB=build/var/xearly/libapprox_counter_amd.so $PYT -m gpu tests/test_gpu_exact.py
+  for rep in 1 2; do for v in cur xearly; do
+    run xe_${v}_cfg4_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so python3 tools/bench_exact.py --fast --reads 1000000 --lim 500 --steps 10 --no-host
+    run xe_${v}_cfg3_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so python3 tools/bench_exact.py --fast --reads 100000 --lim 2000 --steps 10
+  done; done ;;
 *) echo "unknown part $part" ;;
 esac
 done
