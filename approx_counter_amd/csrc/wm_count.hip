@@ -254,12 +254,6 @@ struct BlockLds {
     uint32_t stage_r;
 };
 
-#ifndef AC_TAIL_SPLIT
-#define AC_TAIL_SPLIT 0  // the launch-tail split of two-word waves' last windows into one-word halves (count_body)
-#endif
-#ifndef AC_TAIL_WINDOWS
-#define AC_TAIL_WINDOWS 2  // windows per sub-queue split into halves (AC_TAIL_SPLIT)
-#endif
 #ifndef AC_COPY_AHEAD
 #define AC_COPY_AHEAD 32  // chunks a copier may run ahead of its segment's copied count (0: no limit; 8 / 16 / 32 measured, profiles/r03_m10/ab.log)
 #endif
@@ -1025,21 +1019,8 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
     // Per-sub-queue constants of the served sub-queue, recomputed only when a
     // steal changes it (their divisions are SALU sequences; with 1-window items
     // they ran once per window).
-    // Launch-tail split (AC_TAIL_SPLIT, two-word waves, one-window items): the last `tail_w` windows of
-    // each sub-queue are claimed as two half items each -- one lane word of the window, counted with the
-    // one-word NFA blocks -- so the launch's last work units are half as long and the SIMDs drain sooner
-    // (§4: the drain, the last window of each SIMD on 1-3 waves, is ~8 us of a cfg2 launch).  Claims
-    // c < F of a sub-queue are whole windows, F <= c < F + 2T halves; the main loop stops at a half
-    // claim (`tail_c`) and the tail loop after it counts halves.
-    constexpr bool TAIL = AC_TAIL_SPLIT && W == 2;
-    const uint32_t tail_w = (TAIL && seg_chunk == 1u) ? (uint32_t)AC_TAIL_WINDOWS : 0u;
-    auto tail_of = [&](uint32_t jj) { return min(n_in(jj), tail_w); };
-    uint32_t jc_waves = waves_in(jc), jc_items = n_in(jc) - tail_of(jc), jc_claims = jc_items + 2u * tail_of(jc);
-    uint32_t tail_c = ~0u;  // (wave-uniform) a half claim of sub-queue jc the main loop handed over
-    auto item_of = [&](uint32_t c) {
-        if (TAIL && c >= jc_items && c < jc_claims) tail_c = c;
-        return c < jc_items ? jc + c * S : n_items;
-    };
+    uint32_t jc_waves = waves_in(jc), jc_items = n_in(jc);
+    auto item_of = [&](uint32_t c) { return c < jc_items ? jc + c * S : n_items; };
     auto dequeue_issue = [&]() -> uint32_t {  // lane 0 holds the result; read with readfirstlane
         uint32_t v = 0;
         if (lane == 0) v = __hip_atomic_fetch_add(counter(jc), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1060,7 +1041,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
                 if (lane < 63u && b + lane < S) {
                     const uint32_t jj = (j + b + lane) % S;
                     const uint32_t v = __hip_atomic_load(counter(jj), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    have = waves_in(jj) + v < n_in(jj) + tail_of(jj);  // (claims: whole windows, and halves)
+                    have = waves_in(jj) + v < n_in(jj);
                 }
                 const uint64_t mk = __ballot(have);
                 if (mk) found = b + (uint32_t)__builtin_ctzll(mk);
@@ -1069,11 +1050,9 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
             const uint32_t jj = (j + found) % S;
             jc = jj;
             jc_waves = waves_in(jj);
-            jc_items = n_in(jj) - tail_of(jj);
-            jc_claims = jc_items + 2u * tail_of(jj);
+            jc_items = n_in(jj);
             const uint32_t c = jc_waves + __builtin_amdgcn_readfirstlane(dequeue_issue());
             if (c < jc_items) return item_of(c);
-            if (TAIL && c < jc_claims) return item_of(c);  // a half: n_items, and tail_c holds it
         }
     };
     uint32_t item = (j < n_items && eb_ok && !skip) ? item_of(rank) : n_items;
@@ -1197,10 +1176,6 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
 #define AC_GATED 0
 #include "wm_window_loop.inc"
 #undef AC_GATED
-    uint32_t nh[2] = {0u, 0u};  // (wave-uniform) halves counted per lane word (AC_TAIL_SPLIT)
-    if constexpr (TAIL) {
-#include "wm_tail_loop.inc"
-    }
 
     stamp(wave, 2);
     stamp_val(wave, 6, ((uint64_t)si << 32) | ((uint64_t)g << 16) | j);
@@ -1220,7 +1195,7 @@ __device__ __forceinline__ void count_body(const LaunchArgs& a, BlockLds<words_f
     // the sum change in one atomic.
 #pragma unroll
     for (int q = 0; q < Q; ++q)
-        if (P <= 2) cnt[q] = 3u * (n_counted + nh[q / P]) - cnt[q];
+        if (P <= 2) cnt[q] = 3u * n_counted - cnt[q];
 #pragma unroll
     for (int q = 0; q < Q; ++q)
         if (cnt[q]) __hip_atomic_fetch_add(&lds.cnt[q * 64 + lane], cnt[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);

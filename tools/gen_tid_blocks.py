@@ -85,9 +85,7 @@ def block(nb, with_n, eb0, skip=0, W=1, init=False):
         return f"%[{pre(w)}a{r}]"
 
     def rd(w, i):
-        # (one word: the table's LDS offset is the template parameter TOFF -- 0, or TABLE_BYTES for a
-        # two-word table's second word, which the launch tail's half items count on its own)
-        return f"ds_read_addtid_b32 {E(w, i)}" + (f" offset:{w * TABLE_BYTES}" if w else (" offset:%[toff]" if W == 1 else ""))
+        return f"ds_read_addtid_b32 {E(w, i)}" + (f" offset:{w * TABLE_BYTES}" if w else "")
 
     L = []
     for j in range(min(AHEAD, nb)):
@@ -187,14 +185,12 @@ def emit(nb, skip=0, name=None, W=1, init=False):
     init_in = "".join(f', [{v}] "v"(ini.{v[1:]})' for v in ("is0", "is1", "is2", "id1", "id2")) if init else ""
     if init:
         sig += ", const TidInit& ini"
-    toff_in = ', [toff] "n"(TOFF)' if W == 1 else ""
     operands = f"""            : {state_ops},
               {outs},
               [t] "=&s"(t), [keep] "=&s"(keep)
-            : [code] "s"(code){code2_in}, [nm] "s"(nm), [eb] "s"(eb), [P] "n"(P){init_in}{toff_in}
+            : [code] "s"(code){code2_in}, [nm] "s"(nm), [eb] "s"(eb), [P] "n"(P){init_in}
             : "memory", "scc");"""
-    tparams = "template <int P, bool EB0, int TOFF = 0>" if W == 1 else "template <int P, bool EB0>"
-    return f"""{tparams}
+    return f"""template <int P, bool EB0>
 __device__ __forceinline__ void {name or f"tid_block{nb}"}({sig}, uint32_t code{code2_arg}, uint32_t nm, uint32_t eb) {{
     uint32_t {decl};
     uint32_t t, keep;

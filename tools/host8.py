@@ -1,11 +1,12 @@
 #!/usr/bin/env python3
 """The host-side work of one rank's step at 8 ranks, eight processes at once.
 
-    python tools/host8.py [--sample pinned|heap] [--ranks 8] [--calls 200]
+    python tools/host8.py [--sample pinned|heap] [--ranks 8] [--calls 200] [--config cfg4|cfg2]
 
 Each process takes LOCAL_RANK r of LOCAL_WORLD_SIZE 8 (so the library plans its host pool as an
 8-rank node would: disjoint CPUs, the rank's share of the cgroup quota) and submits its 1/8 shard
-of cfg4 (2 x 125k windows, strong scaling, bench.build_workload) with ac_error_count_jobs_submit
+of cfg4 (2 x 125k windows, strong scaling, bench.build_workload; or with --config cfg2 its own
+2 x 10k windows, weak scaling as bench.py's cfg2 line) with ac_error_count_jobs_submit
 -- bench.py's N > 1 step -- timing the submit call alone: everything the host does before the
 count kernel owns the step (layout, and with a heap sample the host pool's packing; with a
 pinned sample the kernel packs).  The device work then completes untimed (one GPU
@@ -26,16 +27,16 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def worker(rank, ranks, sample, calls, warmup, go_file):
+def worker(rank, ranks, sample, calls, warmup, go_file, config="cfg4"):
     import torch
 
     import approx_counter_amd as ac
     import bench
     from approx_counter_amd.counter import host_pool_cpus
 
-    sys.argv = ["bench.py", "--config", "cfg4"]
+    sys.argv = ["bench.py", "--config", config]
     args = bench.parse()
-    args.scaling = "strong"
+    args.scaling = "strong" if config == "cfg4" else "weak"
     wl, _ = bench.build_workload(args, rank, ranks)
     ends = ("start", "end")
     smp = [ac.Dna5Sample.from_windows(wl[e]["windows"]) for e in ends]
@@ -74,9 +75,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--worker", type=int, default=-1)
     ap.add_argument("--go", default="")
+    ap.add_argument("--config", choices=("cfg4", "cfg2"), default="cfg4")
     a = ap.parse_args()
     if a.worker >= 0:
-        worker(a.worker, a.ranks, a.sample, a.calls, a.warmup, a.go)
+        worker(a.worker, a.ranks, a.sample, a.calls, a.warmup, a.go, a.config)
         return
     go = f"/tmp/host8_go_{os.getpid()}"
     procs = []
@@ -84,6 +86,7 @@ def main():
         env = dict(os.environ, LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(a.ranks))
         procs.append(subprocess.Popen([sys.executable, __file__, "--worker", str(r), "--ranks", str(a.ranks),
                                        "--sample", a.sample, "--calls", str(a.calls), "--warmup", str(a.warmup),
+                                       "--config", a.config,
                                        "--go", go], env=env, stdout=subprocess.PIPE, text=True))
     t0 = time.time()
     while not all(os.path.exists(go + f".ready{r}") for r in range(a.ranks)):
@@ -103,7 +106,7 @@ def main():
             os.remove(f)
     if len(rows) != a.ranks:
         raise SystemExit(f"only {len(rows)} of {a.ranks} ranks reported")
-    print(json.dumps({"ranks": a.ranks, "sample": a.sample, "modes": sorted({r["mode"] for r in rows}),
+    print(json.dumps({"ranks": a.ranks, "sample": a.sample, "config": a.config, "modes": sorted({r["mode"] for r in rows}),
                       "participants": sorted({r["participants"] for r in rows}),
                       "max_over_ranks_p50_us": max(r["p50_us"] for r in rows),
                       "max_over_ranks_p90_us": max(r["p90_us"] for r in rows),

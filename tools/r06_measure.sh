@@ -164,20 +164,26 @@ rank8)  # cfg2 with one rank's share of an 8-rank node (LOCAL_WORLD_SIZE=8: a 1-
   done
   run submit1 200 python3 bench.py --step-form submit --steps 200 --warmup 10 $BQ --no-kernel-leg ;;
 tailab)  # count kernel: launch-tail split into one-word halves (tools/variants.sh tail1/tail2/tail4) vs cur
-  for v in tail2; do
-    run tests_$v 900 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so $PYT -m gpu tests/test_gpu_parity.py tests/test_gpu_jobs.py tests/test_gpu_bench_path.py tests/test_gpu_device_pack.py
-  done
-  run kab_cfg2 900 bash tools/kernel_ab.sh "cur tail1 tail2 tail4" cfg2
-  run kab_cfg5 900 bash tools/kernel_ab.sh "cur tail2" cfg5
-  for rep in 1 2; do for v in cur tail1 tail2 tail4; do
+  # (and the packed count hand-off, hpack: AC_HAND_PACK=1)
+  run tests_tail2 900 env APPROX_COUNTER_AMD_LIB=build/var/tail2/libapprox_counter_amd.so $PYT -m gpu tests/test_gpu_parity.py tests/test_gpu_jobs.py tests/test_gpu_bench_path.py tests/test_gpu_device_pack.py
+  run tests_hpack 900 env APPROX_COUNTER_AMD_LIB=build/var/hpack/libapprox_counter_amd.so $PYT -m gpu tests/test_gpu_parity.py tests/test_gpu_jobs.py tests/test_gpu_bench_path.py
+  run kab_cfg2 900 bash tools/kernel_ab.sh "cur tail1 tail2 tail4 hpack" cfg2
+  run kab_cfg5 900 bash tools/kernel_ab.sh "cur tail2 hpack" cfg5
+  for rep in 1 2; do for v in cur tail1 tail2 tail4 hpack; do
     run stage_${v}_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so $B
   done; done ;;
-xearly)  # exact count: the next bucket's first batch requested before this bucket's inserts (xearly) vs cur
-  run tests_xearly 600 env APPROX_COUNTER_AMD_LIB=build/var/xearly/libapprox_counter_amd.so $PYT -m gpu tests/test_gpu_exact.py
-  for rep in 1 2; do for v in cur xearly; do
+xearly)  # exact count: the next bucket's first batch requested before this bucket's inserts (xearly), buckets of
+         # ~4k keys (xb4k: AC_BUCKET_KEYS=4096), both (xeb4k), vs cur
+  run tests_xeb4k 600 env APPROX_COUNTER_AMD_LIB=build/var/xeb4k/libapprox_counter_amd.so $PYT -m gpu tests/test_gpu_exact.py
+  for rep in 1 2; do for v in cur xearly xb4k xeb4k; do
     run xe_${v}_cfg4_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so python3 tools/bench_exact.py --fast --reads 1000000 --lim 500 --steps 10 --no-host
     run xe_${v}_cfg3_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so python3 tools/bench_exact.py --fast --reads 100000 --lim 2000 --steps 10
   done; done ;;
+host8c2)  # 8 processes at once, each one rank's host-side work per cfg2 step: host-packed (auto) vs device-packed
+  for rep in 1 2; do
+    run host8c2_auto_$rep 300 python3 tools/host8.py --config cfg2 --sample pinned
+    run host8c2_dev_$rep 300 env AC_DEVICE_PACK=1 python3 tools/host8.py --config cfg2 --sample pinned
+  done ;;
 *) echo "unknown part $part" ;;
 esac
 done
