@@ -93,11 +93,9 @@ def load():
     L.ac_error_count.argtypes = [vp, ctypes.c_uint32, p64, ctypes.c_uint32,
                                  ctypes.POINTER(ACWindows), p64]
     L.ac_error_count.restype = ctypes.c_int
-    for fn in (L.ac_error_count_device, L.ac_error_count_device_accumulate):
-        fn.argtypes = [vp, ctypes.c_uint32, ctypes.POINTER(ACSegment), ctypes.c_uint32, vp]
-        fn.restype = ctypes.c_int
-    L.ac_error_count_device_equal.argtypes = [vp, ctypes.c_uint32, ctypes.POINTER(ACSegment), p32, ctypes.c_uint32, vp]
-    L.ac_error_count_device_equal.restype = ctypes.c_int
+    L.ac_error_count_device.argtypes = [vp, ctypes.c_uint32, ctypes.POINTER(ACSegment), ctypes.c_uint32, p32,
+                                        ctypes.c_uint32, vp]
+    L.ac_error_count_device.restype = ctypes.c_int
     L.ac_image_bases.argtypes = [p32, ctypes.c_uint32]
     L.ac_image_bases.restype = ctypes.c_uint64
     L.ac_pack_windows.argtypes = [p8, p64, p32, ctypes.c_uint32, p32, p32, p64, p32,

@@ -58,7 +58,7 @@ class PackedSample:
 
     def equal_window_len(self):
         """The common window length when every window has it and window w starts at base
-        w * ceil32(length) (the layout ac_error_count_device_equal reads without descriptors),
+        w * ceil32(length) (the layout ac_error_count_device reads without descriptors when given window_len),
         else None."""
         n = self.n_windows
         if n == 0:
@@ -385,19 +385,16 @@ class ApproxCounter:
         """ac_error_count_device over DeviceSegment objects, or an array from
         segment_array (asynchronous).  window_len (one per segment): the samples'
         windows all have that length and sit back to back at ceil32 strides
-        (ac_error_count_device_equal; start / length are not read)."""
+        (start / length are not read).  accumulate: AC_DEVICE_ACCUMULATE."""
         arr = segments if isinstance(segments, ctypes.Array) else self.segment_array(segments)
+        wp = None
         if window_len is not None:
-            if accumulate:
-                raise ValueError("window_len: no accumulate form")
             wl = np.ascontiguousarray(window_len, dtype=np.uint32)
             if wl.size != len(arr):
                 raise ValueError("one window_len per segment")
-            st = self._L.ac_error_count_device_equal(self._h, int(k), arr, _ptr(wl, ctypes.c_uint32), len(arr),
-                                                     ctypes.c_void_p(stream or 0))
-        else:
-            fn = self._L.ac_error_count_device_accumulate if accumulate else self._L.ac_error_count_device
-            st = fn(self._h, int(k), arr, len(arr), ctypes.c_void_p(stream or 0))
+            wp = _ptr(wl, ctypes.c_uint32)
+        st = self._L.ac_error_count_device(self._h, int(k), arr, len(arr), wp, 1 if accumulate else 0,
+                                           ctypes.c_void_p(stream or 0))
         if st:
             check(st, self._h)
 

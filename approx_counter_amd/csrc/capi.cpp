@@ -735,31 +735,19 @@ void ac_destroy(ac_ctx* ctx) {
 }
 
 ac_status ac_error_count_device(ac_ctx* ctx, uint32_t k, const ac_segment* segments, uint32_t n_segments,
-                                void* hip_stream) {
+                                const uint32_t* window_len, uint32_t flags, void* hip_stream) {
     if (!ctx) return fail(nullptr, AC_ERR_INVALID, "ctx is NULL");
-    AC_HIP(ctx, hipSetDevice(ctx->device));
-    return launch(ctx, k, segments, n_segments, (hipStream_t)hip_stream, true);
-}
-
-ac_status ac_error_count_device_accumulate(ac_ctx* ctx, uint32_t k, const ac_segment* segments,
-                                           uint32_t n_segments, void* hip_stream) {
-    if (!ctx) return fail(nullptr, AC_ERR_INVALID, "ctx is NULL");
-    AC_HIP(ctx, hipSetDevice(ctx->device));
-    return launch(ctx, k, segments, n_segments, (hipStream_t)hip_stream, false);
-}
-
-ac_status ac_error_count_device_equal(ac_ctx* ctx, uint32_t k, const ac_segment* segments,
-                                      const uint32_t* window_len, uint32_t n_segments, void* hip_stream) {
-    if (!ctx) return fail(nullptr, AC_ERR_INVALID, "ctx is NULL");
-    if (n_segments && !window_len) return fail(ctx, AC_ERR_INVALID, "window_len is NULL");
+    if (flags & ~AC_DEVICE_ACCUMULATE) return fail(ctx, AC_ERR_INVALID, "unknown flags");
     if (n_segments > AC_MAX_SEGS) return fail(ctx, AC_ERR_INVALID, "too many segments in one launch (max 4)");
     uint32_t ul[AC_MAX_SEGS];
-    for (uint32_t i = 0; i < n_segments; ++i) {
-        if (window_len[i] == AC_NO_ULEN) return fail(ctx, AC_ERR_INVALID, "window_len out of range");
-        ul[i] = window_len[i];
-    }
+    if (window_len)
+        for (uint32_t i = 0; i < n_segments; ++i) {
+            if (window_len[i] == AC_NO_ULEN) return fail(ctx, AC_ERR_INVALID, "window_len out of range");
+            ul[i] = window_len[i];
+        }
     AC_HIP(ctx, hipSetDevice(ctx->device));
-    return launch(ctx, k, segments, n_segments, (hipStream_t)hip_stream, true, nullptr, 0, 0, nullptr, ul);
+    return launch(ctx, k, segments, n_segments, (hipStream_t)hip_stream, !(flags & AC_DEVICE_ACCUMULATE), nullptr, 0,
+                  0, nullptr, window_len ? ul : nullptr);
 }
 
 }  // extern "C"

@@ -431,7 +431,7 @@ def main():
         segs = [ac.DeviceSegment.upload(wl[e]["kmers"], packed[i], device=dev) for i, e in enumerate(ends)]
         arr = ac.ApproxCounter.segment_array(segs)
         # equal windows (every start window sl bases, every end window sl + 1): the launch form the
-        # stage's kernel uses (window places computed, not loaded; ac_error_count_device_equal)
+        # stage's kernel uses (window places computed, not loaded; ac_error_count_device with window_len)
         eq = [p.equal_window_len() for p in packed]
         wlen = eq if all(x is not None for x in eq) else None
         kc = ac.ApproxCounter(local)
@@ -642,7 +642,7 @@ def main():
                                          "ratio": pmc["sq_insts_valu_per_launch"] / model}
             out["kernel_ms"] = kern_ms
             out["kernel_kmer_bp_per_s"] = units_rank / (kern_ms * 1e-3)
-            out["kernel_leg"] = ("ac_error_count_device_equal (equal windows: places computed, as in the stage)"
+            out["kernel_leg"] = ("ac_error_count_device with window_len (equal windows: places computed, as in the stage)"
                                  if wlen else "ac_error_count_device (window descriptors loaded)")
             out["launch"] = geo
             out["roofline"] = roof

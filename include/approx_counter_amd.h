@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define AC_ABI_VERSION 7
+#define AC_ABI_VERSION 8
 
 typedef int32_t ac_status;
 #define AC_OK 0
@@ -133,26 +133,20 @@ ac_status ac_error_count(ac_ctx* ctx, uint32_t k, const uint64_t* kmers, uint32_
  * on the stream first and summed.  The context's scratch (work queues, group
  * sums) is stream-ordered: do not run two launches of one context on
  * different streams at the same time.
+ *   window_len  NULL: every window's start / length is read from the segment's sample.  Otherwise
+ *               one length per segment for samples whose windows all have it -- the reference's
+ *               own sample: every start window holds sl bases and every end window sl + 1
+ *               (sampleSequences, approx_counter.cpp:415-476): segment i's window w starts at base
+ *               w * ceil32(window_len[i]), n_windows * ceil32(window_len[i]) <= n_bases, and
+ *               sample.start / .length are not read (may be NULL) -- the kernel computes each
+ *               window's place instead of loading its descriptor, as the host-buffer stage does.
+ *   flags       AC_DEVICE_ACCUMULATE: add into `counts` without zeroing them first (window shards
+ *               combined on one device); 0: store them.
+ * (ABI 8 folded ac_error_count_device_accumulate and ac_error_count_device_equal into this call.)
  */
-ac_status ac_error_count_device(ac_ctx* ctx, uint32_t k, const ac_segment* segments,
-                                uint32_t n_segments, void* hip_stream);
-
-/* Same as ac_error_count_device but accumulates into `counts` without
- * zeroing them first (used to combine window shards on one device). */
-ac_status ac_error_count_device_accumulate(ac_ctx* ctx, uint32_t k, const ac_segment* segments,
-                                           uint32_t n_segments, void* hip_stream);
-
-/*
- * ac_error_count_device for samples whose windows all have one length -- the
- * reference's own sample: every start window holds sl bases and every end
- * window sl + 1 (sampleSequences, approx_counter.cpp:415-476).  Segment i's
- * window w starts at base w * ceil32(window_len[i]) and holds window_len[i]
- * bases, n_windows * ceil32(window_len[i]) <= n_bases; segments[i].sample.start
- * and .length are not read (may be NULL): the kernel computes each window's
- * place instead of loading its descriptor, as the host-buffer stage does.
- */
-ac_status ac_error_count_device_equal(ac_ctx* ctx, uint32_t k, const ac_segment* segments,
-                                      const uint32_t* window_len, uint32_t n_segments, void* hip_stream);
+#define AC_DEVICE_ACCUMULATE 1u
+ac_status ac_error_count_device(ac_ctx* ctx, uint32_t k, const ac_segment* segments, uint32_t n_segments,
+                                const uint32_t* window_len, uint32_t flags, void* hip_stream);
 
 /*
  * Device copy of a packed sample, owned by the context (valid until the next

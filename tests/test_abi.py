@@ -27,7 +27,7 @@ def test_library_targets_gfx950():
 
 
 def test_abi_version():
-    assert _lib.load().ac_abi_version() == 7  # ABI 7: ac_host_alloc / ac_host_free (device packing)
+    assert _lib.load().ac_abi_version() == 8  # ABI 8: one ac_error_count_device (window_len, flags)
 
 
 def test_pack_layout():
@@ -136,7 +136,16 @@ def test_dna5_sample_rejects_windows_past_the_buffer():
 def test_removed_entry_points_are_gone():
     """ABI 7 removed ac_idle (a no-op since ABI 6's removal of the armed launch) and
     ac_error_count_sample (ac_error_count_samples with one job); round 4's test-only arm statistics
-    went with the armed launch (ABI sprawl)."""
+    went with the armed launch; ABI 8 folded ac_error_count_device_accumulate / _equal into
+    ac_error_count_device's window_len and flags (ABI sprawl)."""
     L = _lib.load()
-    for name in ("ac_idle", "ac_error_count_sample", "ac_testing_arm_stats"):
+    for name in ("ac_idle", "ac_error_count_sample", "ac_testing_arm_stats", "ac_error_count_device_accumulate",
+                 "ac_error_count_device_equal"):
         assert not hasattr(L, name), name
+
+
+def test_device_count_null_ctx_is_rejected():
+    """ac_error_count_device (ABI 8 signature) checks its arguments before it touches the device."""
+    L = _lib.load()
+    st = L.ac_error_count_device(None, 16, None, 0, None, 0, None)
+    assert st == _lib.AC_ERR_INVALID and b"ctx" in L.ac_last_error(None)

@@ -433,8 +433,8 @@ def test_window_count_limit_rejected(counter):
     arr = ac.ApproxCounter.segment_array([seg])
     wl = np.zeros(1, np.uint32)  # length-0 windows: every one at base 0, inside any image
     L = counter._L
-    st = L.ac_error_count_device_equal(counter.handle, 16, arr, wl.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
-                                       1, None)
+    st = L.ac_error_count_device(counter.handle, 16, arr, 1, wl.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), 0,
+                                 None)
     assert st == 1 and "2^32 / 3" in L.ac_last_error(counter.handle).decode()
     seg.n_windows = len(wins)  # the context still counts afterwards
     counter.count_device(16, [seg])
