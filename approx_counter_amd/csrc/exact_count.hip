@@ -978,9 +978,6 @@ constexpr uint32_t COUNT_THREADS = AC_COUNT_THREADS;
 constexpr uint32_t COUNT_APPEND = 2 * COUNT_THREADS;
 
 constexpr uint32_t COUNT_BATCH = 8;  // keys per thread loaded together (one memory latency per batch)
-#ifndef AC_COUNT_EARLY_NEXT
-#define AC_COUNT_EARLY_NEXT 0  // the next bucket's first batch requested before this bucket's inserts (A/B)
-#endif
 
 template <class K>
 __global__ __launch_bounds__(COUNT_THREADS) void part_count_kernel(ExactArgs a) {
@@ -1021,35 +1018,16 @@ __global__ __launch_bounds__(COUNT_THREADS) void part_count_kernel(ExactArgs a) 
         }
     };
     if (blockIdx.x < NB) load_batch(nxt, a.bstart[blockIdx.x], a.bstart[blockIdx.x + 1]);
-#if AC_COUNT_EARLY_NEXT
-    // (A/B) The workgroup's bucket bounds in flight a bucket ahead, through vector loads (lane 0: the
-    // start, lane 1: the end; a scalar load would be waited for by the inserts' LDS waits), and the next
-    // bucket's first batch requested as soon as this one's is taken, so both latencies hide behind the
-    // inserts instead of standing between buckets.
-    auto bounds = [&](uint32_t bb) __attribute__((always_inline)) {
-        return bb < NB ? a.bstart[bb + (t & 1u)] : 0u;
-    };
-    uint32_t bv_cur = bounds(blockIdx.x), bv_nx = bounds(blockIdx.x + gridDim.x);
-#endif
     for (uint32_t b = blockIdx.x; b < NB; b += gridDim.x) {
         for (uint32_t i = t; i < EXACT_PHIST; i += COUNT_THREADS) hist[i] = 0;
         __syncthreads();
-#if AC_COUNT_EARLY_NEXT
-        const uint32_t lo = __builtin_amdgcn_readlane(bv_cur, 0), hi = __builtin_amdgcn_readlane(bv_cur, 1);
-        const uint32_t bv_nn = bounds(b + 2u * gridDim.x);
-#else
         const uint32_t lo = a.bstart[b], hi = a.bstart[b + 1];
-#endif
         uint32_t allt = 0;
         for (uint32_t i0 = lo; i0 < hi; i0 += COUNT_THREADS * COUNT_BATCH) {  // block-uniform batches
             K kb[COUNT_BATCH];
             if (i0 == lo) {
 #pragma unroll
                 for (uint32_t r = 0; r < COUNT_BATCH; ++r) kb[r] = nxt[r];
-#if AC_COUNT_EARLY_NEXT
-                if (b + gridDim.x < NB)
-                    load_batch(nxt, __builtin_amdgcn_readlane(bv_nx, 0), __builtin_amdgcn_readlane(bv_nx, 1));
-#endif
             } else {
                 load_batch(kb, i0, hi);
             }
@@ -1097,14 +1075,7 @@ __global__ __launch_bounds__(COUNT_THREADS) void part_count_kernel(ExactArgs a) 
             }
         }
         if (allt) atomicAdd(&n_allt, allt);
-#if AC_COUNT_EARLY_NEXT
-        if (lo == hi && b + gridDim.x < NB)  // (an empty bucket had no first batch)
-            load_batch(nxt, __builtin_amdgcn_readlane(bv_nx, 0), __builtin_amdgcn_readlane(bv_nx, 1));
-        bv_cur = bv_nx;
-        bv_nx = bv_nn;
-#else
         if (b + gridDim.x < NB) load_batch(nxt, a.bstart[b + gridDim.x], a.bstart[b + gridDim.x + 1]);
-#endif
         __syncthreads();
         uint32_t ones = 0;
         const uint32_t m = n_occ;
