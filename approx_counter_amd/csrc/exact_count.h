@@ -95,7 +95,10 @@ struct ExactArgs {
 
 #define EXACT_SCAN_SLAB 128   // level-1 histogram rows (chunks) per workgroup of the column scan
 #define EXACT_MAX_SUPER 1024  // level-1 super-buckets (at most): 2^16 buckets of <= 64 sub-buckets each
-#define EXACT_MAX_SUB 64     // buckets per super-bucket (at most)
+#ifndef AC_SUB_LOG2
+#define AC_SUB_LOG2 6  // log2 buckets per super-bucket at 2^16 buckets (A/B builds: 7)
+#endif
+#define EXACT_MAX_SUB (1 << AC_SUB_LOG2)  // buckets per super-bucket (at most)
 #define EXACT_BUCKET_SLOTS 4096  // LDS counting table of the per-bucket kernel (32 KB of keys + counts)
 
 hipError_t launch_exact_insert(const ExactArgs& a, hipStream_t stream);

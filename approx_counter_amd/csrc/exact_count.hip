@@ -898,7 +898,7 @@ __global__ __launch_bounds__(EXACT_THREADS) void part_hist2_kernel(ExactArgs a) 
     for (uint32_t j = t; j < SUB; j += EXACT_THREADS) a.h2[(uint64_t)blockIdx.x * SUB + j] = h[j];
 }
 
-// Level 2, per super-bucket (one wave each, lane j = sub-bucket j): bucket
+// Level 2, per super-bucket (one wave each, lane j = sub-buckets j, j + 64, ..): bucket
 // starts bstart[s * SUB + j] (and bstart[NB]), h2 -> each chunk's cursor.
 template <class K>
 __global__ __launch_bounds__(EXACT_THREADS) void part_scan2_kernel(ExactArgs a) {
@@ -909,23 +909,28 @@ __global__ __launch_bounds__(EXACT_THREADS) void part_scan2_kernel(ExactArgs a) 
     const uint32_t s = blockIdx.x * (EXACT_THREADS / 64) + (threadIdx.x >> 6);
     if (s >= S) return;
     const uint32_t c0 = cbeg[s], c1 = cbeg[s + 1];
-    uint32_t tot = 0;
-    if (lane < SUB)
-        for (uint32_t c = c0; c < c1; ++c) tot += a.h2[(uint64_t)c * SUB + lane];
-    uint32_t incl = tot;
+    uint32_t carry = sstart[s];
+    for (uint32_t j0 = 0; j0 < SUB; j0 += 64u) {
+        const uint32_t j = j0 + lane;
+        uint32_t tot = 0;
+        if (j < SUB)
+            for (uint32_t c = c0; c < c1; ++c) tot += a.h2[(uint64_t)c * SUB + j];
+        uint32_t incl = tot;
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(incl, d, 64);
-        if ((int)lane >= d) incl += y;
-    }
-    uint32_t run = sstart[s] + incl - tot;
-    if (lane < SUB) {
-        a.bstart[s * SUB + lane] = run;
-        for (uint32_t c = c0; c < c1; ++c) {
-            uint32_t* p = &a.h2[(uint64_t)c * SUB + lane];
-            const uint32_t x = *p;
-            *p = run;
-            run += x;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(incl, d, 64);
+            if ((int)lane >= d) incl += y;
+        }
+        uint32_t run = carry + incl - tot;
+        carry += __shfl(incl, 63, 64);
+        if (j < SUB) {
+            a.bstart[s * SUB + j] = run;
+            for (uint32_t c = c0; c < c1; ++c) {
+                uint32_t* p = &a.h2[(uint64_t)c * SUB + j];
+                const uint32_t x = *p;
+                *p = run;
+                run += x;
+            }
         }
     }
     if (s == S - 1u && lane == 0) a.bstart[S * SUB] = sstart[S];

@@ -184,6 +184,15 @@ host8c2)  # 8 processes at once, each one rank's host-side work per cfg2 step: h
     run host8c2_auto_$rep 300 python3 tools/host8.py --config cfg2 --sample pinned
     run host8c2_dev_$rep 300 env AC_DEVICE_PACK=1 python3 tools/host8.py --config cfg2 --sample pinned
   done ;;
+sub7)  # exact count: 512 super-buckets of 128 buckets (sub7: AC_SUB_LOG2=7; longer level-1 runs) vs 1024 x 64 (cur)
+  run tests_sub7 600 env APPROX_COUNTER_AMD_LIB=build/var/sub7/libapprox_counter_amd.so $PYT -m gpu tests/test_gpu_exact.py
+  for rep in 1 2; do for v in cur sub7; do
+    run xs_${v}_cfg4_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so python3 tools/bench_exact.py --fast --reads 1000000 --lim 500 --steps 10 --no-host
+    run xs_${v}_cfg3_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so python3 tools/bench_exact.py --fast --reads 100000 --lim 2000 --steps 10
+    run xs_${v}_cfg5_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so python3 tools/bench_exact.py --fast --reads 100000 --sl 150 --k 22 --lim 1000 --steps 10
+  done; done
+  export TMPDIR=/tmp
+  run xs_trace_sub7 200 env APPROX_COUNTER_AMD_LIB=build/var/sub7/libapprox_counter_amd.so rocprofv3 --kernel-trace --stats -d "$OUT/xs_trace_sub7" -o run -- python3 tools/bench_exact.py --fast --reads 1000000 --lim 500 --steps 5 --no-host ;;
 *) echo "unknown part $part" ;;
 esac
 done
