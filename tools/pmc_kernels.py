@@ -27,7 +27,7 @@ def main():
             for kname, cname, did, v in con.execute(
                     "select kernel_name, counter_name, dispatch_id, value from counters_collection"):
                 if a.match in kname:
-                    m = re.search(r"(\w+)\(", kname)
+                    m = re.search(r"::(\w+)(?:<[^(]*>)?\(", kname) or re.search(r"(\w+)\(", kname)
                     key = (m.group(1) if m else kname, cname)
                     per[key][(db, did)] = per[key].get((db, did), 0.0) + float(v)
             con.close()

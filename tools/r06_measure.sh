@@ -193,6 +193,8 @@ sub7)  # exact count: 512 super-buckets of 128 buckets (sub7: AC_SUB_LOG2=7; lon
   done; done
   export TMPDIR=/tmp
   run xs_trace_sub7 200 env APPROX_COUNTER_AMD_LIB=build/var/sub7/libapprox_counter_amd.so rocprofv3 --kernel-trace --stats -d "$OUT/xs_trace_sub7" -o run -- python3 tools/bench_exact.py --fast --reads 1000000 --lim 500 --steps 5 --no-host ;;
+xsq)  # exact count at cfg4: SQ wave-cycle split and LDS counters per kernel (where the count kernel's time goes)
+  run xsq 600 bash tools/pmc_exact_sq.sh "$OUT/xsq" ;;
 *) echo "unknown part $part" ;;
 esac
 done
