@@ -898,6 +898,7 @@ __global__ __launch_bounds__(EXACT_THREADS) void part_hist2_kernel(ExactArgs a) 
     for (uint32_t j = t; j < SUB; j += EXACT_THREADS) a.h2[(uint64_t)blockIdx.x * SUB + j] = h[j];
 }
 
+constexpr uint32_t SCAN2_BATCH = 8;  // level-2 scan: chunk rows loaded per batch
 // Level 2, per super-bucket (one wave each, lane j = sub-buckets j, j + 64, ..): bucket
 // starts bstart[s * SUB + j] (and bstart[NB]), h2 -> each chunk's cursor.
 template <class K>
@@ -914,7 +915,13 @@ __global__ __launch_bounds__(EXACT_THREADS) void part_scan2_kernel(ExactArgs a) 
         const uint32_t j = j0 + lane;
         uint32_t tot = 0;
         if (j < SUB)
-            for (uint32_t c = c0; c < c1; ++c) tot += a.h2[(uint64_t)c * SUB + j];
+            for (uint32_t c = c0; c < c1; c += SCAN2_BATCH) {
+                uint32_t x[SCAN2_BATCH];
+#pragma unroll
+                for (uint32_t u = 0; u < SCAN2_BATCH; ++u) x[u] = c + u < c1 ? a.h2[(uint64_t)(c + u) * SUB + j] : 0u;
+#pragma unroll
+                for (uint32_t u = 0; u < SCAN2_BATCH; ++u) tot += x[u];
+            }
         uint32_t incl = tot;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
@@ -925,11 +932,17 @@ __global__ __launch_bounds__(EXACT_THREADS) void part_scan2_kernel(ExactArgs a) 
         carry += __shfl(incl, 63, 64);
         if (j < SUB) {
             a.bstart[s * SUB + j] = run;
-            for (uint32_t c = c0; c < c1; ++c) {
-                uint32_t* p = &a.h2[(uint64_t)c * SUB + j];
-                const uint32_t x = *p;
-                *p = run;
-                run += x;
+            // (a batch of loads before its stores: one at a time, each load waited for the store before it)
+            for (uint32_t c = c0; c < c1; c += SCAN2_BATCH) {
+                uint32_t x[SCAN2_BATCH];
+#pragma unroll
+                for (uint32_t u = 0; u < SCAN2_BATCH; ++u) x[u] = c + u < c1 ? a.h2[(uint64_t)(c + u) * SUB + j] : 0u;
+#pragma unroll
+                for (uint32_t u = 0; u < SCAN2_BATCH; ++u)
+                    if (c + u < c1) {
+                        a.h2[(uint64_t)(c + u) * SUB + j] = run;
+                        run += x[u];
+                    }
             }
         }
     }
