@@ -195,6 +195,15 @@ sub7)  # exact count: 512 super-buckets of 128 buckets (sub7: AC_SUB_LOG2=7; lon
   run xs_trace_sub7 200 env APPROX_COUNTER_AMD_LIB=build/var/sub7/libapprox_counter_amd.so rocprofv3 --kernel-trace --stats -d "$OUT/xs_trace_sub7" -o run -- python3 tools/bench_exact.py --fast --reads 1000000 --lim 500 --steps 5 --no-host ;;
 xsq)  # exact count at cfg4: SQ wave-cycle split and LDS counters per kernel (where the count kernel's time goes)
   run xsq 600 bash tools/pmc_exact_sq.sh "$OUT/xsq" ;;
+phab)  # exact count: phased inserts (ph8 / ph4: AC_COUNT_PHASED, batch 8 / 4) vs sub7, all with 512 x 128 buckets
+  for v in ph4 ph8; do
+    run tests_$v 600 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so $PYT -m gpu tests/test_gpu_exact.py
+  done
+  for rep in 1 2; do for v in sub7 ph8 ph4; do
+    run xp_${v}_cfg4_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so python3 tools/bench_exact.py --fast --reads 1000000 --lim 500 --steps 10 --no-host
+    run xp_${v}_cfg3_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so python3 tools/bench_exact.py --fast --reads 100000 --lim 2000 --steps 10
+    run xp_${v}_cfg5_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so python3 tools/bench_exact.py --fast --reads 100000 --sl 150 --k 22 --lim 1000 --steps 10
+  done; done ;;
 *) echo "unknown part $part" ;;
 esac
 done
