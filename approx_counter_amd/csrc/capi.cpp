@@ -1088,7 +1088,7 @@ ac_status ac_exact_count_device(ac_ctx* ctx, uint32_t k, const ac_windows* dev, 
         while (nb_log2 < 16 && (key_cap >> nb_log2) > 2048) ++nb_log2;
         a.nb_log2 = nb_log2;
         a.key_cap = key_cap;
-        // super-buckets of <= 64 buckets, at least 128 of them when there are that many buckets
+        // super-buckets of <= 2^AC_SUB_LOG2 (128) buckets, at least 128 of them when there are that many buckets
         a.s_log2 = std::max(std::min(nb_log2, 7u), nb_log2 > AC_SUB_LOG2 ? nb_log2 - (uint32_t)AC_SUB_LOG2 : 0u);
         const uint32_t chunk = acamd::exact_part_chunk(k);
         a.n_chunks = (uint32_t)((key_cap + chunk - 1) / chunk);

@@ -94,9 +94,12 @@ struct ExactArgs {
 #define EXACT_PHIST 32  // per-bucket partial histogram bins (counts 1..32; larger counts go straight to hist)
 
 #define EXACT_SCAN_SLAB 128   // level-1 histogram rows (chunks) per workgroup of the column scan
-#define EXACT_MAX_SUPER 1024  // level-1 super-buckets (at most): 2^16 buckets of <= 64 sub-buckets each
+#define EXACT_MAX_SUPER 1024  // level-1 super-buckets (at most)
 #ifndef AC_SUB_LOG2
-#define AC_SUB_LOG2 6  // log2 buckets per super-bucket at 2^16 buckets (A/B builds: 7)
+// log2 buckets per super-bucket at 2^16 buckets: 512 super-buckets of 128 (round 6; 1024 of 64 before):
+// the level-1 scatter writes runs of ~16 keys per chunk and super-bucket instead of ~8 (partial
+// lines), cfg4 2.14-2.17 ms against 2.26-2.27 (profiles/r06_m14, r06_m15)
+#define AC_SUB_LOG2 7
 #endif
 #define EXACT_MAX_SUB (1 << AC_SUB_LOG2)  // buckets per super-bucket (at most)
 #define EXACT_BUCKET_SLOTS 4096  // LDS counting table of the per-bucket kernel (32 KB of keys + counts)

@@ -995,16 +995,10 @@ __device__ __forceinline__ float key_complexity(uint64_t key, uint32_t k) { retu
 constexpr uint32_t COUNT_THREADS = AC_COUNT_THREADS;
 constexpr uint32_t COUNT_APPEND = 2 * COUNT_THREADS;
 
-#ifndef AC_COUNT_BATCH
-#define AC_COUNT_BATCH 8
-#endif
-constexpr uint32_t COUNT_BATCH = AC_COUNT_BATCH;  // keys per thread loaded together (one memory latency per batch)
-#ifndef AC_COUNT_PHASED
-#define AC_COUNT_PHASED 0  // (A/B) inserts in phases over the batch's keys
-#endif
+constexpr uint32_t COUNT_BATCH = 8;  // keys per thread loaded together (one memory latency per batch)
 
 template <class K>
-__global__ __launch_bounds__(COUNT_THREADS, AC_COUNT_PHASED ? (sizeof(K) == 4 ? 6 : 4) : 1) void part_count_kernel(ExactArgs a) {
+__global__ __launch_bounds__(COUNT_THREADS) void part_count_kernel(ExactArgs a) {
     constexpr uint32_t SLOTS = EXACT_BUCKET_SLOTS;
     __shared__ K tk[SLOTS];  // key + 1; 0 = empty
     __shared__ uint32_t tc[SLOTS];
@@ -1055,98 +1049,6 @@ __global__ __launch_bounds__(COUNT_THREADS, AC_COUNT_PHASED ? (sizeof(K) == 4 ? 
             } else {
                 load_batch(kb, i0, hi);
             }
-#if AC_COUNT_PHASED
-            // Phased inserts: the batch's keys go through each step together -- every first-slot read
-            // issued before any is used, then every add / CAS, then every claimed slot's listing --
-            // so a thread waits for one LDS round trip per step instead of one per key and step.
-            uint32_t ha[COUNT_BATCH];  // a key's first slot (bits 0-15) and its add (16-31)
-            K curs[COUNT_BATCH];
-            uint32_t gom = 0;  // bit r: key r still to insert
-#pragma unroll
-            for (uint32_t r = 0; r < COUNT_BATCH; ++r) {
-                const uint32_t i = i0 + r * COUNT_THREADS + t;
-                const bool have = i < hi;
-                const K key = kb[r], stored = (K)(key + 1u);
-                // lanes holding the wave's first key: one add of their number
-                const uint32_t lo32 = __builtin_amdgcn_readfirstlane((uint32_t)key);
-                K k0 = (K)lo32;
-                if constexpr (sizeof(K) == 8)
-                    k0 |= (K)__builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)key >> 32)) << 32;
-                const uint64_t same = __ballot(have && key == k0);
-                uint32_t add = 1u;
-                bool go = have;
-                if (have && key == k0) {
-                    go = __lane_id() == (uint32_t)__builtin_ctzll(same);
-                    add = (uint32_t)__popcll(same);
-                }
-                if (go && !stored) {
-                    allt += add;
-                    go = false;
-                }
-                ha[r] = (part_hash(key) & (SLOTS - 1u)) | (add << 16);
-                if (go) gom |= 1u << r;
-            }
-#pragma unroll
-            for (uint32_t r = 0; r < COUNT_BATCH; ++r) curs[r] = (gom >> r) & 1u ? tk[ha[r] & 0xffffu] : (K)0;
-            uint32_t casm = 0;
-#pragma unroll
-            for (uint32_t r = 0; r < COUNT_BATCH; ++r) {
-                if (!((gom >> r) & 1u)) continue;
-                const K stored = (K)(kb[r] + 1u);
-                if (curs[r] == stored) {
-                    atomicAdd(&tc[ha[r] & 0xffffu], ha[r] >> 16);
-                    gom &= ~(1u << r);
-                } else if (curs[r] == (K)0) {
-                    curs[r] = atomicCAS(&tk[ha[r] & 0xffffu], (K)0, stored);
-                    casm |= 1u << r;
-                }
-            }
-            uint32_t clm = 0;
-#pragma unroll
-            for (uint32_t r = 0; r < COUNT_BATCH; ++r) {
-                if (!((casm >> r) & 1u)) continue;
-                if (curs[r] == (K)0) {  // claimed
-                    clm |= 1u << r;
-                    gom &= ~(1u << r);
-                } else if (curs[r] == (K)(kb[r] + 1u)) {  // the same key, claimed by another lane first
-                    atomicAdd(&tc[ha[r] & 0xffffu], ha[r] >> 16);
-                    gom &= ~(1u << r);
-                }
-            }
-#pragma unroll
-            for (uint32_t r = 0; r < COUNT_BATCH; ++r)  // (a claimed key's curs: its place in the list)
-                if ((clm >> r) & 1u) curs[r] = (K)atomicAdd(&n_occ, 1u);
-#pragma unroll
-            for (uint32_t r = 0; r < COUNT_BATCH; ++r)
-                if ((clm >> r) & 1u) {  // listed for scoring and clearing, then counted
-                    occ[(uint32_t)curs[r]] = (uint16_t)ha[r];
-                    atomicAdd(&tc[ha[r] & 0xffffu], ha[r] >> 16);
-                }
-            // the rest found another key in their first slot: probe on from the next one
-            while (gom) {
-                const uint32_t r = (uint32_t)__builtin_ctz(gom);
-                gom &= gom - 1u;
-                const K stored = (K)(kb[r] + 1u);
-                uint32_t h = ((ha[r] & 0xffffu) + 1u) & (SLOTS - 1u);
-                uint32_t probe = 1;
-                for (; probe < COUNT_PROBES; ++probe) {
-                    K cur = tk[h];
-                    if (cur == 0u) {
-                        cur = atomicCAS(&tk[h], (K)0, stored);
-                        if (cur == 0u) {
-                            cur = stored;
-                            occ[atomicAdd(&n_occ, 1u)] = (uint16_t)h;
-                        }
-                    }
-                    if (cur == stored) {
-                        atomicAdd(&tc[h], ha[r] >> 16);
-                        break;
-                    }
-                    h = (h + 1u) & (SLOTS - 1u);
-                }
-                if (probe == COUNT_PROBES) atomicOr(a.overflow, 1u);
-            }
-#else
 #pragma unroll
             for (uint32_t r = 0; r < COUNT_BATCH; ++r) {
                 const uint32_t i = i0 + r * COUNT_THREADS + t;
@@ -1189,7 +1091,6 @@ __global__ __launch_bounds__(COUNT_THREADS, AC_COUNT_PHASED ? (sizeof(K) == 4 ? 
                     if (probe == COUNT_PROBES) atomicOr(a.overflow, 1u);  // the host falls back to the hash table
                 }
             }
-#endif
         }
         if (allt) atomicAdd(&n_allt, allt);
         if (b + gridDim.x < NB) load_batch(nxt, a.bstart[b + gridDim.x], a.bstart[b + gridDim.x + 1]);
