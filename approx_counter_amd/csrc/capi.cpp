@@ -1084,8 +1084,11 @@ ac_status ac_exact_count_device(ac_ctx* ctx, uint32_t k, const ac_windows* dev, 
     std::vector<char> h_small(small_bytes);
     if (partitioned) {
         // buckets: about 1,024-2,048 keys each (the LDS table holds 4,096)
+#ifndef AC_BUCKET_KEYS
+#define AC_BUCKET_KEYS 2048  // (A/B builds: the bucket size target)
+#endif
         uint32_t nb_log2 = 6;
-        while (nb_log2 < 16 && (key_cap >> nb_log2) > 2048) ++nb_log2;
+        while (nb_log2 < 16 && (key_cap >> nb_log2) > AC_BUCKET_KEYS) ++nb_log2;
         a.nb_log2 = nb_log2;
         a.key_cap = key_cap;
         // super-buckets of <= 2^AC_SUB_LOG2 (128) buckets, at least 128 of them when there are that many buckets

@@ -462,7 +462,10 @@ __global__ __launch_bounds__(EXACT_THREADS) void exact_gather_list_kernel(ExactA
 // read end fit); larger samples take the hash table.
 
 constexpr uint32_t MAX_NB_LOG2 = 16;
-constexpr uint32_t COUNT_PROBES = 64;
+#ifndef AC_COUNT_PROBES
+#define AC_COUNT_PROBES 64
+#endif
+constexpr uint32_t COUNT_PROBES = AC_COUNT_PROBES;
 
 // Keys per histogram / scatter chunk: the scatter stages a chunk in LDS (32 KB).
 template <class K>

@@ -204,6 +204,17 @@ phab)  # exact count: phased inserts (ph8 / ph4: AC_COUNT_PHASED, batch 8 / 4) v
     run xp_${v}_cfg3_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so python3 tools/bench_exact.py --fast --reads 100000 --lim 2000 --steps 10
     run xp_${v}_cfg5_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so python3 tools/bench_exact.py --fast --reads 100000 --sl 150 --k 22 --lim 1000 --steps 10
   done; done ;;
+bkab)  # exact count: 256 super-buckets of 256 (sub8), buckets of ~4k keys with a 1,024-probe reach (b4k), vs cur
+  for v in sub8 b4k; do
+    run tests_$v 600 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so $PYT -m gpu tests/test_gpu_exact.py
+  done
+  for rep in 1 2; do for v in cur sub8 b4k; do
+    run xb_${v}_cfg4_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so python3 tools/bench_exact.py --fast --reads 1000000 --lim 500 --steps 10 --no-host
+    run xb_${v}_cfg3_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so python3 tools/bench_exact.py --fast --reads 100000 --lim 2000 --steps 10
+    run xb_${v}_cfg5_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so python3 tools/bench_exact.py --fast --reads 100000 --sl 150 --k 22 --lim 1000 --steps 10
+  done; done
+  export TMPDIR=/tmp
+  run xb_trace_b4k 200 env APPROX_COUNTER_AMD_LIB=build/var/b4k/libapprox_counter_amd.so rocprofv3 --kernel-trace --stats -d "$OUT/xb_trace_b4k" -o run -- python3 tools/bench_exact.py --fast --reads 1000000 --lim 500 --steps 5 --no-host ;;
 *) echo "unknown part $part" ;;
 esac
 done
