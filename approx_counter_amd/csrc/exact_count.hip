@@ -185,7 +185,8 @@ __global__ __launch_bounds__(EXACT_THREADS) void exact_insert_kernel(ExactArgs a
 
 // getComplexity (approx_counter.cpp:247-267): dimer counts (16 bins, 8 bits
 // each, packed in two registers: no scratch-indexed array), their sum of
-// v*(v-1), then one float division exactly as the reference.
+// v*(v-1) (0 * (0 - 1) wraps to 0 in the reference: a zero count adds 0), then one float division
+// exactly as the reference.
 __device__ __forceinline__ float complexity(uint64_t kmer, uint32_t k) {
     uint64_t lo = 0, hi = 0;  // bins 0..7 / 8..15
     for (uint32_t i = 0; i + 1 < k; ++i) {
@@ -195,29 +196,33 @@ __device__ __forceinline__ float complexity(uint64_t kmer, uint32_t k) {
         else hi += one;
         kmer >>= 2;
     }
-    uint32_t sum = 0;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const uint32_t a = (uint32_t)(lo >> (8 * i)) & 0xffu, b = (uint32_t)(hi >> (8 * i)) & 0xffu;
-        sum += a * (a - 1u) + b * (b - 1u);  // 0 * (0 - 1) wraps to 0, as in the reference
-    }
+    // sum v * (v - 1) = sum v^2 - (k - 1): four v_dot4_u32_u8 over the byte counts (complexity16)
+    uint32_t sq = __builtin_amdgcn_udot4((uint32_t)lo, (uint32_t)lo, 0u, false);
+    sq = __builtin_amdgcn_udot4((uint32_t)(lo >> 32), (uint32_t)(lo >> 32), sq, false);
+    sq = __builtin_amdgcn_udot4((uint32_t)hi, (uint32_t)hi, sq, false);
+    sq = __builtin_amdgcn_udot4((uint32_t)(hi >> 32), (uint32_t)(hi >> 32), sq, false);
+    const uint32_t sum = sq - (k >= 1u ? k - 1u : 0u);
     return (float)sum / (float)(2 * ((int)k - 2));
 }
 
 // The same score for k <= 16: at most 15 dimers, so each of the 16 dimer
 // counts fits a 4-bit field of one 64-bit register (one shift + add per dimer).
+// The sum of v * (v - 1) over the 16 counts is sum v^2 - sum v, and sum v = k - 1 (the dimers):
+// the nibbles spread to bytes, sum v^2 is four v_dot4_u32_u8 (was 16 extract / multiply / add
+// steps; the score runs once per distinct k-mer in the count kernel).  Counts v = 0 add 0 either way,
+// as 0 * (0 - 1) does in the reference.
 __device__ __forceinline__ float complexity16(uint32_t kmer, uint32_t k) {
     uint64_t c = 0;
-    for (uint32_t i = 0; i + 1 < k; ++i) {
-        c += 1ull << (4u * (kmer & 15u));
-        kmer >>= 2;
-    }
-    uint32_t sum = 0;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const uint32_t v = (uint32_t)(c >> (4 * i)) & 15u;
-        sum += v * (v - 1u);  // 0 * (0 - 1) wraps to 0, as in the reference
+    for (uint32_t i = 0; i < 15u; ++i) {
+        if (i + 1u < k) c += 1ull << (4u * ((kmer >> (2u * i)) & 15u));
     }
+    const uint64_t lo = c & 0x0F0F0F0F0F0F0F0Full, hi = (c >> 4) & 0x0F0F0F0F0F0F0F0Full;
+    uint32_t sq = __builtin_amdgcn_udot4((uint32_t)lo, (uint32_t)lo, 0u, false);
+    sq = __builtin_amdgcn_udot4((uint32_t)(lo >> 32), (uint32_t)(lo >> 32), sq, false);
+    sq = __builtin_amdgcn_udot4((uint32_t)hi, (uint32_t)hi, sq, false);
+    sq = __builtin_amdgcn_udot4((uint32_t)(hi >> 32), (uint32_t)(hi >> 32), sq, false);
+    const uint32_t sum = sq - (k >= 1u ? k - 1u : 0u);
     return (float)sum / (float)(2 * ((int)k - 2));
 }
 

@@ -215,6 +215,14 @@ bkab)  # exact count: 256 super-buckets of 256 (sub8), buckets of ~4k keys with 
   done; done
   export TMPDIR=/tmp
   run xb_trace_b4k 200 env APPROX_COUNTER_AMD_LIB=build/var/b4k/libapprox_counter_amd.so rocprofv3 --kernel-trace --stats -d "$OUT/xb_trace_b4k" -o run -- python3 tools/bench_exact.py --fast --reads 1000000 --lim 500 --steps 5 --no-host ;;
+dustab)  # exact count: DUST sums by v_dot4_u32_u8 (dust) vs the extract / multiply loop (cur)
+  run tests_dust 600 env APPROX_COUNTER_AMD_LIB=build/var/dust/libapprox_counter_amd.so $PYT -m gpu tests/test_gpu_exact.py
+  for rep in 1 2; do for v in cur dust; do
+    run xd_${v}_cfg4_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so python3 tools/bench_exact.py --fast --reads 1000000 --lim 500 --steps 10 --no-host
+    run xd_${v}_cfg3_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so python3 tools/bench_exact.py --fast --reads 100000 --lim 2000 --steps 10
+    run xd_${v}_cfg5_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so python3 tools/bench_exact.py --fast --reads 100000 --sl 150 --k 22 --lim 1000 --steps 10
+  done; done
+  run xsq_dust 600 bash tools/pmc_exact_sq.sh "$OUT/xsq_dust" build/var/dust/libapprox_counter_amd.so ;;
 *) echo "unknown part $part" ;;
 esac
 done
