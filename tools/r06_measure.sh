@@ -223,6 +223,12 @@ dustab)  # exact count: DUST sums by v_dot4_u32_u8 (dust) vs the extract / multi
     run xd_${v}_cfg5_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so python3 tools/bench_exact.py --fast --reads 100000 --sl 150 --k 22 --lim 1000 --steps 10
   done; done
   run xsq_dust 600 bash tools/pmc_exact_sq.sh "$OUT/xsq_dust" build/var/dust/libapprox_counter_amd.so ;;
+xkt)  # keys kernel: static per-workgroup ranges with a non-returning count add (timing-only xkt) vs cur, kernel traces
+  export TMPDIR=/tmp
+  for rep in 1 2; do for v in cur xkt; do
+    run xkt_${v}_$rep 200 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so rocprofv3 --kernel-trace --stats -d "$OUT/xkt_${v}_$rep" -o run -- python3 tools/bench_exact.py --fast --reads 1000000 --lim 500 --steps 5 --no-host
+    python3 tools/prof_summary.py "$OUT/xkt_${v}_$rep" | grep part_keys | tee -a "$OUT/summary.log"
+  done; done ;;
 *) echo "unknown part $part" ;;
 esac
 done
