@@ -98,8 +98,9 @@ def test_fused_segments_one_launch(counter):
 
 @pytest.mark.parametrize("k,lens", [(16, (100, 101)), (22, (151, 151)), (9, (300, 37))])
 def test_device_equal_windows(counter, k, lens):
-    """ac_error_count_device_equal: windows back to back at ceil32 strides, places computed
-    instead of loaded (start / length not read) -- both ends fused, bit-exact."""
+    """ac_error_count_device with window_len: windows back to back at ceil32 strides, places
+    computed instead of loaded (start / length not read) -- both ends fused, bit-exact; with
+    AC_DEVICE_ACCUMULATE too (ABI 8: the equal and accumulate forms combine)."""
     import torch
 
     parts = []
@@ -112,8 +113,14 @@ def test_device_equal_windows(counter, k, lens):
     counter.count_device(k, segs, window_len=list(lens))
     torch.cuda.synchronize()
     counter.check()
-    for (km, w), seg in zip(parts, segs):
-        assert np.array_equal(seg.counts_numpy(), oracle.count_myers(k, km, w))
+    exp = [oracle.count_myers(k, km, w) for km, w in parts]
+    for e, seg in zip(exp, segs):
+        assert np.array_equal(seg.counts_numpy(), e)
+    counter.count_device(k, segs, window_len=list(lens), accumulate=True)
+    torch.cuda.synchronize()
+    counter.check()
+    for e, seg in zip(exp, segs):
+        assert np.array_equal(seg.counts_numpy(), 2 * e)
     # windows that would reach past n_bases are refused on the host
     with pytest.raises(ac.ApproxCounterError):
         counter.count_device(k, segs[:1], window_len=[lens[0] + 64])
