@@ -213,6 +213,10 @@ def main():
         AHEAD, WAIT_PAIR = 3, False
         NE = AHEAD + 3
         OUT = os.path.join(ROOT, "build", "wm_tid_blocks_v6.inc")
+    if "--ahead" in sys.argv:  # A/B: N reads ahead (build/var only)
+        AHEAD = int(sys.argv[sys.argv.index("--ahead") + 1])
+        NE = AHEAD + 3
+        OUT = os.path.join(ROOT, "build", f"wm_tid_blocks_a{AHEAD}.inc")
     parts = [
         "// GENERATED by tools/gen_tid_blocks.py -- do not edit.  Inline-asm blocks of the\n"
         "// table-driven count loop (wm_count.hip, DESIGN.md §4).\n"

@@ -229,6 +229,14 @@ xkt)  # keys kernel: static per-workgroup ranges with a non-returning count add 
     run xkt_${v}_$rep 200 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so rocprofv3 --kernel-trace --stats -d "$OUT/xkt_${v}_$rep" -o run -- python3 tools/bench_exact.py --fast --reads 1000000 --lim 500 --steps 5 --no-host
     python3 tools/prof_summary.py "$OUT/xkt_${v}_$rep" | grep part_keys | tee -a "$OUT/summary.log"
   done; done ;;
+aheadab)  # count kernel: ~Eq LDS reads 5 / 6 bases ahead (a5 / a6, tools/gen_tid_blocks.py --ahead) vs 4 (cur)
+  run tests_a6 900 env APPROX_COUNTER_AMD_LIB=build/var/a6/libapprox_counter_amd.so $PYT -m gpu tests/test_gpu_parity.py
+  run kab_cfg2 900 bash tools/kernel_ab.sh "cur a5 a6" cfg2
+  run kab_cfg5 900 bash tools/kernel_ab.sh "cur a5 a6" cfg5
+  run kab_cfg3 900 bash tools/kernel_ab.sh "cur a5 a6" cfg3
+  for rep in 1 2; do for v in cur a5 a6; do
+    run stage_${v}_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so $B
+  done; done ;;
 *) echo "unknown part $part" ;;
 esac
 done
