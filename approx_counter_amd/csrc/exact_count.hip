@@ -211,12 +211,14 @@ __device__ __forceinline__ float complexity(uint64_t kmer, uint32_t k) {
 // the nibbles spread to bytes, sum v^2 is four v_dot4_u32_u8 (was 16 extract / multiply / add
 // steps; the score runs once per distinct k-mer in the count kernel).  Counts v = 0 add 0 either way,
 // as 0 * (0 - 1) does in the reference.
+// All 15 dimer places are counted unconditionally (one v_bfe + one v_lshl_add_u64 each; a guard on k
+// made every step a pair of selects): below k = 16 the places k - 1 .. 14 read the zero bases above the
+// k-mer -- one (top base, A) dimer and 15 - k (A, A) dimers, taken off again (no nibble exceeds 15).
 __device__ __forceinline__ float complexity16(uint32_t kmer, uint32_t k) {
     uint64_t c = 0;
 #pragma unroll
-    for (uint32_t i = 0; i < 15u; ++i) {
-        if (i + 1u < k) c += 1ull << (4u * ((kmer >> (2u * i)) & 15u));
-    }
+    for (uint32_t i = 0; i < 15u; ++i) c += 1ull << (4u * ((kmer >> (2u * i)) & 15u));
+    if (k < 16u) c -= (1ull << (4u * ((kmer >> (2u * (k - 1u))) & 15u))) + (uint64_t)(15u - k);
     const uint64_t lo = c & 0x0F0F0F0F0F0F0F0Full, hi = (c >> 4) & 0x0F0F0F0F0F0F0F0Full;
     uint32_t sq = __builtin_amdgcn_udot4((uint32_t)lo, (uint32_t)lo, 0u, false);
     sq = __builtin_amdgcn_udot4((uint32_t)(lo >> 32), (uint32_t)(lo >> 32), sq, false);

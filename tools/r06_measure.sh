@@ -237,6 +237,12 @@ aheadab)  # count kernel: ~Eq LDS reads 5 / 6 bases ahead (a5 / a6, tools/gen_ti
   for rep in 1 2; do for v in cur a5 a6; do
     run stage_${v}_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so $B
   done; done ;;
+dust2ab)  # exact count: DUST with all 15 dimer places counted unconditionally (dust2) vs guarded (dust)
+  run tests_dust2 600 env APPROX_COUNTER_AMD_LIB=build/var/dust2/libapprox_counter_amd.so $PYT -m gpu tests/test_gpu_exact.py
+  for rep in 1 2; do for v in dust dust2; do
+    run xd2_${v}_cfg4_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so python3 tools/bench_exact.py --fast --reads 1000000 --lim 500 --steps 10 --no-host
+    run xd2_${v}_cfg3_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so python3 tools/bench_exact.py --fast --reads 100000 --lim 2000 --steps 10
+  done; done ;;
 *) echo "unknown part $part" ;;
 esac
 done
