@@ -183,20 +183,29 @@ __global__ __launch_bounds__(EXACT_THREADS) void exact_insert_kernel(ExactArgs a
     if (t == 0 && n_had) atomicAdd(a.had_n, (unsigned long long)n_had);
 }
 
-// getComplexity (approx_counter.cpp:247-267): dimer counts (16 bins, 8 bits
-// each, packed in two registers: no scratch-indexed array), their sum of
-// v*(v-1) (0 * (0 - 1) wraps to 0 in the reference: a zero count adds 0), then one float division
-// exactly as the reference.
+// getComplexity (approx_counter.cpp:247-267) for k <= 32: the dimer counts, their sum of v * (v - 1)
+// (0 * (0 - 1) wraps to 0 in the reference: a zero count adds 0), then one float division exactly as
+// the reference.  Counts of up to 31 dimers need more than a nibble, so places 0-14 and 15-29 are
+// counted in two nibble histograms (one v_lshl_add_u64 each, as complexity16), spread to bytes and
+// added, place 30 added to its byte; below k = 32 the places past the k-mer read zero bases -- one
+// (top base, A) dimer and 31 - k (A, A) dimers -- and are subtracted; then sum v^2 - (k - 1) by four
+// v_dot4_u32_u8.
 __device__ __forceinline__ float complexity(uint64_t kmer, uint32_t k) {
-    uint64_t lo = 0, hi = 0;  // bins 0..7 / 8..15
-    for (uint32_t i = 0; i + 1 < k; ++i) {
-        const uint32_t d = (uint32_t)(kmer & 15u);
-        const uint64_t one = 1ull << (8u * (d & 7u));
-        if (d < 8u) lo += one;
-        else hi += one;
-        kmer >>= 2;
+    uint64_t h1 = 0, h2 = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 15u; ++i) {
+        h1 += 1ull << (4u * ((uint32_t)(kmer >> (2u * i)) & 15u));
+        h2 += 1ull << (4u * ((uint32_t)(kmer >> (2u * (i + 15u))) & 15u));
     }
-    // sum v * (v - 1) = sum v^2 - (k - 1): four v_dot4_u32_u8 over the byte counts (complexity16)
+    const uint64_t m = 0x0F0F0F0F0F0F0F0Full;
+    uint64_t lo = (h1 & m) + (h2 & m), hi = ((h1 >> 4) & m) + ((h2 >> 4) & m);  // bytes: even / odd dimers
+    const uint32_t d30 = (uint32_t)(kmer >> 60) & 15u;  // place 30: bases 30 and 31
+    (d30 & 1u ? hi : lo) += 1ull << (8u * (d30 >> 1));
+    if (k < 32u) {
+        const uint32_t top = (uint32_t)(kmer >> (2u * (k - 1u))) & 15u;  // (top base, A): 0-3
+        (top & 1u ? hi : lo) -= 1ull << (8u * (top >> 1));
+        lo -= (uint64_t)(31u - k);  // (A, A): dimer 0, byte 0 of the even bytes
+    }
     uint32_t sq = __builtin_amdgcn_udot4((uint32_t)lo, (uint32_t)lo, 0u, false);
     sq = __builtin_amdgcn_udot4((uint32_t)(lo >> 32), (uint32_t)(lo >> 32), sq, false);
     sq = __builtin_amdgcn_udot4((uint32_t)hi, (uint32_t)hi, sq, false);

@@ -243,6 +243,12 @@ dust2ab)  # exact count: DUST with all 15 dimer places counted unconditionally (
     run xd2_${v}_cfg4_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so python3 tools/bench_exact.py --fast --reads 1000000 --lim 500 --steps 10 --no-host
     run xd2_${v}_cfg3_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so python3 tools/bench_exact.py --fast --reads 100000 --lim 2000 --steps 10
   done; done ;;
+dust3ab)  # exact count, k > 16: DUST by two nibble histograms + dot products (dust3) vs the guarded byte loop (dust2)
+  run tests_dust3 600 env APPROX_COUNTER_AMD_LIB=build/var/dust3/libapprox_counter_amd.so $PYT -m gpu tests/test_gpu_exact.py tests/test_gpu_cli.py
+  for rep in 1 2; do for v in dust2 dust3; do
+    run xd3_${v}_cfg5_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so python3 tools/bench_exact.py --fast --reads 100000 --sl 150 --k 22 --lim 1000 --steps 10
+    run xd3_${v}_cfg4_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so python3 tools/bench_exact.py --fast --reads 1000000 --lim 500 --steps 10 --no-host
+  done; done ;;
 *) echo "unknown part $part" ;;
 esac
 done
