@@ -75,6 +75,8 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-host", action="store_true")
+    ap.add_argument("--forbidden", type=int, default=0,
+                    help="pass N random k-mers as the forbidden set (timing of the forbidden filter; use with --no-host)")
     ap.add_argument("--fast", action="store_true",
                     help="vectorised equal-length windows (tools/synth.make_windows_fast) instead of make_reads: "
                          "for the 10^6-window (cfg4) sample")
@@ -102,10 +104,13 @@ def main():
         ac.counter.check(L.ac_sample_upload(c.handle, ctypes.byref(hw), ctypes.byref(dw)), c.handle)
         km, ct = np.zeros(a.lim, np.uint64), np.zeros(a.lim, np.uint64)
         fb = np.zeros(1, np.uint64)
+        if a.forbidden:
+            rng = np.random.default_rng(7)
+            fb = rng.integers(0, 1 << min(63, 2 * a.k), size=a.forbidden, dtype=np.uint64)
         n_out, n_dist, had_n = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
 
         def once():
-            st = L.ac_exact_count_device(c.handle, a.k, ctypes.byref(dw), thr, _ptr(fb, ctypes.c_uint64), 0, a.lim,
+            st = L.ac_exact_count_device(c.handle, a.k, ctypes.byref(dw), thr, _ptr(fb, ctypes.c_uint64), a.forbidden, a.lim,
                                          0, _ptr(km, ctypes.c_uint64), _ptr(ct, ctypes.c_uint64), a.lim,
                                          ctypes.byref(n_out), ctypes.byref(n_dist), ctypes.byref(had_n))
             ac.counter.check(st, c.handle)

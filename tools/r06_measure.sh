@@ -249,6 +249,13 @@ dust3ab)  # exact count, k > 16: DUST by two nibble histograms + dot products (d
     run xd3_${v}_cfg5_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so python3 tools/bench_exact.py --fast --reads 100000 --sl 150 --k 22 --lim 1000 --steps 10
     run xd3_${v}_cfg4_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so python3 tools/bench_exact.py --fast --reads 1000000 --lim 500 --steps 10 --no-host
   done; done ;;
+fbfab)  # exact count with a forbidden set: LDS filter before the binary search (fbf) vs the search for every slot (dust3)
+  run tests_fbf 600 env APPROX_COUNTER_AMD_LIB=build/var/fbf/libapprox_counter_amd.so $PYT -m gpu tests/test_gpu_exact.py tests/test_gpu_cli.py
+  for rep in 1 2; do for v in dust3 fbf; do
+    for nf in 0 1000; do
+      run xf_${v}_cfg4_f${nf}_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so python3 tools/bench_exact.py --fast --reads 1000000 --lim 500 --steps 10 --no-host --forbidden $nf
+    done
+  done; done ;;
 *) echo "unknown part $part" ;;
 esac
 done
