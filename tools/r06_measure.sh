@@ -256,6 +256,10 @@ fbfab)  # exact count with a forbidden set: LDS filter before the binary search 
       run xf_${v}_cfg4_f${nf}_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so python3 tools/bench_exact.py --fast --reads 1000000 --lim 500 --steps 10 --no-host --forbidden $nf
     done
   done; done ;;
+xhost)  # exact count's host side: HIP API + kernel + copy trace of cfg3 / cfg4 calls (where the non-kernel time goes)
+  export TMPDIR=/tmp
+  run xhost_cfg3 200 rocprofv3 --hip-trace --kernel-trace --memory-copy-trace -d "$OUT/xhost_cfg3" -o run -- python3 tools/bench_exact.py --fast --reads 100000 --lim 2000 --steps 5 --warmup 2 --no-host
+  run xhost_cfg4 200 rocprofv3 --hip-trace --kernel-trace --memory-copy-trace -d "$OUT/xhost_cfg4" -o run -- python3 tools/bench_exact.py --fast --reads 1000000 --lim 500 --steps 5 --warmup 2 --no-host ;;
 *) echo "unknown part $part" ;;
 esac
 done
