@@ -237,14 +237,6 @@ __device__ __forceinline__ float complexity16(uint32_t kmer, uint32_t k) {
     return (float)sum / (float)(2 * ((int)k - 2));
 }
 
-// A 4,096-bit filter of the forbidden set in LDS (the count kernel): a key whose bit is clear is not
-// forbidden, and only a key whose bit is set pays is_forbidden's binary search through global memory
-// (log2 n dependent loads per claimed slot otherwise).
-constexpr uint32_t FB_FILTER_WORDS = 128;
-__device__ __forceinline__ uint32_t fb_filter_bit(uint64_t key) {
-    return ((uint32_t)key ^ (uint32_t)(key >> 32)) * 0x9E3779B1u >> 20;
-}
-
 __device__ __forceinline__ bool is_forbidden(const ExactArgs& a, uint64_t key) {
     uint32_t lo = 0, hi = a.n_forbidden;
     while (lo < hi) {
@@ -1037,7 +1029,6 @@ __global__ __launch_bounds__(COUNT_THREADS) void part_count_kernel(ExactArgs a) 
     __shared__ uint32_t app_n;
     __shared__ unsigned long long app_b;
     __shared__ uint32_t n_allt;
-    __shared__ uint32_t fbits[FB_FILTER_WORDS];
     const K* parts = (const K*)a.parts;
     const uint32_t t = threadIdx.x;
     const uint32_t NB = 1u << a.nb_log2;
@@ -1050,12 +1041,7 @@ __global__ __launch_bounds__(COUNT_THREADS) void part_count_kernel(ExactArgs a) 
         app_n = 0;
         n_occ = 0;
     }
-    for (uint32_t i = t; i < FB_FILTER_WORDS; i += COUNT_THREADS) fbits[i] = 0;
-    __syncthreads();
-    for (uint32_t i = t; i < a.n_forbidden; i += COUNT_THREADS) {
-        const uint32_t h = fb_filter_bit(a.forbidden[i]);
-        atomicOr(&fbits[h >> 5], 1u << (h & 31u));
-    }
+
     BlockAppender app{a.list_keys, a.list_cnts, a.n_list, a.list_cap, app_k, app_c, &app_n, &app_b};
     // Persistent: workgroup g counts buckets g, g + grid, ...; between buckets
     // only the claimed slots are cleared.  The first batch of keys of the next
@@ -1142,9 +1128,7 @@ __global__ __launch_bounds__(COUNT_THREADS) void part_count_kernel(ExactArgs a) 
                 tk[s] = 0;  // cleared for the next bucket
                 tc[s] = 0;
                 if (key_complexity(kk, a.k) >= a.lc_threshold) c = 0;  // haveLowComplexity (214-234)
-                else if (a.n_forbidden && ((fbits[fb_filter_bit(key) >> 5] >> (fb_filter_bit(key) & 31u)) & 1u) &&
-                         is_forbidden(a, key))
-                    c = 0;  // isForbiddenKmer (330-332)
+                else if (is_forbidden(a, key)) c = 0;                  // isForbiddenKmer (330-332)
             }
             if (!a.emit_only && c) {
                 if (c == 1u) ++ones;
