@@ -63,9 +63,10 @@ struct ac_ctx {
     uint32_t s_ulen[4] = {AC_NO_ULEN, AC_NO_ULEN, AC_NO_ULEN, AC_NO_ULEN};
     bool s_no_n[4] = {false, false, false, false};
     uint64_t s_windows[4] = {0, 0, 0, 0}, s_bases[4] = {0, 0, 0, 0};
-    // (+ the partitioned path's keys, parts, tmp, h1/h2/stot, bstart, phist: e_buf[6..11])
-    void* e_buf[12] = {};
-    size_t e_cap[12] = {};
+    // (+ the partitioned path's keys, parts, tmp, h1/h2/stot, bstart, phist: e_buf[6..11]; the forbidden
+    // set by bucket and its bucket starts: e_buf[12..13])
+    void* e_buf[14] = {};
+    size_t e_cap[14] = {};
     // Count-kernel scratch, one set per stream a launch may run on at the same
     // time as another: the parts of a synchronous jobs call (0 .. MAX_PARTS-1),
     // the parts of a submit (MAX_PARTS ..), so a synchronous call never shares
@@ -1046,6 +1047,8 @@ ac_status ac_exact_count_device(ac_ctx* ctx, uint32_t k, const ac_windows* dev, 
     // overflow u32 @44, n_keys u64 @48, hist[EXACT_HIST_BINS] u32 @64
     const size_t small_bytes = 64 + sizeof(uint32_t) * EXACT_HIST_BINS;
     std::vector<uint64_t> fb(forbidden, forbidden + n_forbidden);
+    std::vector<uint64_t> fbb;  // (the partitioned path: fb by bucket, and the bucket starts; host copies
+    std::vector<uint32_t> fst;  // live until the call's syncs)
     std::sort(fb.begin(), fb.end());
     fb.erase(std::unique(fb.begin(), fb.end()), fb.end());
     if (ac_status s2 = grow(ctx, &ctx->e_buf[1], &ctx->e_cap[1], (sizeof(uint64_t) + sizeof(uint32_t)) * list_cap))
@@ -1115,6 +1118,25 @@ ac_status ac_exact_count_device(ac_ctx* ctx, uint32_t k, const ac_windows* dev, 
         a.stot = a.h2 + h2;
         a.slab = a.stot + S;
         a.bstart = (uint32_t*)ctx->e_buf[10];
+        if (!fb.empty()) {  // the forbidden set by bucket: the count kernel searches only its bucket's entries
+            std::vector<std::pair<uint32_t, uint64_t>> byb(fb.size());
+            for (size_t i = 0; i < fb.size(); ++i)
+                byb[i] = {compact ? acamd::bucket_of((uint32_t)fb[i], nb_log2) : acamd::bucket_of(fb[i], nb_log2), fb[i]};
+            std::sort(byb.begin(), byb.end());
+            fbb.assign(fb.size(), 0);
+            fst.assign(NB + 1, 0);
+            for (size_t i = 0; i < byb.size(); ++i) {
+                fbb[i] = byb[i].second;
+                ++fst[byb[i].first + 1];
+            }
+            for (size_t b = 0; b < NB; ++b) fst[b + 1] += fst[b];
+            if (ac_status s2 = grow(ctx, &ctx->e_buf[12], &ctx->e_cap[12], sizeof(uint64_t) * fbb.size())) return s2;
+            if (ac_status s2 = grow(ctx, &ctx->e_buf[13], &ctx->e_cap[13], sizeof(uint32_t) * (NB + 1))) return s2;
+            AC_HIP(ctx, hipMemcpyAsync(ctx->e_buf[12], fbb.data(), sizeof(uint64_t) * fbb.size(), hipMemcpyHostToDevice, st));
+            AC_HIP(ctx, hipMemcpyAsync(ctx->e_buf[13], fst.data(), sizeof(uint32_t) * (NB + 1), hipMemcpyHostToDevice, st));
+            a.fb_bucketed = (const uint64_t*)ctx->e_buf[12];
+            a.fb_start = (const uint32_t*)ctx->e_buf[13];
+        }
         AC_HIP(ctx, hipMemsetAsync(small, 0, small_bytes, st));
         AC_HIP(ctx, acamd::launch_exact_partitioned(a, st));
         AC_HIP(ctx, hipMemcpyAsync(h_small.data(), small, small_bytes, hipMemcpyDeviceToHost, st));

@@ -51,6 +51,10 @@ struct ExactArgs {
     float lc_threshold;
     const uint64_t* forbidden;  // sorted
     uint32_t n_forbidden;
+    // partitioned path: the forbidden k-mers sorted by (bucket, k-mer), bucket b's at
+    // [fb_start[b], fb_start[b + 1]) (NULL when the set is empty)
+    const uint64_t* fb_bucketed;
+    const uint32_t* fb_start;
     // scan: count histogram of the kept entries, and the kept entries with
     // count >= EXACT_LIST_MIN compacted into list_keys/list_cnts
     uint32_t* hist;  // EXACT_HIST_BINS
@@ -116,5 +120,25 @@ hipError_t launch_exact_partitioned(const ExactArgs& a, hipStream_t stream);
 // one chunk staged in 32 KB of LDS; 16,384 gave 2 scatter workgroups per CU, level-2 scatter 37 us).
 uint32_t exact_part_chunk(uint32_t k);
 hipError_t launch_exact_part_count(const ExactArgs& a, hipStream_t stream);
+
+// Hash of a key for the partition (its top bits pick the bucket) and the per-bucket LDS table (its
+// low bits pick the slot): a 32-bit mixer (two u32 multiplies; the 64-bit murmur finaliser costs ~8
+// quarter-rate multiplies and the partition hashes every key five times); 64-bit keys fold their
+// high half in.  Host and device: the host sorts the forbidden set by bucket with it.
+__host__ __device__ inline uint32_t part_hash(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+__host__ __device__ inline uint32_t part_hash(uint64_t x) {
+    return part_hash((uint32_t)x ^ part_hash((uint32_t)(x >> 32) + 0x9e3779b9u));
+}
+template <class K>
+__host__ __device__ inline uint32_t bucket_of(K key, uint32_t nb_log2) {
+    return part_hash(key) >> (32u - nb_log2);
+}
 
 }  // namespace acamd

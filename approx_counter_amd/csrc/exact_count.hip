@@ -237,6 +237,19 @@ __device__ __forceinline__ float complexity16(uint32_t kmer, uint32_t k) {
     return (float)sum / (float)(2 * ((int)k - 2));
 }
 
+// The forbidden k-mers of one bucket (the host's per-bucket ranges, ExactArgs::fb_start): a binary
+// search over the bucket's few entries, none at all for the many buckets without one.
+__device__ __forceinline__ bool forbidden_in(const uint64_t* fb, uint32_t lo, uint32_t hi, uint64_t key) {
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        const uint64_t v = fb[mid];
+        if (v == key) return true;
+        if (v < key) lo = mid + 1;
+        else hi = mid;
+    }
+    return false;
+}
+
 __device__ __forceinline__ bool is_forbidden(const ExactArgs& a, uint64_t key) {
     uint32_t lo = 0, hi = a.n_forbidden;
     while (lo < hi) {
@@ -489,26 +502,7 @@ struct PartKey {
     static constexpr uint32_t CHUNK = (uint32_t)(32768 / sizeof(K));
 };
 
-// Hash of a key for the partition (its top bits pick the bucket) and the
-// per-bucket LDS table (its low bits pick the slot): a 32-bit mixer (two u32
-// multiplies; the 64-bit murmur finaliser costs ~8 quarter-rate multiplies and
-// the partition hashes every key five times); 64-bit keys fold their high half in.
-__device__ __forceinline__ uint32_t part_hash(uint32_t x) {
-    x ^= x >> 16;
-    x *= 0x7feb352du;
-    x ^= x >> 15;
-    x *= 0x846ca68bu;
-    x ^= x >> 16;
-    return x;
-}
-__device__ __forceinline__ uint32_t part_hash(uint64_t x) {
-    return part_hash((uint32_t)x ^ part_hash((uint32_t)(x >> 32) + 0x9e3779b9u));
-}
-
-template <class K>
-__device__ __forceinline__ uint32_t bucket_of(K key, uint32_t nb_log2) {
-    return part_hash(key) >> (32u - nb_log2);
-}
+// (part_hash and bucket_of: exact_count.h, shared with the host, which sorts the forbidden set by bucket)
 
 // Exclusive prefix of a block's values (thread t of NT holds x); returns the total.
 template <uint32_t NT = EXACT_THREADS>
@@ -1060,6 +1054,7 @@ __global__ __launch_bounds__(COUNT_THREADS) void part_count_kernel(ExactArgs a) 
         for (uint32_t i = t; i < EXACT_PHIST; i += COUNT_THREADS) hist[i] = 0;
         __syncthreads();
         const uint32_t lo = a.bstart[b], hi = a.bstart[b + 1];
+        const uint32_t f0 = a.fb_start ? a.fb_start[b] : 0u, f1 = a.fb_start ? a.fb_start[b + 1] : 0u;
         uint32_t allt = 0;
         for (uint32_t i0 = lo; i0 < hi; i0 += COUNT_THREADS * COUNT_BATCH) {  // block-uniform batches
             K kb[COUNT_BATCH];
@@ -1128,7 +1123,7 @@ __global__ __launch_bounds__(COUNT_THREADS) void part_count_kernel(ExactArgs a) 
                 tk[s] = 0;  // cleared for the next bucket
                 tc[s] = 0;
                 if (key_complexity(kk, a.k) >= a.lc_threshold) c = 0;  // haveLowComplexity (214-234)
-                else if (is_forbidden(a, key)) c = 0;                  // isForbiddenKmer (330-332)
+                else if (f1 > f0 && forbidden_in(a.fb_bucketed, f0, f1, key)) c = 0;  // isForbiddenKmer (330-332)
             }
             if (!a.emit_only && c) {
                 if (c == 1u) ++ones;

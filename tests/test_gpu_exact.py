@@ -64,6 +64,26 @@ def test_forbidden_solid_and_limits(counter):
     check(counter, wins, 16, 1.0, solid=10**6)  # nothing that solid
 
 
+@pytest.mark.parametrize("k", [11, 16, 22])
+def test_forbidden_by_bucket(counter, k):
+    """The partitioned count kernel searches only its bucket's forbidden k-mers (the host sorts the set
+    by bucket): many forbidden k-mers, the sample's most frequent among them, duplicates and k-mers
+    absent from the sample, against the host restatement (isForbiddenKmer, approx_counter.cpp:330-332)."""
+    import random
+
+    from tools.synth import make_reads
+
+    reads, _ = make_reads(1500, read_len=220, seed=11)
+    wins = host_ref.sample_all([r.decode() for r in reads], 100, False)
+    thr = float(host_ref.adjust_threshold(1.0, 16, k))
+    top, _, _ = expected(wins, k, thr, limit=200)
+    rnd = random.Random(k)
+    forbidden = {km for i, (km, _) in enumerate(top) if i % 3 == 0}
+    forbidden |= {rnd.randrange(1 << (2 * k)) for _ in range(500)}
+    check(counter, wins, k, thr, forbidden, limit=150)
+    check(counter, wins, k, thr, forbidden | {top[1][0]}, limit=10**6)
+
+
 @pytest.mark.parametrize("k", [16, 22])
 def test_overlapping_windows_more_positions_than_bases(counter, k):
     """ac_windows allows overlapping windows: here every window starts at image base 0,
