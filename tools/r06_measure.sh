@@ -260,6 +260,12 @@ xhost)  # exact count's host side: HIP API + kernel + copy trace of cfg3 / cfg4 
   export TMPDIR=/tmp
   run xhost_cfg3 200 rocprofv3 --hip-trace --kernel-trace --memory-copy-trace -d "$OUT/xhost_cfg3" -o run -- python3 tools/bench_exact.py --fast --reads 100000 --lim 2000 --steps 5 --warmup 2 --no-host
   run xhost_cfg4 200 rocprofv3 --hip-trace --kernel-trace --memory-copy-trace -d "$OUT/xhost_cfg4" -o run -- python3 tools/bench_exact.py --fast --reads 1000000 --lim 500 --steps 5 --warmup 2 --no-host ;;
+fbb)  # exact count with a forbidden set searched per bucket (the in-tree library): tests, cfg4 / cfg5 with 0 / 1,000
+  run tests_fbb 600 $PYT -m gpu tests/test_gpu_exact.py tests/test_gpu_cli.py
+  for rep in 1 2; do for nf in 0 1000; do
+    run xfb_cfg4_f${nf}_$rep 120 python3 tools/bench_exact.py --fast --reads 1000000 --lim 500 --steps 10 --no-host --forbidden $nf
+    run xfb_cfg5_f${nf}_$rep 120 python3 tools/bench_exact.py --fast --reads 100000 --sl 150 --k 22 --lim 1000 --steps 10 --no-host --forbidden $nf
+  done; done ;;
 *) echo "unknown part $part" ;;
 esac
 done
