@@ -258,8 +258,11 @@ fbfab)  # exact count with a forbidden set: LDS filter before the binary search 
   done; done ;;
 xhost)  # exact count's host side: HIP API + kernel + copy trace of cfg3 / cfg4 calls (where the non-kernel time goes)
   export TMPDIR=/tmp
-  run xhost_cfg3 200 rocprofv3 --hip-trace --kernel-trace --memory-copy-trace -d "$OUT/xhost_cfg3" -o run -- python3 tools/bench_exact.py --fast --reads 100000 --lim 2000 --steps 5 --warmup 2 --no-host
-  run xhost_cfg4 200 rocprofv3 --hip-trace --kernel-trace --memory-copy-trace -d "$OUT/xhost_cfg4" -o run -- python3 tools/bench_exact.py --fast --reads 1000000 --lim 500 --steps 5 --warmup 2 --no-host ;;
+  for c in "cfg3 100000 2000" "cfg4 1000000 500"; do
+    set -- $c
+    run xhost_$1 200 rocprofv3 --hip-trace --kernel-trace --memory-copy-trace -d "/tmp/xhost_$1" -o run -- python3 tools/bench_exact.py --fast --reads $2 --lim $3 --steps 4 --warmup 2 --no-host
+    python3 tools/host_gaps.py "/tmp/xhost_$1" > "$OUT/xhost_$1_timeline.txt" 2>&1; rm -rf "/tmp/xhost_$1"
+  done ;;
 fbb)  # exact count with a forbidden set searched per bucket (the in-tree library): tests, cfg4 / cfg5 with 0 / 1,000
   run tests_fbb 600 $PYT -m gpu tests/test_gpu_exact.py tests/test_gpu_cli.py
   for rep in 1 2; do for nf in 0 1000; do
