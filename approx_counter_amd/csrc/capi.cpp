@@ -67,6 +67,10 @@ struct ac_ctx {
     // set by bucket and its bucket starts: e_buf[12..13])
     void* e_buf[14] = {};
     size_t e_cap[14] = {};
+    // the exact count's readbacks (the small block, the list count, the gathered entries): pinned, so each
+    // is one DMA into place instead of a copy through HIP's staging buffer (grown as needed, 16 MB at most)
+    char* e_pin = nullptr;
+    size_t e_pin_cap = 0;
     // Count-kernel scratch, one set per stream a launch may run on at the same
     // time as another: the parts of a synchronous jobs call (0 .. MAX_PARTS-1),
     // the parts of a submit (MAX_PARTS ..), so a synchronous call never shares
@@ -722,6 +726,7 @@ void ac_destroy(ac_ctx* ctx) {
         if (p) (void)hipFree(p);
     for (void* p : ctx->e_buf)
         if (p) (void)hipFree(p);
+    if (ctx->e_pin) (void)hipHostFree(ctx->e_pin);
     if (ctx->d_err) (void)hipFree(ctx->d_err);
     if (ctx->h_err) (void)hipHostFree(ctx->h_err);
     for (auto& sl : ctx->slot) {
@@ -1084,7 +1089,15 @@ ac_status ac_exact_count_device(ac_ctx* ctx, uint32_t k, const ac_windows* dev, 
     a.forbidden = (const uint64_t*)ctx->e_buf[3];
     a.n_forbidden = (uint32_t)fb.size();
     a.list_min = EXACT_LIST_MIN;
-    std::vector<char> h_small(small_bytes);
+    // readbacks into the context's pinned block: [0, 32 KB) the small block and the list / gather counts,
+    // then the gathered entries when they fit (else pageable vectors)
+    constexpr size_t PIN_HEAD = 32768, PIN_MAX = size_t(16) << 20;
+    static_assert(64 + sizeof(uint32_t) * EXACT_HIST_BINS + 16 <= PIN_HEAD, "small block fits the pinned head");
+    if (!ctx->e_pin) {
+        AC_HIP(ctx, hipHostMalloc((void**)&ctx->e_pin, PIN_HEAD, hipHostMallocDefault));
+        ctx->e_pin_cap = PIN_HEAD;
+    }
+    char* h_small = ctx->e_pin;
     if (partitioned) {
         // buckets: about 1,024-2,048 keys each (the LDS table holds 4,096)
 #ifndef AC_BUCKET_KEYS
@@ -1139,13 +1152,13 @@ ac_status ac_exact_count_device(ac_ctx* ctx, uint32_t k, const ac_windows* dev, 
         }
         AC_HIP(ctx, hipMemsetAsync(small, 0, small_bytes, st));
         AC_HIP(ctx, acamd::launch_exact_partitioned(a, st));
-        AC_HIP(ctx, hipMemcpyAsync(h_small.data(), small, small_bytes, hipMemcpyDeviceToHost, st));
+        AC_HIP(ctx, hipMemcpyAsync(h_small, small, small_bytes, hipMemcpyDeviceToHost, st));
         AC_HIP(ctx, hipStreamSynchronize(st));
-        if (*(const uint32_t*)(h_small.data() + 44)) partitioned = false;  // a bucket overflowed its LDS table
+        if (*(const uint32_t*)(h_small + 44)) partitioned = false;  // a bucket overflowed its LDS table
         // Overlapping windows (allowed by ac_windows) hold more k-mer positions than the image
         // has bases: the dense key arrays dropped the excess, so count on the hash table instead
         // (its distinct keys are still bounded by the image's positions).
-        if (*(const unsigned long long*)(h_small.data() + 48) > key_cap) partitioned = false;
+        if (*(const unsigned long long*)(h_small + 48) > key_cap) partitioned = false;
     }
     if (!partitioned) {
         // Table: a power of two >= 1.5 x the image size (an upper bound on k-mer
@@ -1164,17 +1177,17 @@ ac_status ac_exact_count_device(ac_ctx* ctx, uint32_t k, const ac_windows* dev, 
         AC_HIP(ctx, hipMemsetAsync(small, 0, small_bytes, st));
         AC_HIP(ctx, acamd::launch_exact_insert(a, st));
         AC_HIP(ctx, acamd::launch_exact_scan(a, st));
-        AC_HIP(ctx, hipMemcpyAsync(h_small.data(), small, small_bytes, hipMemcpyDeviceToHost, st));
+        AC_HIP(ctx, hipMemcpyAsync(h_small, small, small_bytes, hipMemcpyDeviceToHost, st));
         AC_HIP(ctx, hipStreamSynchronize(st));
     }
-    if (ac_status rc = device_error(ctx, *(const uint32_t*)(h_small.data() + 40))) return rc;
+    if (ac_status rc = device_error(ctx, *(const uint32_t*)(h_small + 40))) return rc;
     ctx->exact_path = partitioned ? 1 : 0;
-    const uint32_t* hist = (const uint32_t*)(h_small.data() + 64);
+    const uint32_t* hist = (const uint32_t*)(h_small + 64);
     uint64_t kept = 0;
     for (int i = 0; i < EXACT_HIST_BINS; ++i) kept += hist[i];
     if (n_distinct) *n_distinct = kept;
-    if (had_n) *had_n = *(const unsigned long long*)(h_small.data() + 16);
-    uint64_t n_list = *(const unsigned long long*)(h_small.data() + 32);
+    if (had_n) *had_n = *(const unsigned long long*)(h_small + 16);
+    uint64_t n_list = *(const unsigned long long*)(h_small + 32);
     if (n_list > list_cap) return fail(ctx, AC_ERR_INTERNAL, "exact count: candidate list overflow");
     // Threshold: solid mode keeps count >= solid; otherwise the largest count c
     // such that at least `limit` kept entries have count >= c (all if fewer).
@@ -1201,10 +1214,10 @@ ac_status ac_exact_count_device(ac_ctx* ctx, uint32_t k, const ac_windows* dev, 
         a.emit_only = 1;
         AC_HIP(ctx, hipMemsetAsync(a.n_list, 0, sizeof(unsigned long long), st));
         AC_HIP(ctx, acamd::launch_exact_part_count(a, st));
-        unsigned long long nl = 0;
-        AC_HIP(ctx, hipMemcpyAsync(&nl, a.n_list, sizeof nl, hipMemcpyDeviceToHost, st));
+        unsigned long long* nl = (unsigned long long*)(ctx->e_pin + PIN_HEAD - 16);
+        AC_HIP(ctx, hipMemcpyAsync(nl, a.n_list, sizeof *nl, hipMemcpyDeviceToHost, st));
         AC_HIP(ctx, hipStreamSynchronize(st));
-        n_list = nl;
+        n_list = *nl;
         if (n_list > list_cap) return fail(ctx, AC_ERR_INTERNAL, "exact count: candidate list overflow");
         from_list = true;
     }
@@ -1217,16 +1230,44 @@ ac_status ac_exact_count_device(ac_ctx* ctx, uint32_t k, const ac_windows* dev, 
     a.out_cnts = (uint32_t*)ctx->e_buf[5];
     a.out_cap = gather_cap;
     AC_HIP(ctx, acamd::launch_exact_gather(a, from_list, n_list, st));
-    unsigned long long got = 0;
-    AC_HIP(ctx, hipMemcpyAsync(&got, a.n_out, sizeof got, hipMemcpyDeviceToHost, st));
+    // The gathered count is at most gather_cap (the histogram's due entries): with room in the pinned
+    // block, the count and gather_cap entries come back in one synchronised batch of DMAs (the extra
+    // entries, if any, are ignored); otherwise the count first, then exactly that many entries.
+    unsigned long long* got_p = (unsigned long long*)(ctx->e_pin + PIN_HEAD - 8);
+    const size_t entry_bytes = (sizeof(uint64_t) + sizeof(uint32_t)) * gather_cap;
+    const bool pin_entries = entry_bytes <= PIN_MAX;
+    if (pin_entries && PIN_HEAD + entry_bytes > ctx->e_pin_cap) {
+        AC_HIP(ctx, hipStreamSynchronize(st));  // (the head's readbacks are done with; the block moves)
+        char* old = ctx->e_pin;
+        char* grown = nullptr;
+        const size_t cap = std::min(PIN_MAX + PIN_HEAD, std::max(2 * ctx->e_pin_cap, PIN_HEAD + entry_bytes));
+        AC_HIP(ctx, hipHostMalloc((void**)&grown, cap, hipHostMallocDefault));
+        std::memcpy(grown, old, PIN_HEAD);
+        (void)hipHostFree(old);
+        ctx->e_pin = grown;
+        ctx->e_pin_cap = cap;
+        got_p = (unsigned long long*)(ctx->e_pin + PIN_HEAD - 8);
+    }
+    uint64_t* gk_p = (uint64_t*)(ctx->e_pin + PIN_HEAD);
+    uint32_t* gc_p = (uint32_t*)(ctx->e_pin + PIN_HEAD + sizeof(uint64_t) * gather_cap);
+    std::vector<uint64_t> gk;
+    std::vector<uint32_t> gc;
+    AC_HIP(ctx, hipMemcpyAsync(got_p, a.n_out, sizeof *got_p, hipMemcpyDeviceToHost, st));
+    if (pin_entries) {
+        AC_HIP(ctx, hipMemcpyAsync(gk_p, a.out_keys, sizeof(uint64_t) * gather_cap, hipMemcpyDeviceToHost, st));
+        AC_HIP(ctx, hipMemcpyAsync(gc_p, a.out_cnts, sizeof(uint32_t) * gather_cap, hipMemcpyDeviceToHost, st));
+    }
     AC_HIP(ctx, hipStreamSynchronize(st));
+    const unsigned long long got = *got_p;
     if (got > gather_cap) return fail(ctx, AC_ERR_INTERNAL, "exact count: gathered more entries than the histogram");
-    std::vector<uint64_t> gk(got);
-    std::vector<uint32_t> gc(got);
-    if (got) {
+    if (!pin_entries && got) {
+        gk.resize(got);
+        gc.resize(got);
         AC_HIP(ctx, hipMemcpyAsync(gk.data(), a.out_keys, sizeof(uint64_t) * got, hipMemcpyDeviceToHost, st));
         AC_HIP(ctx, hipMemcpyAsync(gc.data(), a.out_cnts, sizeof(uint32_t) * got, hipMemcpyDeviceToHost, st));
         AC_HIP(ctx, hipStreamSynchronize(st));
+        gk_p = gk.data();
+        gc_p = gc.data();
     }
     struct Entry {
         uint64_t count, kmer;
@@ -1235,7 +1276,7 @@ ac_status ac_exact_count_device(ac_ctx* ctx, uint32_t k, const ac_windows* dev, 
     std::vector<Entry> v;
     v.reserve(got);
     for (uint64_t i = 0; i < got; ++i)
-        if (!solid || gc[i] >= solid) v.push_back({gc[i], gk[i], complexity(gk[i], k)});
+        if (!solid || gc_p[i] >= solid) v.push_back({gc_p[i], gk_p[i], complexity(gk_p[i], k)});
     auto less = [](const Entry& x, const Entry& y) {  // CompareCount: a strict total order
         if (x.count != y.count) return x.count > y.count;
         if (x.comp != y.comp) return x.comp < y.comp;
