@@ -269,6 +269,16 @@ fbb)  # exact count with a forbidden set searched per bucket (the in-tree librar
     run xfb_cfg4_f${nf}_$rep 120 python3 tools/bench_exact.py --fast --reads 1000000 --lim 500 --steps 10 --no-host --forbidden $nf
     run xfb_cfg5_f${nf}_$rep 120 python3 tools/bench_exact.py --fast --reads 100000 --sl 150 --k 22 --lim 1000 --steps 10 --no-host --forbidden $nf
   done; done ;;
+xcomp)  # exact count with pinned readbacks and device-side DUST scores for the ranking (in-tree library)
+  run tests_xcomp 600 $PYT -m gpu tests/test_gpu_exact.py tests/test_gpu_cli.py
+  for rep in 1 2; do
+    run xc_cfg3_$rep 120 python3 tools/bench_exact.py --fast --reads 100000 --lim 2000 --steps 10
+    run xc_cfg4_$rep 120 python3 tools/bench_exact.py --fast --reads 1000000 --lim 500 --steps 10 --no-host
+    run xc_cfg5_$rep 120 python3 tools/bench_exact.py --fast --reads 100000 --sl 150 --k 22 --lim 1000 --steps 10
+  done
+  export TMPDIR=/tmp
+  run xhost_cfg3 200 rocprofv3 --hip-trace --kernel-trace --memory-copy-trace -d "/tmp/xhost_cfg3" -o run -- python3 tools/bench_exact.py --fast --reads 100000 --lim 2000 --steps 4 --warmup 2 --no-host
+  python3 tools/host_gaps.py "/tmp/xhost_cfg3" > "$OUT/xhost_cfg3_timeline.txt" 2>&1; rm -rf "/tmp/xhost_cfg3" ;;
 *) echo "unknown part $part" ;;
 esac
 done
