@@ -218,6 +218,19 @@ ac_status h2d_staged(ac_ctx* ctx, int n, const void* const* src, const size_t* s
     return AC_OK;
 }
 
+// getComplexity (approx_counter.cpp:247-267) and CompareCount (275-305), for the
+// final ranking of the exact count's short list.
+float complexity(uint64_t kmer, uint32_t k) {
+    uint64_t counts[16] = {0};
+    for (uint32_t i = 0; i + 1 < k; ++i) {
+        counts[kmer & 15u]++;
+        kmer >>= 2;
+    }
+    size_t sum = 0;
+    for (uint64_t v : counts) sum += v * (v - 1);
+    return (float)sum / float(2 * ((int)k - 2));
+}
+
 ac_status check_sample(ac_ctx* ctx, const ac_windows* s) {
     if (!s) return fail(ctx, AC_ERR_INVALID, "sample is NULL");
     if (s->n_bases % 32 || s->n_bases >= AC_MAX_IMAGE_BASES)
@@ -1211,20 +1224,17 @@ ac_status ac_exact_count_device(ac_ctx* ctx, uint32_t k, const ac_windows* dev, 
     // (a solid threshold past the last bin is applied exactly on the gathered list)
     const uint64_t gather_cap = std::max<uint64_t>(1, due);
     if (ac_status s2 = grow(ctx, &ctx->e_buf[4], &ctx->e_cap[4], sizeof(uint64_t) * gather_cap)) return s2;
-    if (ac_status s2 = grow(ctx, &ctx->e_buf[5], &ctx->e_cap[5], (sizeof(uint32_t) + sizeof(float)) * gather_cap))
-        return s2;
+    if (ac_status s2 = grow(ctx, &ctx->e_buf[5], &ctx->e_cap[5], sizeof(uint32_t) * gather_cap)) return s2;
     a.threshold = (uint32_t)std::min<uint64_t>(thr, 0xffffffffu);
     a.out_keys = (uint64_t*)ctx->e_buf[4];
     a.out_cnts = (uint32_t*)ctx->e_buf[5];
-    a.out_comp = (float*)((uint32_t*)ctx->e_buf[5] + gather_cap);
     a.out_cap = gather_cap;
     AC_HIP(ctx, acamd::launch_exact_gather(a, from_list, n_list, st));
-    AC_HIP(ctx, acamd::launch_exact_comp(a, gather_cap, st));
     // The gathered count is at most gather_cap (the histogram's due entries): with room in the pinned
     // block, the count and gather_cap entries come back in one synchronised batch of DMAs (the extra
     // entries, if any, are ignored); otherwise the count first, then exactly that many entries.
     unsigned long long* got_p = (unsigned long long*)(ctx->e_pin + PIN_HEAD - 8);
-    const size_t entry_bytes = (sizeof(uint64_t) + sizeof(uint32_t) + sizeof(float)) * gather_cap;
+    const size_t entry_bytes = (sizeof(uint64_t) + sizeof(uint32_t)) * gather_cap;
     const bool pin_entries = entry_bytes <= PIN_MAX;
     if (pin_entries && PIN_HEAD + entry_bytes > ctx->e_pin_cap) {
         AC_HIP(ctx, hipStreamSynchronize(st));  // (the head's readbacks are done with; the block moves)
@@ -1240,15 +1250,12 @@ ac_status ac_exact_count_device(ac_ctx* ctx, uint32_t k, const ac_windows* dev, 
     }
     uint64_t* gk_p = (uint64_t*)(ctx->e_pin + PIN_HEAD);
     uint32_t* gc_p = (uint32_t*)(ctx->e_pin + PIN_HEAD + sizeof(uint64_t) * gather_cap);
-    float* gs_p = (float*)(gc_p + gather_cap);
     std::vector<uint64_t> gk;
     std::vector<uint32_t> gc;
-    std::vector<float> gs;
     AC_HIP(ctx, hipMemcpyAsync(got_p, a.n_out, sizeof *got_p, hipMemcpyDeviceToHost, st));
     if (pin_entries) {
         AC_HIP(ctx, hipMemcpyAsync(gk_p, a.out_keys, sizeof(uint64_t) * gather_cap, hipMemcpyDeviceToHost, st));
         AC_HIP(ctx, hipMemcpyAsync(gc_p, a.out_cnts, sizeof(uint32_t) * gather_cap, hipMemcpyDeviceToHost, st));
-        AC_HIP(ctx, hipMemcpyAsync(gs_p, a.out_comp, sizeof(float) * gather_cap, hipMemcpyDeviceToHost, st));
     }
     AC_HIP(ctx, hipStreamSynchronize(st));
     const unsigned long long got = *got_p;
@@ -1256,14 +1263,11 @@ ac_status ac_exact_count_device(ac_ctx* ctx, uint32_t k, const ac_windows* dev, 
     if (!pin_entries && got) {
         gk.resize(got);
         gc.resize(got);
-        gs.resize(got);
         AC_HIP(ctx, hipMemcpyAsync(gk.data(), a.out_keys, sizeof(uint64_t) * got, hipMemcpyDeviceToHost, st));
         AC_HIP(ctx, hipMemcpyAsync(gc.data(), a.out_cnts, sizeof(uint32_t) * got, hipMemcpyDeviceToHost, st));
-        AC_HIP(ctx, hipMemcpyAsync(gs.data(), a.out_comp, sizeof(float) * got, hipMemcpyDeviceToHost, st));
         AC_HIP(ctx, hipStreamSynchronize(st));
         gk_p = gk.data();
         gc_p = gc.data();
-        gs_p = gs.data();
     }
     struct Entry {
         uint64_t count, kmer;
@@ -1272,7 +1276,7 @@ ac_status ac_exact_count_device(ac_ctx* ctx, uint32_t k, const ac_windows* dev, 
     std::vector<Entry> v;
     v.reserve(got);
     for (uint64_t i = 0; i < got; ++i)
-        if (!solid || gc_p[i] >= solid) v.push_back({gc_p[i], gk_p[i], gs_p[i]});  // (scored on the device)
+        if (!solid || gc_p[i] >= solid) v.push_back({gc_p[i], gk_p[i], complexity(gk_p[i], k)});
     auto less = [](const Entry& x, const Entry& y) {  // CompareCount: a strict total order
         if (x.count != y.count) return x.count > y.count;
         if (x.comp != y.comp) return x.comp < y.comp;

@@ -67,7 +67,6 @@ struct ExactArgs {
     uint32_t threshold;
     uint64_t* out_keys;
     uint32_t* out_cnts;
-    float* out_comp;  // the gathered entries' DUST scores (exact_comp_kernel), for the host's CompareCount
     unsigned long long* n_out;
     uint64_t out_cap;
     // Partitioned path: every k-mer position's key
@@ -113,8 +112,6 @@ hipError_t launch_exact_insert(const ExactArgs& a, hipStream_t stream);
 hipError_t launch_exact_scan(const ExactArgs& a, hipStream_t stream);
 // from_list: gather from the scan's compacted list of n_list entries, else from the table
 hipError_t launch_exact_gather(const ExactArgs& a, bool from_list, uint64_t n_list, hipStream_t stream);
-// The gathered entries' DUST scores (out_comp[i] for i < *n_out; `cap` = the host's bound on *n_out).
-hipError_t launch_exact_comp(const ExactArgs& a, uint64_t cap, hipStream_t stream);
 // Partitioned path (k <= 16): keys, bucket partition, per-bucket count (fills
 // hist / list / special like insert + scan).  `count_only` re-runs just the
 // per-bucket count (with a.list_min / a.emit_only) on the partition already built.

@@ -1262,22 +1262,6 @@ hipError_t launch_exact_scan(const ExactArgs& a, hipStream_t stream) {
     return hipGetLastError();
 }
 
-// DUST scores of the gathered entries (getComplexity, 247-267): the host's CompareCount ranks them
-// by (count, score, k-mer); scored here, the host computed one per gathered entry before (a few
-// thousand at cfg3: ~0.15 ms of a 0.52 ms call, profiles/r06_m26/xhost_cfg3_timeline.txt).
-__global__ __launch_bounds__(EXACT_THREADS) void exact_comp_kernel(ExactArgs a) {
-    const uint64_t n = min((unsigned long long)a.out_cap, *a.n_out);
-    for (uint64_t i = (uint64_t)blockIdx.x * EXACT_THREADS + threadIdx.x; i < n; i += (uint64_t)gridDim.x * EXACT_THREADS)
-        a.out_comp[i] = a.compact ? complexity16((uint32_t)a.out_keys[i], a.k) : complexity(a.out_keys[i], a.k);
-}
-
-hipError_t launch_exact_comp(const ExactArgs& a, uint64_t cap, hipStream_t stream) {
-    if (!cap) return hipSuccess;
-    const uint32_t blocks = (uint32_t)std::min<uint64_t>(1024, (cap + EXACT_THREADS - 1) / EXACT_THREADS);
-    hipLaunchKernelGGL(exact_comp_kernel, dim3(blocks), dim3(EXACT_THREADS), 0, stream, a);
-    return hipGetLastError();
-}
-
 hipError_t launch_exact_gather(const ExactArgs& a, bool from_list, uint64_t n_list, hipStream_t stream) {
     if (from_list) {
         if (!n_list) return hipSuccess;
