@@ -68,7 +68,7 @@ struct ac_ctx {
     void* e_buf[14] = {};
     size_t e_cap[14] = {};
     // the exact count's readbacks (the small block, the list count, the gathered entries): pinned, so each
-    // is one DMA into place instead of a copy through HIP's staging buffer (grown as needed, 16 MB at most)
+    // is one DMA into place instead of a copy through HIP's staging buffer (32 KB + 16 MB, at the first call)
     char* e_pin = nullptr;
     size_t e_pin_cap = 0;
     // Count-kernel scratch, one set per stream a launch may run on at the same
@@ -1093,9 +1093,9 @@ ac_status ac_exact_count_device(ac_ctx* ctx, uint32_t k, const ac_windows* dev, 
     // then the gathered entries when they fit (else pageable vectors)
     constexpr size_t PIN_HEAD = 32768, PIN_MAX = size_t(16) << 20;
     static_assert(64 + sizeof(uint32_t) * EXACT_HIST_BINS + 16 <= PIN_HEAD, "small block fits the pinned head");
-    if (!ctx->e_pin) {
-        AC_HIP(ctx, hipHostMalloc((void**)&ctx->e_pin, PIN_HEAD, hipHostMallocDefault));
-        ctx->e_pin_cap = PIN_HEAD;
+    if (!ctx->e_pin) {  // (allocated once at its full size: no pinned block freed or moved while a call runs)
+        AC_HIP(ctx, hipHostMalloc((void**)&ctx->e_pin, PIN_HEAD + PIN_MAX, hipHostMallocDefault));
+        ctx->e_pin_cap = PIN_HEAD + PIN_MAX;
     }
     char* h_small = ctx->e_pin;
     if (partitioned) {
@@ -1236,18 +1236,6 @@ ac_status ac_exact_count_device(ac_ctx* ctx, uint32_t k, const ac_windows* dev, 
     unsigned long long* got_p = (unsigned long long*)(ctx->e_pin + PIN_HEAD - 8);
     const size_t entry_bytes = (sizeof(uint64_t) + sizeof(uint32_t)) * gather_cap;
     const bool pin_entries = entry_bytes <= PIN_MAX;
-    if (pin_entries && PIN_HEAD + entry_bytes > ctx->e_pin_cap) {
-        AC_HIP(ctx, hipStreamSynchronize(st));  // (the head's readbacks are done with; the block moves)
-        char* old = ctx->e_pin;
-        char* grown = nullptr;
-        const size_t cap = std::min(PIN_MAX + PIN_HEAD, std::max(2 * ctx->e_pin_cap, PIN_HEAD + entry_bytes));
-        AC_HIP(ctx, hipHostMalloc((void**)&grown, cap, hipHostMallocDefault));
-        std::memcpy(grown, old, PIN_HEAD);
-        (void)hipHostFree(old);
-        ctx->e_pin = grown;
-        ctx->e_pin_cap = cap;
-        got_p = (unsigned long long*)(ctx->e_pin + PIN_HEAD - 8);
-    }
     uint64_t* gk_p = (uint64_t*)(ctx->e_pin + PIN_HEAD);
     uint32_t* gc_p = (uint32_t*)(ctx->e_pin + PIN_HEAD + sizeof(uint64_t) * gather_cap);
     std::vector<uint64_t> gk;
