@@ -1257,23 +1257,52 @@ ac_status ac_exact_count_device(ac_ctx* ctx, uint32_t k, const ac_windows* dev, 
         gk_p = gk.data();
         gc_p = gc.data();
     }
+    // CompareCount (275-305): count descending, DUST score ascending, k-mer descending.  For k > 2 the
+    // score is a non-negative float, so its bits order like it and the whole order is one 128-bit key
+    // ((~count, score bits), ~k-mer) compared as two integers; the first n by nth_element, then sorted
+    // (partial_sort with the three-field comparator was most of a cfg3 call's host time).  k = 2 (a
+    // score of 0 / 0) keeps the comparator, whose NaN ties are the reference's.
+    const size_t n_all = solid ? (size_t)std::count_if(gc_p, gc_p + got, [&](uint32_t c) { return c >= solid; })
+                               : (size_t)got;
+    const size_t n = solid ? n_all : std::min<size_t>(n_all, limit);
+    *n_out = n;
+    if (n > capacity) return fail(ctx, AC_ERR_INVALID, "exact count: capacity too small (n_out holds the size needed)");
+    if (k > 2) {
+        struct Key {
+            uint64_t hi, lo;
+        };
+        std::vector<Key> w;
+        w.reserve(n_all);
+        for (uint64_t i = 0; i < got; ++i)
+            if (!solid || gc_p[i] >= solid) {
+                const float c = complexity(gk_p[i], k);
+                uint32_t cb;
+                std::memcpy(&cb, &c, sizeof cb);
+                w.push_back({((uint64_t)(0xffffffffu - gc_p[i]) << 32) | cb, ~gk_p[i]});
+            }
+        auto kl = [](const Key& x, const Key& y) { return x.hi < y.hi || (x.hi == y.hi && x.lo < y.lo); };
+        if (n < w.size()) std::nth_element(w.begin(), w.begin() + n, w.end(), kl);
+        std::sort(w.begin(), w.begin() + n, kl);
+        for (size_t i = 0; i < n; ++i) {
+            kmers_out[i] = ~w[i].lo;
+            counts_out[i] = 0xffffffffu - (uint32_t)(w[i].hi >> 32);
+        }
+        return AC_OK;
+    }
     struct Entry {
         uint64_t count, kmer;
         float comp;
     };
     std::vector<Entry> v;
-    v.reserve(got);
+    v.reserve(n_all);
     for (uint64_t i = 0; i < got; ++i)
         if (!solid || gc_p[i] >= solid) v.push_back({gc_p[i], gk_p[i], complexity(gk_p[i], k)});
-    auto less = [](const Entry& x, const Entry& y) {  // CompareCount: a strict total order
+    auto less = [](const Entry& x, const Entry& y) {
         if (x.count != y.count) return x.count > y.count;
         if (x.comp != y.comp) return x.comp < y.comp;
         return x.kmer > y.kmer;
     };
-    const size_t n = solid ? v.size() : std::min<size_t>(v.size(), limit);
     std::partial_sort(v.begin(), v.begin() + n, v.end(), less);
-    *n_out = n;
-    if (n > capacity) return fail(ctx, AC_ERR_INVALID, "exact count: capacity too small (n_out holds the size needed)");
     for (size_t i = 0; i < n; ++i) {
         kmers_out[i] = v[i].kmer;
         counts_out[i] = v[i].count;
