@@ -279,6 +279,13 @@ xcomp)  # exact count with pinned readbacks and device-side DUST scores for the 
   export TMPDIR=/tmp
   run xhost_cfg3 200 rocprofv3 --hip-trace --kernel-trace --memory-copy-trace -d "/tmp/xhost_cfg3" -o run -- python3 tools/bench_exact.py --fast --reads 100000 --lim 2000 --steps 4 --warmup 2 --no-host
   python3 tools/host_gaps.py "/tmp/xhost_cfg3" > "$OUT/xhost_cfg3_timeline.txt" 2>&1; rm -rf "/tmp/xhost_cfg3" ;;
+dbab)  # exact count: histogram / list count double-buffered by bucket parity, one barrier less per bucket (db) vs cur
+  run tests_db 600 env APPROX_COUNTER_AMD_LIB=build/var/db/libapprox_counter_amd.so $PYT -m gpu tests/test_gpu_exact.py
+  for rep in 1 2; do for v in cur db; do
+    run xdb_${v}_cfg4_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so python3 tools/bench_exact.py --fast --reads 1000000 --lim 500 --steps 10 --no-host
+    run xdb_${v}_cfg3_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so python3 tools/bench_exact.py --fast --reads 100000 --lim 2000 --steps 10 --no-host
+    run xdb_${v}_cfg5_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so python3 tools/bench_exact.py --fast --reads 100000 --sl 150 --k 22 --lim 1000 --steps 10 --no-host
+  done; done ;;
 *) echo "unknown part $part" ;;
 esac
 done
