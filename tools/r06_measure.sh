@@ -286,6 +286,8 @@ dbab)  # exact count: histogram / list count double-buffered by bucket parity, o
     run xdb_${v}_cfg3_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so python3 tools/bench_exact.py --fast --reads 100000 --lim 2000 --steps 10 --no-host
     run xdb_${v}_cfg5_$rep 120 env APPROX_COUNTER_AMD_LIB=build/var/$v/libapprox_counter_amd.so python3 tools/bench_exact.py --fast --reads 100000 --sl 150 --k 22 --lim 1000 --steps 10 --no-host
   done; done ;;
+rehearse)  # the N > 1 bench path end to end on one GPU: cfg2 weak (the driver's SCALE config), 1 / 2 / 4 gloo ranks
+  run rehearse_cfg2 900 bash tools/rehearse_ranks.sh "$OUT/rehearsal" cfg2 ;;
 *) echo "unknown part $part" ;;
 esac
 done
